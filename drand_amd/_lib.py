@@ -1,0 +1,122 @@
+"""ctypes binding of libdrand_gpu.so (the C-ABI in include/drand_gpu.h).
+
+The product path has no CPU fallback: if the library is missing or no gfx950
+GPU is available, opening a context raises DrandGPUError.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdrand_gpu.so")
+
+DGPU_OK = 0
+DGPU_EINVAL = -1
+DGPU_EDEVICE = -2
+DGPU_ENOMEM = -3
+DGPU_EUNSUPPORTED = -4
+DGPU_ENOKEY = -5
+
+SCHEME_CHAINED = 0
+SCHEME_UNCHAINED = 1
+SCHEME_UNCHAINED_G1 = 2
+
+MODE_PER_ROUND = 0
+MODE_RLC = 1
+
+REASON_OK = 0
+REASON_DECODE = 1
+REASON_SUBGROUP = 2
+REASON_PAIRING = 3
+REASON_INFINITY = 4
+
+# every symbol include/drand_gpu.h declares: (name, restype, argtypes)
+_c = ctypes
+_P = _c.c_void_p
+SYMBOLS = [
+    ("dgpu_abi_version", _c.c_int, []),
+    ("dgpu_last_error", _c.c_char_p, []),
+    ("dgpu_open", _c.c_int, [_c.c_int, _c.POINTER(_P)]),
+    ("dgpu_close", None, [_P]),
+    ("dgpu_scheme_from_name", _c.c_int, [_c.c_char_p]),
+    ("dgpu_set_pubkey", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t]),
+    ("dgpu_verify_batch", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P, _c.c_size_t, _P,
+                                     _c.c_int, _c.c_uint64, _P, _P]),
+    ("dgpu_verify_batch_device", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P, _c.c_size_t,
+                                            _P, _c.c_int, _c.c_uint64, _P, _P, _P]),
+    ("dgpu_digest_batch", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P]),
+    ("dgpu_hash_to_g2", _c.c_int, [_P, _c.c_size_t, _P, _P]),
+    ("dgpu_derive_pubkey", _c.c_int, [_P, _c.c_int, _P, _P, _c.c_size_t]),
+    ("dgpu_make_chain", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _P, _P]),
+]
+
+
+class DrandGPUError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"drand_gpu error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load(path=None):
+    """Load libdrand_gpu.so and bind every declared symbol (raises if absent)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise DrandGPUError(DGPU_EDEVICE, f"{p} not built (run __graft_entry__.build())")
+        lib = ctypes.CDLL(p)
+        for name, res, args in SYMBOLS:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.dgpu_abi_version() != 1:
+            raise DrandGPUError(DGPU_EINVAL, "ABI version mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc):
+    if rc != DGPU_OK:
+        lib = load()
+        raise DrandGPUError(rc, lib.dgpu_last_error().decode(errors="replace"))
+    return rc
+
+
+def ptr(buf):
+    """Address of a numpy array / bytes-like / torch tensor for the C-ABI."""
+    if buf is None:
+        return None
+    if hasattr(buf, "data_ptr"):
+        return buf.data_ptr()
+    if hasattr(buf, "ctypes"):
+        return buf.ctypes.data
+    raise TypeError(type(buf))
+
+
+class Context:
+    """One GPU context (dgpu_ctx*).  Thread-safe: the library serializes."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        check(self.lib.dgpu_open(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.dgpu_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

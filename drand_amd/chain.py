@@ -1,0 +1,188 @@
+"""Host-side mirror of drand's chain verification surface, backed by the
+MI355X kernels through the C-ABI (include/drand_gpu.h).
+
+Mirrors (same names, argument meaning and error behaviour):
+  chain.Beacon                      chain/beacon.go:13-20  (+ Randomness :51-54)
+  chain.RoundToBytes                chain/store.go:42-46
+  chain.NewVerifier / Verifier      chain/verify.go:13-49
+      DigestMessage(round, prevSig) chain/verify.go:24-32
+      VerifyBeacon(b, pubkey) error chain/verify.go:38-45
+      IsPrevSigMeaningful()         chain/verify.go:47-49
+and adds the batch form every bulk caller needs (sync_manager.go:188-222,
+client/verify.go:149-169): Verifier.verify_beacons(beacons, pubkey).
+
+There is no CPU fallback: every digest and every verification runs on the
+GPU; constructing a Verifier without the HIP library or a gfx950 device
+raises DrandGPUError.
+"""
+import hashlib
+import struct
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .scheme import Scheme, scheme_code
+
+
+class VerifyError(Exception):
+    """Non-nil error of VerifyBeacon; `reason` is the DGPU_REASON_* code."""
+
+    MESSAGES = {
+        _lib.REASON_DECODE: "bls: invalid signature encoding",
+        _lib.REASON_SUBGROUP: "bls: signature point is not on correct subgroup",
+        _lib.REASON_PAIRING: "bls: invalid signature",
+        _lib.REASON_INFINITY: "bls: invalid signature",
+    }
+
+    def __init__(self, round_, reason):
+        super().__init__(f"round {round_}: {self.MESSAGES.get(reason, 'invalid beacon')}")
+        self.round = round_
+        self.reason = reason
+
+
+@dataclass
+class Beacon:
+    """chain/beacon.go:13-20"""
+    previous_sig: bytes
+    round: int
+    signature: bytes
+
+    def randomness(self):
+        """chain/beacon.go:43-45 (host bookkeeping, SHA-256 of the signature)."""
+        return randomness_from_signature(self.signature)
+
+    def get_round(self):
+        return self.round
+
+
+def round_to_bytes(r):
+    """chain/store.go:42-46: 8-byte big-endian."""
+    return struct.pack(">Q", r)
+
+
+def randomness_from_signature(sig):
+    """chain/beacon.go:51-54 (not part of the verify hot path)."""
+    return hashlib.sha256(sig).digest()
+
+
+_contexts = {}
+_ctx_lock = threading.Lock()
+
+
+def get_context(device=0):
+    with _ctx_lock:
+        ctx = _contexts.get(device)
+        if ctx is None:
+            ctx = _lib.Context(device)
+            _contexts[device] = ctx
+        return ctx
+
+
+def pack_beacons(beacons, sig_stride=96, prev_stride=None):
+    """Fixed-stride records for dgpu_verify_batch (numpy arrays)."""
+    n = len(beacons)
+    if prev_stride is None:
+        prev_stride = max([96] + [len(b.previous_sig or b"") for b in beacons])
+    rounds = np.fromiter((b.round for b in beacons), dtype=np.uint64, count=n)
+    sig_len = np.fromiter((len(b.signature or b"") for b in beacons), dtype=np.uint32, count=n)
+    prev_len = np.fromiter((len(b.previous_sig or b"") for b in beacons), dtype=np.uint32, count=n)
+    stride = max(sig_stride, 96)
+    sigs = np.zeros((n, stride), dtype=np.uint8)
+    prev = np.zeros((n, prev_stride), dtype=np.uint8)
+    for i, b in enumerate(beacons):
+        s = b.signature or b""
+        if 0 < len(s) <= stride:
+            sigs[i, : len(s)] = np.frombuffer(s, dtype=np.uint8)
+        elif len(s) > stride:
+            sig_len[i] = 0xFFFFFFFF  # any length != 96 fails decode, like kilic (R)
+        p = b.previous_sig or b""
+        if p:
+            prev[i, : len(p)] = np.frombuffer(p, dtype=np.uint8)
+    return rounds, sigs, sig_len, prev, prev_len
+
+
+class Verifier:
+    """chain.Verifier (chain/verify.go:13-20): stateless apart from the scheme;
+    safe for concurrent use (the GPU context serializes)."""
+
+    def __init__(self, scheme: Scheme, device=0):
+        self.scheme = scheme
+        self.ctx = get_context(device)
+        self._code = scheme_code(scheme)
+        self._pk_loaded = None
+
+    def is_prev_sig_meaningful(self):
+        """chain/verify.go:47-49"""
+        return not self.scheme.decouple_prev_sig
+
+    def digest_message(self, round_, prev_sig):
+        """chain/verify.go:24-32 (computed on the GPU)."""
+        return self.digest_messages([round_], [prev_sig])[0]
+
+    def digest_messages(self, rounds, prev_sigs):
+        n = len(rounds)
+        r = np.asarray(rounds, dtype=np.uint64)
+        stride = max([1] + [len(p or b"") for p in prev_sigs])
+        prev = np.zeros((n, stride), dtype=np.uint8)
+        plen = np.zeros(n, dtype=np.uint32)
+        for i, p in enumerate(prev_sigs):
+            if p:
+                prev[i, : len(p)] = np.frombuffer(p, dtype=np.uint8)
+                plen[i] = len(p)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        lib = self.ctx.lib
+        _lib.check(lib.dgpu_digest_batch(self.ctx.handle, self._code, n, _lib.ptr(r), _lib.ptr(prev), stride,
+                                         _lib.ptr(plen), _lib.ptr(out)))
+        return [bytes(row) for row in out]
+
+    def _set_key(self, pubkey):
+        if self._pk_loaded != pubkey:
+            _lib.check(self.ctx.lib.dgpu_set_pubkey(self.ctx.handle, self._code, pubkey, len(pubkey)))
+            self._pk_loaded = pubkey
+
+    def verify_beacons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=0):
+        """Batch VerifyBeacon: returns a list of (None | VerifyError), one per beacon."""
+        reasons = self.verify_reasons(beacons, pubkey, mode, rlc_seed)
+        return [None if r == _lib.REASON_OK else VerifyError(b.round, int(r)) for b, r in zip(beacons, reasons)]
+
+    def verify_reasons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=0):
+        n = len(beacons)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint8)
+        rounds, sigs, sig_len, prev, prev_len = pack_beacons(beacons)
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        reason = np.zeros(n, dtype=np.uint8)
+        lib = self.ctx.lib
+        with _ctx_lock:
+            self._set_key(pubkey)
+            _lib.check(lib.dgpu_verify_batch(self.ctx.handle, self._code, n, _lib.ptr(rounds), _lib.ptr(sigs),
+                                             sigs.shape[1], _lib.ptr(sig_len), _lib.ptr(prev), prev.shape[1],
+                                             _lib.ptr(prev_len), mode, rlc_seed, _lib.ptr(bits), _lib.ptr(reason)))
+        valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+        if not np.array_equal(valid, reason == _lib.REASON_OK):
+            raise _lib.DrandGPUError(_lib.DGPU_EINVAL, "verdict bitmap and reasons disagree")
+        return reason
+
+    def verify_beacon(self, b: Beacon, pubkey: bytes):
+        """chain/verify.go:38-45: raises VerifyError (the reference's non-nil
+        error) or returns None."""
+        err = self.verify_beacons([b], pubkey)[0]
+        if err is not None:
+            raise err
+
+
+def new_verifier(scheme: Scheme, device=0):
+    """chain.NewVerifier (chain/verify.go:18-20)."""
+    return Verifier(scheme, device)
+
+
+def hash_to_g2(msgs, device=0):
+    """kyber G2 Hash (R) of 32-byte messages -> 96-byte compressed points (parity surface)."""
+    ctx = get_context(device)
+    n = len(msgs)
+    m = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    out = np.zeros(n * 96, dtype=np.uint8)
+    _lib.check(ctx.lib.dgpu_hash_to_g2(ctx.handle, n, _lib.ptr(m), _lib.ptr(out)))
+    return [bytes(out[i * 96:(i + 1) * 96]) for i in range(n)]

@@ -1,0 +1,356 @@
+// libdrand_gpu.so: the C-ABI boundary (include/drand_gpu.h) over the gfx950
+// kernels.  Host side of the product path: device memory, streams, launches.
+// There is deliberately no CPU fallback anywhere in this file.
+#include <hip/hip_runtime.h>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/drand_gpu.h"
+#include "kernels.cuh"
+
+using namespace dgpu;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return set_err(DGPU_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+// Grow-only device scratch buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return DGPU_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return set_err(DGPU_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    cap = bytes;
+    return DGPU_OK;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+struct dgpu_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  bool have_key = false;
+  int key_scheme = -1;
+  g1_key pk{};
+  // scratch
+  DevBuf h_pts, sig_pts, status;
+  // staging for host-pointer entry points
+  DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
+};
+
+extern "C" {
+
+int dgpu_abi_version(void) { return DGPU_ABI_VERSION; }
+const char* dgpu_last_error(void) { return g_last_error.c_str(); }
+
+int dgpu_scheme_from_name(const char* name) {
+  if (!name) return set_err(DGPU_EINVAL, "null scheme name");
+  if (name[0] == 0 || !strcmp(name, "pedersen-bls-chained")) return DGPU_SCHEME_CHAINED;
+  if (!strcmp(name, "pedersen-bls-unchained")) return DGPU_SCHEME_UNCHAINED;
+  if (!strcmp(name, "bls-unchained-on-g1")) return DGPU_SCHEME_UNCHAINED_G1;
+  return set_err(DGPU_EINVAL, "scheme [%s] is not valid", name);
+}
+
+int dgpu_open(int device, dgpu_ctx** out) {
+  if (!out) return set_err(DGPU_EINVAL, "null out");
+  *out = nullptr;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return set_err(DGPU_EDEVICE, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= count) return set_err(DGPU_EINVAL, "device %d out of range (%d devices)", device, count);
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(DGPU_EDEVICE, "device %d is %s; this library is built for gfx950 only", device, prop.gcnArchName);
+  HIP_TRY(hipSetDevice(device));
+  dgpu_ctx* c = new dgpu_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return set_err(DGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return DGPU_OK;
+}
+
+void dgpu_close(dgpu_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+                    &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
+    b->release();
+  hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
+  if (!c || !pk) return set_err(DGPU_EINVAL, "null argument");
+  if (scheme == DGPU_SCHEME_UNCHAINED_G1) return set_err(DGPU_EUNSUPPORTED, "bls-unchained-on-g1 not built yet");
+  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (len != 48) return set_err(DGPU_EINVAL, "public key must be 48 bytes (compressed G1), got %zu", len);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = c->misc.ensure(256);
+  if (rc) return rc;
+  uint8_t* d = (uint8_t*)c->misc.p;
+  HIP_TRY(hipMemcpyAsync(d, pk, 48, hipMemcpyHostToDevice, c->stream));
+  uint32_t* d_out = (uint32_t*)(d + 64);
+  int* d_rc = (int*)(d + 64 + 2 * FP_LIMBS * 4);
+  hipLaunchKernelGGL(k_decode_g1_pk, dim3(1), dim3(64), 0, c->stream, d, d_out, d_rc);
+  HIP_TRY(hipGetLastError());
+  uint32_t host[2 * FP_LIMBS + 1];
+  HIP_TRY(hipMemcpyAsync(host, d_out, sizeof host, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  int drc = (int)host[2 * FP_LIMBS];
+  if (drc != DEC_OK) return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
+  memcpy(c->pk.neg_x.l, host, FP_LIMBS * 4);
+  memcpy(c->pk.y.l, host + FP_LIMBS, FP_LIMBS * 4);
+  c->have_key = true;
+  c->key_scheme = scheme;
+  return DGPU_OK;
+}
+
+static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
+                                size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev,
+                                size_t prev_stride, const uint32_t* d_prev_len, int mode, uint64_t rlc_seed,
+                                uint8_t* d_bits, uint8_t* d_reason, hipStream_t s) {
+  (void)rlc_seed;
+  if (scheme == DGPU_SCHEME_UNCHAINED_G1) return set_err(DGPU_EUNSUPPORTED, "bls-unchained-on-g1 not built yet");
+  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (mode != DGPU_MODE_PER_ROUND) return set_err(DGPU_EUNSUPPORTED, "mode %d not built yet", mode);
+  if (!c->have_key) return set_err(DGPU_ENOKEY, "no public key installed (dgpu_set_pubkey)");
+  if (n == 0) return DGPU_OK;
+  bool chained = scheme == DGPU_SCHEME_CHAINED;
+  if (!d_rounds || !d_sigs || !d_sig_len || !d_bits || sig_stride < 96) return set_err(DGPU_EINVAL, "bad buffers");
+  if (chained && (!d_prev || !d_prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
+  int rc;
+  if ((rc = c->h_pts.ensure(n * G2A_WORDS * 4))) return rc;
+  if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
+  if ((rc = c->status.ensure(n))) return rc;
+  uint32_t* h = (uint32_t*)c->h_pts.p;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  const unsigned B = 256;
+  hipLaunchKernelGGL(k_hash_to_g2_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
+                     d_prev_len, chained ? 1 : 0, h);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);
+  HIP_TRY(hipGetLastError());
+  if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, n, hipMemcpyDeviceToDevice, s));
+  return DGPU_OK;
+}
+
+int dgpu_verify_batch_device(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
+                             size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev, size_t prev_stride,
+                             const uint32_t* d_prev_len, int mode, uint64_t rlc_seed, uint8_t* d_bits,
+                             uint8_t* d_reason, void* stream) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return verify_device_locked(c, scheme, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len,
+                              mode, rlc_seed, d_bits, d_reason, s);
+}
+
+int dgpu_verify_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds, const uint8_t* sigs,
+                      size_t sig_stride, const uint32_t* sig_len, const uint8_t* prev, size_t prev_stride,
+                      const uint32_t* prev_len, int mode, uint64_t rlc_seed, uint8_t* verdict_bits, uint8_t* reason) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  if (n == 0) return DGPU_OK;
+  if (!rounds || !sigs || !sig_len || !verdict_bits) return set_err(DGPU_EINVAL, "null buffer");
+  bool chained = scheme == DGPU_SCHEME_CHAINED;
+  if (chained && (!prev || !prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  if ((rc = c->in_rounds.ensure(n * 8))) return rc;
+  if ((rc = c->in_sigs.ensure(n * sig_stride))) return rc;
+  if ((rc = c->in_sig_len.ensure(n * 4))) return rc;
+  if ((rc = c->out_bits.ensure((n + 7) / 8))) return rc;
+  if ((rc = c->out_reason.ensure(n))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_rounds.p, rounds, n * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, sigs, n * sig_stride, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->in_sig_len.p, sig_len, n * 4, hipMemcpyHostToDevice, s));
+  const uint8_t* d_prev = nullptr;
+  const uint32_t* d_prev_len = nullptr;
+  if (chained) {
+    if ((rc = c->in_prev.ensure(n * prev_stride + 1))) return rc;
+    if ((rc = c->in_prev_len.ensure(n * 4))) return rc;
+    for (size_t i = 0; i < n; ++i)
+      if (prev_len[i] > prev_stride) return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, prev_len[i]);
+    if (prev_stride) HIP_TRY(hipMemcpyAsync(c->in_prev.p, prev, n * prev_stride, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->in_prev_len.p, prev_len, n * 4, hipMemcpyHostToDevice, s));
+    d_prev = (const uint8_t*)c->in_prev.p;
+    d_prev_len = (const uint32_t*)c->in_prev_len.p;
+  }
+  rc = verify_device_locked(c, scheme, n, (const uint64_t*)c->in_rounds.p, (const uint8_t*)c->in_sigs.p, sig_stride,
+                            (const uint32_t*)c->in_sig_len.p, d_prev, prev_stride, d_prev_len, mode, rlc_seed,
+                            (uint8_t*)c->out_bits.p, (uint8_t*)c->out_reason.p, s);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(verdict_bits, c->out_bits.p, (n + 7) / 8, hipMemcpyDeviceToHost, s));
+  if (reason) HIP_TRY(hipMemcpyAsync(reason, c->out_reason.p, n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+int dgpu_digest_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds, const uint8_t* prev,
+                      size_t prev_stride, const uint32_t* prev_len, uint8_t* out32) {
+  if (!c || !rounds || !out32) return set_err(DGPU_EINVAL, "null argument");
+  if (n == 0) return DGPU_OK;
+  bool chained = scheme == DGPU_SCHEME_CHAINED;
+  if (chained && (!prev || !prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  if ((rc = c->in_rounds.ensure(n * 8))) return rc;
+  if ((rc = c->misc.ensure(n * 32))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_rounds.p, rounds, n * 8, hipMemcpyHostToDevice, s));
+  const uint8_t* d_prev = nullptr;
+  const uint32_t* d_prev_len = nullptr;
+  if (chained) {
+    if ((rc = c->in_prev.ensure(n * prev_stride + 1))) return rc;
+    if ((rc = c->in_prev_len.ensure(n * 4))) return rc;
+    for (size_t i = 0; i < n; ++i)
+      if (prev_len[i] > prev_stride) return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, prev_len[i]);
+    if (prev_stride) HIP_TRY(hipMemcpyAsync(c->in_prev.p, prev, n * prev_stride, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->in_prev_len.p, prev_len, n * 4, hipMemcpyHostToDevice, s));
+    d_prev = (const uint8_t*)c->in_prev.p;
+    d_prev_len = (const uint32_t*)c->in_prev_len.p;
+  }
+  hipLaunchKernelGGL(k_digest, dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const uint64_t*)c->in_rounds.p, d_prev,
+                     prev_stride, d_prev_len, chained ? 1 : 0, (uint8_t*)c->misc.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out32, c->misc.p, n * 32, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+int dgpu_hash_to_g2(dgpu_ctx* c, size_t n, const uint8_t* msg32, uint8_t* out96) {
+  if (!c || !msg32 || !out96) return set_err(DGPU_EINVAL, "null argument");
+  if (n == 0) return DGPU_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  if ((rc = c->in_sigs.ensure(n * 32))) return rc;
+  if ((rc = c->misc.ensure(n * 96))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, msg32, n * 32, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_hash_to_g2_msgs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const uint8_t*)c->in_sigs.p,
+                     (uint8_t*)c->misc.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out96, c->misc.p, n * 96, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+static scalar256 scalar_from_be32(const uint8_t* b) {
+  scalar256 k;
+  for (int w = 0; w < 8; ++w)
+    k.w[w] = ((uint32_t)b[31 - 4 * w - 3] << 24) | ((uint32_t)b[31 - 4 * w - 2] << 16) |
+             ((uint32_t)b[31 - 4 * w - 1] << 8) | b[31 - 4 * w];
+  return k;
+}
+
+int dgpu_derive_pubkey(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, uint8_t* pk_out, size_t pk_len) {
+  if (!c || !sk_be32 || !pk_out) return set_err(DGPU_EINVAL, "null argument");
+  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EUNSUPPORTED, "scheme %d", scheme);
+  if (pk_len != 48) return set_err(DGPU_EINVAL, "pk_len must be 48");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = c->misc.ensure(64);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_derive_pubkey, dim3(1), dim3(64), 0, c->stream, scalar_from_be32(sk_be32), (uint8_t*)c->misc.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(pk_out, c->misc.p, 48, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return DGPU_OK;
+}
+
+int dgpu_make_chain(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n_seg, size_t seg_len,
+                    const uint64_t* first_round, const uint8_t* seed_prev, const uint32_t* seed_prev_len,
+                    uint8_t* sigs_out) {
+  if (!c || !sk_be32 || !first_round || !sigs_out) return set_err(DGPU_EINVAL, "null argument");
+  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EUNSUPPORTED, "scheme %d", scheme);
+  bool chained = scheme == DGPU_SCHEME_CHAINED;
+  if (chained && (!seed_prev || !seed_prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs seed_prev");
+  if (n_seg == 0 || seg_len == 0) return DGPU_OK;
+  scalar256 sk = scalar_from_be32(sk_be32);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  DevBuf d_first, d_prev, d_plen, d_sigs;
+  if ((rc = d_first.ensure(n_seg * 8))) return rc;
+  if ((rc = d_prev.ensure(n_seg * 96))) { d_first.release(); return rc; }
+  if ((rc = d_plen.ensure(n_seg * 4))) { d_first.release(); d_prev.release(); return rc; }
+  if ((rc = d_sigs.ensure(n_seg * seg_len * 96))) { d_first.release(); d_prev.release(); d_plen.release(); return rc; }
+  std::vector<uint8_t> pv(n_seg * 96, 0);
+  std::vector<uint32_t> pl(n_seg, 0);
+  if (chained) {
+    for (size_t i = 0; i < n_seg; ++i) {
+      pl[i] = seed_prev_len[i] > 96 ? 96 : seed_prev_len[i];
+      memcpy(&pv[i * 96], seed_prev + i * 96, pl[i]);
+    }
+  }
+  int ret = DGPU_OK;
+  hipError_t e = hipMemcpyAsync(d_first.p, first_round, n_seg * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_prev.p, pv.data(), n_seg * 96, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_plen.p, pl.data(), n_seg * 4, hipMemcpyHostToDevice, s);
+  for (size_t j = 0; e == hipSuccess && j < seg_len; ++j) {
+    // segment-major output: round j of segment s at (s*seg_len + j)*96
+    hipLaunchKernelGGL(k_sign_step, dim3(grid_for(n_seg, 64)), dim3(64), 0, s, n_seg, (const uint64_t*)d_first.p,
+                       (uint64_t)j, (uint8_t*)d_prev.p, (uint32_t*)d_plen.p, chained ? 1 : 0, sk,
+                       (uint8_t*)d_sigs.p + j * 96, seg_len * 96);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(sigs_out, d_sigs.p, n_seg * seg_len * 96, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) ret = set_err(DGPU_EDEVICE, "make_chain: %s", hipGetErrorString(e));
+  d_first.release(); d_prev.release(); d_plen.release(); d_sigs.release();
+  return ret;
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+// G1 (E: y^2 = x^3 + 4 over Fp) and G2 (E': y^2 = x^3 + 4(1+u) over Fp2)
+// group law in Jacobian coordinates (x = X/Z^2, y = Y/Z^3, Z = 0 is the point
+// at infinity), the psi endomorphism, the psi-based G2 membership test, and
+// ZCash compressed encodings (the format kyber-bls12381 / kilic read and
+// write: chain/verify.go:44 -> key.Scheme.VerifyRecovered (R)).
+#pragma once
+#include "tower.cuh"
+
+namespace dgpu {
+
+struct g2a {  // affine
+  fp2 x, y;
+};
+struct g2j {  // Jacobian
+  fp2 x, y, z;
+};
+struct g1a {
+  fp x, y;
+};
+struct g1j {
+  fp x, y, z;
+};
+
+// ================================================================ G2
+DG_FN g2j g2_from_affine(const g2a& a) { return g2j{a.x, a.y, fp2_one()}; }
+DG_FN g2j g2_infinity() { return g2j{fp2_one(), fp2_one(), fp2_zero()}; }
+DG_FN bool g2_is_inf(const g2j& a) { return fp2_is_zero(a.z); }
+DG_FN g2j g2_neg(const g2j& a) { return g2j{a.x, fp2_neg(a.y), a.z}; }
+
+DG_FN g2j g2_cmov(const g2j& a, const g2j& b, bool take_b) {
+  return g2j{fp2_cmov(a.x, b.x, take_b), fp2_cmov(a.y, b.y, take_b), fp2_cmov(a.z, b.z, take_b)};
+}
+
+// dbl-2009-l (a = 0): 2M + 5S.  Infinity stays infinity (Z3 = 2YZ).
+DG_NOINL g2j g2_dbl(const g2j& p) {
+  fp2 A = fp2_sqr(p.x);
+  fp2 B = fp2_sqr(p.y);
+  fp2 C = fp2_sqr(B);
+  fp2 D = fp2_sub(fp2_sqr(fp2_add(p.x, B)), fp2_add(A, C));
+  D = fp2_dbl(D);
+  fp2 E = fp2_add(fp2_dbl(A), A);
+  fp2 F = fp2_sqr(E);
+  g2j r;
+  r.x = fp2_sub(F, fp2_dbl(D));
+  fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
+  r.y = fp2_sub(fp2_mul(E, fp2_sub(D, r.x)), C8);
+  r.z = fp2_dbl(fp2_mul(p.y, p.z));
+  return r;
+}
+
+// add-2007-bl with the exceptional cases resolved (P == Q -> dbl,
+// P == -Q -> infinity, either operand infinity -> the other).
+DG_NOINL g2j g2_add(const g2j& p, const g2j& q) {
+  fp2 z1z1 = fp2_sqr(p.z);
+  fp2 z2z2 = fp2_sqr(q.z);
+  fp2 u1 = fp2_mul(p.x, z2z2);
+  fp2 u2 = fp2_mul(q.x, z1z1);
+  fp2 s1 = fp2_mul(fp2_mul(p.y, q.z), z2z2);
+  fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
+  fp2 h = fp2_sub(u2, u1);
+  fp2 rr = fp2_dbl(fp2_sub(s2, s1));
+  bool p_inf = g2_is_inf(p), q_inf = g2_is_inf(q);
+  bool h0 = fp2_is_zero(h), r0 = fp2_is_zero(rr);
+  fp2 i = fp2_sqr(fp2_dbl(h));
+  fp2 j = fp2_mul(h, i);
+  fp2 v = fp2_mul(u1, i);
+  g2j r;
+  r.x = fp2_sub(fp2_sub(fp2_sqr(rr), j), fp2_dbl(v));
+  r.y = fp2_sub(fp2_mul(rr, fp2_sub(v, r.x)), fp2_dbl(fp2_mul(s1, j)));
+  r.z = fp2_mul(fp2_sub(fp2_sqr(fp2_add(p.z, q.z)), fp2_add(z1z1, z2z2)), h);
+  if (h0 && !p_inf && !q_inf) r = r0 ? g2_dbl(p) : g2_infinity();
+  if (p_inf) r = q;
+  if (q_inf) r = p;
+  return r;
+}
+
+// [|x|] p for the BLS parameter |x| = 0xd201000000010000 (MSB-first double-and-add)
+DG_NOINL g2j g2_mul_absx(const g2j& p) {
+  g2j r = p;
+  for (int i = 62; i >= 0; --i) {
+    r = g2_dbl(r);
+    if ((BLS_X_ABS >> i) & 1ull) r = g2_add(r, p);
+  }
+  return r;
+}
+
+// generic [k] p, k given as little-endian 32-bit words (MSB-first double-and-add)
+DG_NOINL g2j g2_mul_words(const g2j& p, const uint32_t* k, int nwords) {
+  g2j r = g2_infinity();
+  for (int i = nwords * 32 - 1; i >= 0; --i) {
+    r = g2_dbl(r);
+    if ((k[i >> 5] >> (i & 31)) & 1u) r = g2_add(r, p);
+  }
+  return r;
+}
+
+// [x] p with x < 0
+DG_FN g2j g2_mul_x(const g2j& p) { return g2_neg(g2_mul_absx(p)); }
+
+// psi(x, y) = (conj(x) cx, conj(y) cy); on Jacobian coordinates Z -> conj(Z)
+DG_NOINL g2j g2_psi(const g2j& p) {
+  return g2j{fp2_mul(fp2_conj(p.x), C_PSI_CX), fp2_mul(fp2_conj(p.y), C_PSI_CY), fp2_conj(p.z)};
+}
+DG_NOINL g2j g2_psi2(const g2j& p) {
+  return g2j{fp2_mul_fp(p.x, fp2(C_PSI2_CX).c0), fp2_mul_fp(p.y, fp2(C_PSI2_CY).c0), p.z};
+}
+
+DG_NOINL bool g2_eq(const g2j& p, const g2j& q) {
+  bool pi = g2_is_inf(p), qi = g2_is_inf(q);
+  if (pi || qi) return pi && qi;
+  fp2 z1z1 = fp2_sqr(p.z), z2z2 = fp2_sqr(q.z);
+  bool ex = fp2_eq(fp2_mul(p.x, z2z2), fp2_mul(q.x, z1z1));
+  bool ey = fp2_eq(fp2_mul(fp2_mul(p.y, q.z), z2z2), fp2_mul(fp2_mul(q.y, p.z), z1z1));
+  return ex && ey;
+}
+
+// G2 membership: psi(Q) == [x] Q  (Scott, "A note on group membership tests
+// for G1, G2 and GT on BLS pairing-friendly curves"); same verdict as the
+// reference's [r] Q == O test (R), checked against it in tests.
+DG_FN bool g2_in_subgroup(const g2j& p) { return g2_eq(g2_psi(p), g2_mul_x(p)); }
+
+DG_NOINL g2a g2_to_affine(const g2j& p) {
+  fp2 zi = fp2_inv(p.z);
+  fp2 zi2 = fp2_sqr(zi);
+  return g2a{fp2_mul(p.x, zi2), fp2_mul(p.y, fp2_mul(zi2, zi))};
+}
+
+DG_FN bool g2_on_curve_affine(const g2a& a) {
+  fp2 rhs = fp2_add(fp2_mul(fp2_sqr(a.x), a.x), C_B2);
+  return fp2_eq(fp2_sqr(a.y), rhs);
+}
+
+// Clear cofactor: h_eff * P = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P)
+// (RFC 9380 appendix G.3 sequence).
+DG_NOINL g2j g2_clear_cofactor(const g2j& p) {
+  g2j t1 = g2_mul_x(p);
+  g2j t2 = g2_psi(p);
+  g2j t3 = g2_psi2(g2_dbl(p));
+  t3 = g2_add(t3, g2_neg(t2));
+  t2 = g2_add(t1, t2);
+  t2 = g2_mul_x(t2);
+  t3 = g2_add(t3, t2);
+  t3 = g2_add(t3, g2_neg(t1));
+  return g2_add(t3, g2_neg(p));
+}
+
+// ---------------------------------------------------------------- ZCash G2 codec
+enum : int {
+  DEC_OK = 0,
+  DEC_ERR_LENGTH = 1,
+  DEC_ERR_FLAG = 2,
+  DEC_ERR_INFINITY_NONCANON = 3,
+  DEC_INFINITY = 4,
+  DEC_ERR_X_RANGE = 5,
+  DEC_ERR_NOT_ON_CURVE = 6,
+  DEC_ERR_SUBGROUP = 7,
+};
+
+// Decode a 96-byte compressed G2 point (c1 || c0 big-endian, flags in byte 0).
+// Returns DEC_OK (affine point in *out), DEC_INFINITY, or an error code.
+DG_NOINL int g2_decompress(g2a* out, const uint8_t* in, bool check_subgroup) {
+  uint8_t b0 = in[0];
+  if (!(b0 & 0x80)) return DEC_ERR_FLAG;
+  if (b0 & 0x40) {
+    uint32_t acc = b0 & 0x3f;
+    for (int i = 1; i < 96; ++i) acc |= in[i];
+    return acc ? DEC_ERR_INFINITY_NONCANON : DEC_INFINITY;
+  }
+  bool sign = (b0 & 0x20) != 0;
+  uint8_t buf[48];
+  for (int i = 0; i < 48; ++i) buf[i] = in[i];
+  buf[0] &= 0x1f;
+  fp x1 = fp_std_from_be48(buf);
+  fp x0 = fp_std_from_be48(in + 48);
+  if (!fp_std_lt_p(x0) || !fp_std_lt_p(x1)) return DEC_ERR_X_RANGE;
+  fp2 x{fp_to_mont(x0), fp_to_mont(x1)};
+  fp2 rhs = fp2_add(fp2_mul(fp2_sqr(x), x), C_B2);
+  fp2 y;
+  if (!fp2_sqrt(y, rhs)) return DEC_ERR_NOT_ON_CURVE;
+  if (fp2_lexi_largest(y) != sign) y = fp2_neg(y);
+  out->x = x;
+  out->y = y;
+  if (check_subgroup && !g2_in_subgroup(g2_from_affine(*out))) return DEC_ERR_SUBGROUP;
+  return DEC_OK;
+}
+
+DG_NOINL void g2_compress(uint8_t* out, const g2a& a, bool infinity) {
+  if (infinity) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 96; ++i) out[i] = 0;
+    return;
+  }
+  fp x0, x1;
+  fp2_from_mont(x0, x1, a.x);
+  fp_std_to_be48(x1, out);
+  fp_std_to_be48(x0, out + 48);
+  out[0] |= 0x80;
+  if (fp2_lexi_largest(a.y)) out[0] |= 0x20;
+}
+
+// ================================================================ G1
+DG_FN g1j g1_infinity() { return g1j{fp_one(), fp_one(), fp_zero()}; }
+DG_FN bool g1_is_inf(const g1j& a) { return fp_is_zero(a.z); }
+DG_FN g1j g1_neg(const g1j& a) { return g1j{a.x, fp_neg(a.y), a.z}; }
+
+DG_NOINL g1j g1_dbl(const g1j& p) {
+  fp A = fp_sqr(p.x);
+  fp B = fp_sqr(p.y);
+  fp C = fp_sqr(B);
+  fp D = fp_dbl(fp_sub(fp_sqr(fp_add(p.x, B)), fp_add(A, C)));
+  fp E = fp_add(fp_dbl(A), A);
+  fp F = fp_sqr(E);
+  g1j r;
+  r.x = fp_sub(F, fp_dbl(D));
+  r.y = fp_sub(fp_mul(E, fp_sub(D, r.x)), fp_dbl(fp_dbl(fp_dbl(C))));
+  r.z = fp_dbl(fp_mul(p.y, p.z));
+  return r;
+}
+
+DG_NOINL g1j g1_add(const g1j& p, const g1j& q) {
+  fp z1z1 = fp_sqr(p.z), z2z2 = fp_sqr(q.z);
+  fp u1 = fp_mul(p.x, z2z2), u2 = fp_mul(q.x, z1z1);
+  fp s1 = fp_mul(fp_mul(p.y, q.z), z2z2), s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  fp h = fp_sub(u2, u1);
+  fp rr = fp_dbl(fp_sub(s2, s1));
+  bool p_inf = g1_is_inf(p), q_inf = g1_is_inf(q);
+  bool h0 = fp_is_zero(h), r0 = fp_is_zero(rr);
+  fp i = fp_sqr(fp_dbl(h));
+  fp j = fp_mul(h, i);
+  fp v = fp_mul(u1, i);
+  g1j r;
+  r.x = fp_sub(fp_sub(fp_sqr(rr), j), fp_dbl(v));
+  r.y = fp_sub(fp_mul(rr, fp_sub(v, r.x)), fp_dbl(fp_mul(s1, j)));
+  r.z = fp_mul(fp_sub(fp_sqr(fp_add(p.z, q.z)), fp_add(z1z1, z2z2)), h);
+  if (h0 && !p_inf && !q_inf) r = r0 ? g1_dbl(p) : g1_infinity();
+  if (p_inf) r = q;
+  if (q_inf) r = p;
+  return r;
+}
+
+// generic scalar multiplication by a little-endian 32-bit-word scalar
+DG_NOINL g1j g1_mul_words(const g1j& p, const uint32_t* k, int nwords) {
+  g1j r = g1_infinity();
+  for (int i = nwords * 32 - 1; i >= 0; --i) {
+    r = g1_dbl(r);
+    if ((k[i >> 5] >> (i & 31)) & 1u) r = g1_add(r, p);
+  }
+  return r;
+}
+
+DG_FN g1a g1_to_affine(const g1j& p) {
+  fp zi = fp_inv(p.z);
+  fp zi2 = fp_sqr(zi);
+  return g1a{fp_mul(p.x, zi2), fp_mul(p.y, fp_mul(zi2, zi))};
+}
+
+DG_NOINL void g1_compress(uint8_t* out, const g1a& a, bool infinity) {
+  if (infinity) {
+    out[0] = 0xc0;
+    for (int i = 1; i < 48; ++i) out[i] = 0;
+    return;
+  }
+  fp_std_to_be48(fp_from_mont(a.x), out);
+  out[0] |= 0x80;
+  if (fp_std_gt_half(fp_from_mont(a.y))) out[0] |= 0x20;
+}
+
+// Decode a 48-byte compressed G1 point; G1 membership by [r] P == O (r as words).
+DG_NOINL int g1_decompress(g1a* out, const uint8_t* in, const uint32_t* r_words) {
+  uint8_t b0 = in[0];
+  if (!(b0 & 0x80)) return DEC_ERR_FLAG;
+  if (b0 & 0x40) {
+    uint32_t acc = b0 & 0x3f;
+    for (int i = 1; i < 48; ++i) acc |= in[i];
+    return acc ? DEC_ERR_INFINITY_NONCANON : DEC_INFINITY;
+  }
+  bool sign = (b0 & 0x20) != 0;
+  uint8_t buf[48];
+  for (int i = 0; i < 48; ++i) buf[i] = in[i];
+  buf[0] &= 0x1f;
+  fp xs = fp_std_from_be48(buf);
+  if (!fp_std_lt_p(xs)) return DEC_ERR_X_RANGE;
+  fp x = fp_to_mont(xs);
+  fp rhs = fp_add(fp_mul(fp_sqr(x), x), C_B1);
+  fp y = fp_sqrt_cand(rhs);
+  if (!fp_eq(fp_sqr(y), rhs)) return DEC_ERR_NOT_ON_CURVE;
+  if (fp_std_gt_half(fp_from_mont(y)) != sign) y = fp_neg(y);
+  out->x = x;
+  out->y = y;
+  g1j t = g1_mul_words(g1j{x, y, fp_one()}, r_words, 8);
+  if (!g1_is_inf(t)) return DEC_ERR_SUBGROUP;
+  return DEC_OK;
+}
+
+}  // namespace dgpu

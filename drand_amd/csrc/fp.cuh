@@ -1,0 +1,321 @@
+// Fp arithmetic for BLS12-381 on gfx950: 14 x 28-bit unsaturated limbs held
+// in 32-bit VGPRs, Montgomery form with R = 2^392.
+//
+// Why this shape (measured, profiles/r01_microbench_*.txt): on gfx950
+// v_mad_u64_u32 issues at ~half rate (33.5 T/s chip-wide) and carry-chained
+// v_add_co/v_addc pairs serialize on VCC, while plain v_add_u32 is full rate.
+// 28-bit limbs leave 4 bits of headroom per limb, so a 14-term product column
+// (each term < 2^60) accumulates in one 64-bit register pair with a single
+// v_mad_u64_u32 per partial product and no carry flags at all, and field
+// additions are 14 carry-free v_add_u32 (normalized lazily).
+//
+// Value invariant of every public op ("CI"): limbs normalized (< 2^28 each),
+// value < 2.01 p.  fp_mul / fp_sqr accept any inputs whose limbs are < 2^30
+// and whose values multiply to < R*p (~2600 p^2), and return CI (< 1.01 p).
+// Functions with the suffix _lz are lazy (unnormalized) and document the
+// bounds their callers rely on.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "constants.h"
+
+#ifndef DG_FN
+#define DG_FN __host__ __device__ __forceinline__
+#endif
+// Out-of-line on the device: keeps loop bodies small enough for the
+// instruction cache and the compile tractable (args/returns stay in VGPRs
+// for Fp-sized values).
+#ifndef DG_NOINL
+#define DG_NOINL __host__ __device__ __noinline__
+#endif
+
+namespace dgpu {
+
+struct fp {
+  uint32_t l[FP_LIMBS];
+};
+#define FP_CONST(...) ::dgpu::fp{{__VA_ARGS__}}
+
+DG_FN fp fp_zero() {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.l[i] = 0;
+  return r;
+}
+
+DG_FN fp fp_one() { return FP_ONE_MONT; }
+
+// ---------------------------------------------------------------- Montgomery
+// Separated operand scanning in product-scanning order: full 28-limb product,
+// then the Montgomery reduction, both column-wise into a 64-bit accumulator.
+DG_NOINL fp fp_mul(fp a, fp b) {
+  uint32_t t[2 * FP_LIMBS];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * FP_LIMBS - 1; ++k) {
+#pragma unroll
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); i <= (k < FP_LIMBS ? k : FP_LIMBS - 1); ++i)
+      acc += (uint64_t)a.l[i] * b.l[k - i];
+    t[k] = (uint32_t)acc & FP_MASK;
+    acc >>= FP_BITS;
+  }
+  t[2 * FP_LIMBS - 1] = (uint32_t)acc;
+  uint32_t m[FP_LIMBS];
+  fp r;
+  acc = 0;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) {
+#pragma unroll
+    for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * FP_P[k - i];
+    acc += t[k];
+    m[k] = ((uint32_t)acc * FP_PINV) & FP_MASK;
+    acc += (uint64_t)m[k] * FP_P[0];
+    acc >>= FP_BITS;
+  }
+#pragma unroll
+  for (int k = FP_LIMBS; k < 2 * FP_LIMBS; ++k) {
+#pragma unroll
+    for (int i = k - FP_LIMBS + 1; i < FP_LIMBS; ++i) acc += (uint64_t)m[i] * FP_P[k - i];
+    acc += t[k];
+    if (k < 2 * FP_LIMBS - 1) {
+      r.l[k - FP_LIMBS] = (uint32_t)acc & FP_MASK;
+      acc >>= FP_BITS;
+    } else {
+      r.l[k - FP_LIMBS] = (uint32_t)acc;
+    }
+  }
+  return r;
+}
+
+// Squaring: cross products computed once and doubled (98 instead of 196
+// partial products in the first half).
+DG_NOINL fp fp_sqr(fp a) {
+  uint32_t t[2 * FP_LIMBS];
+  uint64_t carry = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * FP_LIMBS - 1; ++k) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); 2 * i < k; ++i) x += (uint64_t)a.l[i] * a.l[k - i];
+    x <<= 1;
+    if ((k & 1) == 0) x += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    x += carry;
+    t[k] = (uint32_t)x & FP_MASK;
+    carry = x >> FP_BITS;
+  }
+  t[2 * FP_LIMBS - 1] = (uint32_t)carry;
+  uint32_t m[FP_LIMBS];
+  fp r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) {
+#pragma unroll
+    for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * FP_P[k - i];
+    acc += t[k];
+    m[k] = ((uint32_t)acc * FP_PINV) & FP_MASK;
+    acc += (uint64_t)m[k] * FP_P[0];
+    acc >>= FP_BITS;
+  }
+#pragma unroll
+  for (int k = FP_LIMBS; k < 2 * FP_LIMBS; ++k) {
+#pragma unroll
+    for (int i = k - FP_LIMBS + 1; i < FP_LIMBS; ++i) acc += (uint64_t)m[i] * FP_P[k - i];
+    acc += t[k];
+    if (k < 2 * FP_LIMBS - 1) {
+      r.l[k - FP_LIMBS] = (uint32_t)acc & FP_MASK;
+      acc >>= FP_BITS;
+    } else {
+      r.l[k - FP_LIMBS] = (uint32_t)acc;
+    }
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- normalization
+// Carry-propagate: limbs < 2^28 except the top one.  Input limbs < 2^31.
+DG_FN fp fp_norm(const fp& a) {
+  fp r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS - 1; ++i) {
+    uint32_t s = a.l[i] + c;
+    r.l[i] = s & FP_MASK;
+    c = s >> FP_BITS;
+  }
+  r.l[FP_LIMBS - 1] = a.l[FP_LIMBS - 1] + c;
+  return r;
+}
+
+// Input normalized, value < 2^392.  Output CI (< 2.01p): subtract q*p with
+// q = floor(top / (floor(p / 2^364) + 1)) <= floor(value / p).
+DG_NOINL fp fp_reduce(fp a) {
+  constexpr uint32_t PTOP1 = FP_P[FP_LIMBS - 1] + 1;
+  uint32_t q = a.l[FP_LIMBS - 1] / PTOP1;
+  fp r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS - 1; ++i) {
+    int64_t s = (int64_t)a.l[i] - (int64_t)((uint64_t)q * FP_P[i]) + c;
+    r.l[i] = (uint32_t)s & FP_MASK;
+    c = s >> FP_BITS;  // arithmetic
+  }
+  r.l[FP_LIMBS - 1] = (uint32_t)((int64_t)a.l[FP_LIMBS - 1] - (int64_t)q * FP_P[FP_LIMBS - 1] + c);
+  return r;
+}
+
+// ---------------------------------------------------------------- lazy add/sub
+DG_FN fp fp_add_lz(const fp& a, const fp& b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.l[i] = a.l[i] + b.l[i];
+  return r;
+}
+
+// a - b + 8p; b normalized with value < 7.99p.  Limbs of result < a_i + 2^29.6.
+DG_FN fp fp_sub_lz(const fp& a, const fp& b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.l[i] = a.l[i] + FP_SUBK[i] - b.l[i];
+  return r;
+}
+
+// a - b + 32p; b = unnormalized sum of two normalized values (value < 31.9p).
+DG_FN fp fp_sub2_lz(const fp& a, const fp& b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.l[i] = a.l[i] + FP_SUBK2[i] - b.l[i];
+  return r;
+}
+
+// ---------------------------------------------------------------- safe ops (CI in, CI out)
+DG_FN fp fp_add(const fp& a, const fp& b) { return fp_reduce(fp_norm(fp_add_lz(a, b))); }
+DG_FN fp fp_sub(const fp& a, const fp& b) { return fp_reduce(fp_norm(fp_sub_lz(a, b))); }
+DG_FN fp fp_neg(const fp& a) { return fp_sub(fp_zero(), a); }
+DG_FN fp fp_dbl(const fp& a) { return fp_add(a, a); }
+
+// a / 2 mod p.  a CI.  If odd add p (value < 3.01p), then shift right.
+DG_NOINL fp fp_half(fp a) {
+  uint32_t odd = a.l[0] & 1u;
+  uint32_t mask = 0u - odd;
+  fp t;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) t.l[i] = a.l[i] + (FP_P[i] & mask);
+  t = fp_norm(t);
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS - 1; ++i) r.l[i] = (t.l[i] >> 1) | ((t.l[i + 1] & 1u) << (FP_BITS - 1));
+  r.l[FP_LIMBS - 1] = t.l[FP_LIMBS - 1] >> 1;
+  return r;
+}
+
+DG_FN fp fp_cmov(const fp& a, const fp& b, bool take_b) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.l[i] = take_b ? b.l[i] : a.l[i];
+  return r;
+}
+
+// ---------------------------------------------------------------- canonical form
+// Exact reduction of a normalized value < 2p into [0, p).
+DG_NOINL fp fp_csub_p(fp a) {
+  fp d;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) {
+    int32_t s = (int32_t)a.l[i] - (int32_t)FP_P[i] + c;
+    d.l[i] = (uint32_t)s & FP_MASK;
+    c = s >> FP_BITS;
+  }
+  // c < 0 <=> a < p
+  return fp_cmov(d, a, c < 0);
+}
+
+// Montgomery -> standard canonical integer in [0, p).
+DG_FN fp fp_from_mont(const fp& a) {
+  fp one = fp_zero();
+  one.l[0] = 1;
+  return fp_csub_p(fp_mul(a, one));  // < p + 2^-10 p
+}
+
+// standard integer (limbs normalized, value < 2^384) -> Montgomery (CI)
+DG_FN fp fp_to_mont(const fp& a) { return fp_mul(a, FP_R2); }
+
+DG_FN bool fp_is_zero_std(const fp& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) acc |= a.l[i];
+  return acc == 0;
+}
+
+DG_FN bool fp_is_zero(const fp& a) { return fp_is_zero_std(fp_from_mont(a)); }
+
+DG_FN bool fp_eq(const fp& a, const fp& b) { return fp_is_zero(fp_sub(a, b)); }
+
+// ---------------------------------------------------------------- exponentiation
+// MSB-first square-and-multiply over a public constant exponent (uniform branch).
+DG_NOINL fp fp_pow(fp a, const uint32_t* e, int nbits) {
+  fp r = a;
+  for (int i = nbits - 2; i >= 0; --i) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+DG_FN fp fp_inv(const fp& a) { return fp_pow(a, EXP_P_MINUS_2, EXP_P_MINUS_2_BITS); }
+
+// candidate square root a^((p+1)/4); caller checks (r^2 == a)
+DG_FN fp fp_sqrt_cand(const fp& a) { return fp_pow(a, EXP_P_PLUS_1_DIV_4, EXP_P_PLUS_1_DIV_4_BITS); }
+
+// Legendre-style test: a is a square (or zero)
+DG_FN bool fp_is_square(const fp& a) {
+  fp t = fp_pow(a, EXP_P_MINUS_1_DIV_2, EXP_P_MINUS_1_DIV_2_BITS);
+  return fp_is_zero(t) || fp_eq(t, fp_one());
+}
+
+// ---------------------------------------------------------------- bytes <-> fp
+// 48 big-endian bytes (value < 2^384) -> standard limbs (not Montgomery)
+DG_FN fp fp_std_from_be48(const uint8_t* b) {
+  fp r = fp_zero();
+#pragma unroll
+  for (int byte = 0; byte < 48; ++byte) {
+    uint32_t v = b[47 - byte];
+    int bit = byte * 8;
+    r.l[bit / FP_BITS] |= (v << (bit % FP_BITS)) & FP_MASK;
+    if (bit % FP_BITS > FP_BITS - 8) r.l[bit / FP_BITS + 1] |= v >> (FP_BITS - bit % FP_BITS);
+  }
+  return r;
+}
+
+// standard canonical limbs -> 48 big-endian bytes
+DG_FN void fp_std_to_be48(const fp& a, uint8_t* b) {
+#pragma unroll
+  for (int byte = 0; byte < 48; ++byte) {
+    int bit = byte * 8;
+    uint32_t v = a.l[bit / FP_BITS] >> (bit % FP_BITS);
+    if (bit % FP_BITS > FP_BITS - 8) v |= a.l[bit / FP_BITS + 1] << (FP_BITS - bit % FP_BITS);
+    b[47 - byte] = (uint8_t)v;
+  }
+}
+
+// a < p for standard normalized limbs
+DG_FN bool fp_std_lt_p(const fp& a) {
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) {
+    int32_t s = (int32_t)a.l[i] - (int32_t)FP_P[i] + c;
+    c = s >> FP_BITS;
+  }
+  return c < 0;
+}
+
+// a > (p-1)/2 for standard canonical limbs, i.e. 2a > p-1, i.e. 2a >= p
+DG_FN bool fp_std_gt_half(const fp& a) {
+  fp d;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) d.l[i] = a.l[i] << 1;
+  d = fp_norm(d);
+  return !fp_std_lt_p(d);
+}
+
+}  // namespace dgpu

@@ -1,0 +1,267 @@
+// SHA-256, drand's round digest, and RFC 9380 hash-to-curve
+// (BLS12381G2_XMD:SHA-256_SSWU_RO_) on the 32-bit integer VALU.
+//
+// Reference: chain/verify.go:24-32 (DigestMessage), key/curve.go:36 (G2
+// signatures hashed by kyber-bls12381 KyberG2.Hash -> kilic HashToCurve (R));
+// pinned bit-exactly by key/curve_test.go:10-30 through the oracle.
+#pragma once
+#include "curve.cuh"
+
+namespace dgpu {
+
+// ================================================================ SHA-256
+struct sha_state {
+  uint32_t h[8];
+};
+
+#ifdef __HIP_DEVICE_COMPILE__
+#define DG_ROTR(x, n) __builtin_amdgcn_alignbit((x), (x), (n))
+#else
+#define DG_ROTR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
+#endif
+
+__host__ __device__ constexpr uint32_t SHA_K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+DG_FN sha_state sha_init() {
+  return sha_state{{0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19}};
+}
+
+// One compression of a 16-word big-endian block.
+DG_NOINL void sha_compress(sha_state& s, const uint32_t* blk) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = blk[i];
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3], e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      uint32_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+      uint32_t s0 = DG_ROTR(w15, 7) ^ DG_ROTR(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = DG_ROTR(w2, 17) ^ DG_ROTR(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i + 9) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    uint32_t S1 = DG_ROTR(e, 6) ^ DG_ROTR(e, 11) ^ DG_ROTR(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + ch + SHA_K[i] + wi;
+    uint32_t S0 = DG_ROTR(a, 2) ^ DG_ROTR(a, 13) ^ DG_ROTR(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t t2 = S0 + mj;
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  s.h[0] += a;
+  s.h[1] += b;
+  s.h[2] += c;
+  s.h[3] += d;
+  s.h[4] += e;
+  s.h[5] += f;
+  s.h[6] += g;
+  s.h[7] += h;
+}
+
+// drand DigestMessage: SHA-256(prev[0..prev_len) || BE64(round)), or
+// SHA-256(BE64(round)) when prev_len == 0 (unchained / nil previous).
+// Arbitrary prev_len: the padded message is streamed block by block.
+DG_NOINL void drand_digest(uint32_t out[8], const uint8_t* prev, uint32_t prev_len, uint64_t round) {
+  sha_state s = sha_init();
+  uint32_t L = prev_len + 8;
+  uint32_t nblk = (L + 9 + 63) / 64;
+  uint64_t bitlen = (uint64_t)L * 8;
+  for (uint32_t bidx = 0; bidx < nblk; ++bidx) {
+    uint32_t blk[16];
+    for (int wd = 0; wd < 16; ++wd) {
+      uint32_t word = 0;
+      for (int byte = 0; byte < 4; ++byte) {
+        uint32_t pos = bidx * 64 + wd * 4 + byte;
+        uint32_t v;
+        if (pos < prev_len)
+          v = prev[pos];
+        else if (pos < L)
+          v = (uint32_t)(round >> (8 * (7 - (pos - prev_len)))) & 0xff;
+        else if (pos == L)
+          v = 0x80;
+        else if (pos >= nblk * 64 - 8)
+          v = (uint32_t)(bitlen >> (8 * (nblk * 64 - 1 - pos))) & 0xff;
+        else
+          v = 0;
+        word = (word << 8) | v;
+      }
+      blk[wd] = word;
+    }
+    sha_compress(s, blk);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = s.h[i];
+}
+
+// ================================================================ expand_message_xmd
+// DST bytes as big-endian words: "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_" (43 bytes)
+// followed by I2OSP(43, 1): DST_prime = 44 bytes = 11 words.
+__host__ __device__ constexpr uint32_t DST_G2_PRIME[11] = {0x424c535f, 0x5349475f, 0x424c5331, 0x32333831,
+                                                             0x47325f58, 0x4d443a53, 0x48412d32, 0x35365f53,
+                                                             0x5357555f, 0x524f5f4e, 0x554c5f2b};
+
+// expand_message_xmd(msg (32 bytes), DST_G2, 256) -> 64 big-endian words
+// Message layouts (bytes):
+//  b0: Z_pad(64) || msg(32) || 0x01 0x00 || 0x00 || DST'(44)  = 143 bytes, 3 blocks
+//  bi: x(32) || i(1) || DST'(44)                              =  77 bytes, 2 blocks
+DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) {
+  // b0
+  sha_state s0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0.h[i] = SHA_ZPAD_MIDSTATE[i];  // after the all-zero Z_pad block
+  {
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) blk[i] = msg[i];
+    // bytes 96..: 0x01 0x00 0x00 DST'[0]
+    blk[8] = 0x01000000u | (DST_G2_PRIME[0] >> 24);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) blk[8 + i] = (DST_G2_PRIME[i - 1] << 8) | (DST_G2_PRIME[i] >> 24);
+    sha_compress(s0, blk);
+    // remaining DST' bytes: DST'[29..43] (15 bytes), then 0x80, zeros, length 143*8 = 1144
+    uint32_t blk2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) blk2[i] = 0;
+    blk2[0] = (DST_G2_PRIME[7] << 8) | (DST_G2_PRIME[8] >> 24);
+    blk2[1] = (DST_G2_PRIME[8] << 8) | (DST_G2_PRIME[9] >> 24);
+    blk2[2] = (DST_G2_PRIME[9] << 8) | (DST_G2_PRIME[10] >> 24);
+    blk2[3] = (DST_G2_PRIME[10] << 8) | 0x80u;
+    blk2[15] = 143 * 8;
+    sha_compress(s0, blk2);
+  }
+  uint32_t b0[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b0[i] = s0.h[i];
+  uint32_t prev[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) prev[i] = 0;
+  for (int idx = 1; idx <= 8; ++idx) {
+    sha_state s = sha_init();
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) blk[i] = b0[i] ^ prev[i];
+    blk[8] = ((uint32_t)idx << 24) | (DST_G2_PRIME[0] >> 8);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) blk[8 + i] = (DST_G2_PRIME[i - 1] << 24) | (DST_G2_PRIME[i] >> 8);
+    sha_compress(s, blk);
+    // bytes 64..76: DST'[31..43] (13 bytes), 0x80, zeros, length 77*8 = 616
+    uint32_t blk2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) blk2[i] = 0;
+    blk2[0] = (DST_G2_PRIME[7] << 24) | (DST_G2_PRIME[8] >> 8);
+    blk2[1] = (DST_G2_PRIME[8] << 24) | (DST_G2_PRIME[9] >> 8);
+    blk2[2] = (DST_G2_PRIME[9] << 24) | (DST_G2_PRIME[10] >> 8);
+    blk2[3] = (DST_G2_PRIME[10] << 24) | 0x00800000u;
+    blk2[15] = 77 * 8;
+    sha_compress(s, blk2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      prev[i] = s.h[i];
+      out[(idx - 1) * 8 + i] = s.h[i];
+    }
+  }
+}
+
+// 64 big-endian bytes (as 16 BE words) -> Fp (Montgomery): x = hi * 2^384 + lo
+DG_NOINL fp fp_from_be64_words(const uint32_t* w) {
+  uint8_t bytes[64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    bytes[4 * i] = (uint8_t)(w[i] >> 24);
+    bytes[4 * i + 1] = (uint8_t)(w[i] >> 16);
+    bytes[4 * i + 2] = (uint8_t)(w[i] >> 8);
+    bytes[4 * i + 3] = (uint8_t)w[i];
+  }
+  uint8_t hi48[48];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) hi48[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) hi48[32 + i] = bytes[i];
+  fp lo = fp_std_from_be48(bytes + 16);
+  fp hi = fp_std_from_be48(hi48);
+  return fp_add(fp_mul(lo, FP_R2), fp_mul(hi, FP_2_384_R2));
+}
+
+DG_FN void hash_to_field_g2(fp2& u0, fp2& u1, const uint32_t msg[8]) {
+  uint32_t uni[64];
+  expand_xmd_g2(uni, msg);
+  u0.c0 = fp_from_be64_words(uni + 0);
+  u0.c1 = fp_from_be64_words(uni + 16);
+  u1.c0 = fp_from_be64_words(uni + 32);
+  u1.c1 = fp_from_be64_words(uni + 48);
+}
+
+// ================================================================ SSWU + 3-isogeny
+// Simplified SWU on E2': y^2 = x^3 + A'x + B' (RFC 9380 section 6.6.2).
+DG_NOINL g2a map_to_curve_sswu_g2(const fp2& u) {
+  fp2 u2 = fp2_sqr(u);
+  fp2 zu2 = fp2_mul(C_SSWU_Z, u2);
+  fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+  bool den0 = fp2_is_zero(den);
+  fp2 tv1 = fp2_inv(den);
+  fp2 x1 = fp2_mul(C_SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), tv1));
+  x1 = fp2_cmov(x1, C_SSWU_B_OVER_ZA, den0);
+  fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), C_SSWU_A), x1), C_SSWU_B);
+  fp2 x2 = fp2_mul(zu2, x1);
+  fp2 gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x2), C_SSWU_A), x2), C_SSWU_B);
+  bool e1 = fp2_is_square(gx1);
+  fp2 x = fp2_cmov(x2, x1, e1);
+  fp2 gx = fp2_cmov(gx2, gx1, e1);
+  fp2 y;
+  fp2_sqrt(y, gx);  // gx is a square by construction
+  if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
+  return g2a{x, y};
+}
+
+// 3-isogeny E2' -> E2 evaluated projectively (no inversion): with
+// x = xn/xd and y = y' yn/yd, choose Z = xd*yd so that
+// X = xn xd yd^2, Y = y' yn xd^3 yd^2.
+DG_NOINL g2j iso3_map(const g2a& p) {
+  const fp2& x = p.x;
+  fp2 x2 = fp2_sqr(x);
+  fp2 x3 = fp2_mul(x2, x);
+  fp2 xn = fp2_add(fp2_add(fp2_mul(C_ISO3_XNUM_3, x3), fp2_mul(C_ISO3_XNUM_2, x2)),
+                   fp2_add(fp2_mul(C_ISO3_XNUM_1, x), C_ISO3_XNUM_0));
+  fp2 xd = fp2_add(fp2_add(x2, fp2_mul(C_ISO3_XDEN_1, x)), C_ISO3_XDEN_0);
+  fp2 yn = fp2_add(fp2_add(fp2_mul(C_ISO3_YNUM_3, x3), fp2_mul(C_ISO3_YNUM_2, x2)),
+                   fp2_add(fp2_mul(C_ISO3_YNUM_1, x), C_ISO3_YNUM_0));
+  fp2 yd = fp2_add(fp2_add(x3, fp2_mul(C_ISO3_YDEN_2, x2)), fp2_add(fp2_mul(C_ISO3_YDEN_1, x), C_ISO3_YDEN_0));
+  fp2 yd2 = fp2_sqr(yd);
+  fp2 xdyd2 = fp2_mul(xd, yd2);
+  g2j r;
+  r.z = fp2_mul(xd, yd);
+  r.x = fp2_mul(xn, xdyd2);
+  r.y = fp2_mul(fp2_mul(p.y, yn), fp2_mul(fp2_sqr(xd), xdyd2));
+  // an exceptional input (xd or yd = 0) maps to the identity (RFC 9380 section 6.6.3)
+  return r;
+}
+
+// hash_to_curve for G2 from the 32-byte drand digest; returns Jacobian H(m)
+DG_NOINL g2j hash_to_g2(const uint32_t msg[8]) {
+  fp2 u0, u1;
+  hash_to_field_g2(u0, u1, msg);
+  g2j q0 = iso3_map(map_to_curve_sswu_g2(u0));
+  g2j q1 = iso3_map(map_to_curve_sswu_g2(u1));
+  return g2_clear_cofactor(g2_add(q0, q1));
+}
+
+}  // namespace dgpu

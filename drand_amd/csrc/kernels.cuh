@@ -1,0 +1,211 @@
+// Batch kernels: one thread per beacon round.  Intermediate points live in
+// HBM as structure-of-arrays ([limb][round], round fastest) so every limb
+// load/store of a wavefront is one coalesced 256-byte access.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "h2c.cuh"
+#include "pairing.cuh"
+
+namespace dgpu {
+
+constexpr int FP_WORDS = FP_LIMBS;          // 14 dwords per Fp in HBM
+constexpr int G2A_WORDS = 4 * FP_WORDS;     // affine G2 point
+
+__device__ __forceinline__ void st_fp(uint32_t* base, size_t n, size_t i, const fp& a) {
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) base[(size_t)k * n + i] = a.l[k];
+}
+__device__ __forceinline__ fp ld_fp(const uint32_t* base, size_t n, size_t i) {
+  fp a;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) a.l[k] = base[(size_t)k * n + i];
+  return a;
+}
+__device__ __forceinline__ void st_g2a(uint32_t* base, size_t n, size_t i, const g2a& p) {
+  st_fp(base, n, i, p.x.c0);
+  st_fp(base + FP_WORDS * n, n, i, p.x.c1);
+  st_fp(base + 2 * FP_WORDS * n, n, i, p.y.c0);
+  st_fp(base + 3 * FP_WORDS * n, n, i, p.y.c1);
+}
+__device__ __forceinline__ g2a ld_g2a(const uint32_t* base, size_t n, size_t i) {
+  g2a p;
+  p.x.c0 = ld_fp(base, n, i);
+  p.x.c1 = ld_fp(base + FP_WORDS * n, n, i);
+  p.y.c0 = ld_fp(base + 2 * FP_WORDS * n, n, i);
+  p.y.c1 = ld_fp(base + 3 * FP_WORDS * n, n, i);
+  return p;
+}
+
+// per-round status codes carried between kernels (also the public `reason`)
+enum : uint8_t {
+  ST_OK = 0,
+  ST_DECODE = 1,    // wrong length / flags / x >= p / not on curve / non-canonical infinity
+  ST_SUBGROUP = 2,  // point not in the r-order subgroup
+  ST_PAIRING = 3,   // e(pk, H(m)) != e(g1, sig)
+  ST_INFINITY = 4,  // signature is the point at infinity (pairing check fails)
+};
+
+struct g1_key {  // public key prepared for line evaluation: (-x, y), Montgomery
+  fp neg_x, y;
+};
+
+// ---------------------------------------------------------------- kernels
+// H(m) for m = DigestMessage(round, prev) (chain/verify.go:24-32).
+// chained != 0: prev bytes are hashed (any length up to prev_stride).
+__global__ void __launch_bounds__(256) k_hash_to_g2_beacons(size_t n, const uint64_t* __restrict__ rounds,
+                                                             const uint8_t* __restrict__ prev, size_t prev_stride,
+                                                             const uint32_t* __restrict__ prev_len, int chained,
+                                                             uint32_t* __restrict__ h_out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t msg[8];
+  uint32_t plen = chained ? prev_len[i] : 0u;
+  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, plen, rounds[i]);
+  g2j h = hash_to_g2(msg);
+  st_g2a(h_out, n, i, g2_to_affine(h));
+}
+
+// H(m) for raw 32-byte messages (parity/debug: dgpu_hash_to_g2)
+__global__ void __launch_bounds__(256) k_hash_to_g2_msgs(size_t n, const uint8_t* __restrict__ msgs,
+                                                          uint8_t* __restrict__ out96) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t msg[8];
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* b = msgs + i * 32 + 4 * w;
+    msg[w] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+  }
+  g2j h = hash_to_g2(msg);
+  bool inf = g2_is_inf(h);
+  g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h);
+  g2_compress(out96 + i * 96, a, inf);
+}
+
+// drand digests only (parity/debug: dgpu_digest)
+__global__ void __launch_bounds__(256) k_digest(size_t n, const uint64_t* __restrict__ rounds,
+                                                 const uint8_t* __restrict__ prev, size_t prev_stride,
+                                                 const uint32_t* __restrict__ prev_len, int chained,
+                                                 uint8_t* __restrict__ out32) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t msg[8];
+  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, chained ? prev_len[i] : 0u, rounds[i]);
+  for (int w = 0; w < 8; ++w) {
+    out32[i * 32 + 4 * w] = (uint8_t)(msg[w] >> 24);
+    out32[i * 32 + 4 * w + 1] = (uint8_t)(msg[w] >> 16);
+    out32[i * 32 + 4 * w + 2] = (uint8_t)(msg[w] >> 8);
+    out32[i * 32 + 4 * w + 3] = (uint8_t)msg[w];
+  }
+}
+
+// Signature decode (kilic G2.FromCompressed semantics (R)) + G2 membership.
+__global__ void __launch_bounds__(256) k_decode_g2_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
+                                                         const uint32_t* __restrict__ sig_len,
+                                                         uint32_t* __restrict__ sig_out, uint8_t* __restrict__ status) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st;
+  g2a p{fp2_zero(), fp2_zero()};
+  if (sig_len[i] != 96) {
+    st = ST_DECODE;
+  } else {
+    uint8_t buf[96];
+    const uint8_t* src = sigs + i * sig_stride;
+    for (int k = 0; k < 96; ++k) buf[k] = src[k];
+    int rc = g2_decompress(&p, buf, true);
+    st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
+  }
+  st_g2a(sig_out, n, i, p);
+  status[i] = st;
+}
+
+// e(pk, H) * e(-g1, sig) == 1 per round.
+__global__ void __launch_bounds__(256) k_pairing_check(size_t n, const uint32_t* __restrict__ h_pts,
+                                                        const uint32_t* __restrict__ sig_pts,
+                                                        uint8_t* __restrict__ status, g1_key pk) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st = status[i];
+  if (st != ST_OK) return;  // decode verdicts are final
+  g2a h = ld_g2a(h_pts, n, i);
+  g2a s = ld_g2a(sig_pts, n, i);
+  fp g1_negx = fp_neg(C_G1_X);
+  // pair 2 is (-g1, sig): (-x(-g1), y(-g1)) = (-x_g1, -y_g1)
+  fp12 f = miller_loop_2(h, pk.neg_x, pk.y, s, g1_negx, C_G1_NEG_Y);
+  fp12 e = final_exponentiation(f);
+  status[i] = fp12_is_one(e) ? ST_OK : ST_PAIRING;
+}
+
+// Synthetic-chain generator (test-data tool, not the verify path): one step
+// of S independent chained segments, following the reference's fixture
+// generator client/test/result/mock/result.go:86-130 (msg = DigestMessage,
+// sig = sk * H(msg), previous = sig).  Segment s signs round first_round[s] + step
+// over prev (prev_len[s] bytes at prev + s*96) and writes the 96-byte
+// signature to sig_out + s*96 and to prev (for the next step).
+struct scalar256 {
+  uint32_t w[8];
+};
+__global__ void __launch_bounds__(256) k_sign_step(size_t S, const uint64_t* __restrict__ first_round, uint64_t step,
+                                                    uint8_t* __restrict__ prev, uint32_t* __restrict__ prev_len,
+                                                    int chained, scalar256 sk, uint8_t* __restrict__ sig_out,
+                                                    size_t sig_stride) {
+  size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  uint32_t msg[8];
+  uint8_t pb[96];
+  uint32_t plen = chained ? prev_len[s] : 0u;
+  for (uint32_t k = 0; k < plen && k < 96; ++k) pb[k] = prev[s * 96 + k];
+  drand_digest(msg, pb, plen, first_round[s] + step);
+  g2j h = hash_to_g2(msg);
+  g2j sg = g2_mul_words(h, sk.w, 8);
+  bool inf = g2_is_inf(sg);
+  g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(sg);
+  uint8_t out[96];
+  g2_compress(out, a, inf);
+  for (int k = 0; k < 96; ++k) {
+    sig_out[s * sig_stride + k] = out[k];
+    prev[s * 96 + k] = out[k];
+  }
+  prev_len[s] = 96;
+}
+
+// pk = sk * g1, compressed (synthetic-chain tool)
+__global__ void k_derive_pubkey(scalar256 sk, uint8_t* __restrict__ out48) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  g1j g{C_G1_X, C_G1_Y, fp_one()};
+  g1j p = g1_mul_words(g, sk.w, 8);
+  bool inf = g1_is_inf(p);
+  g1a a = inf ? g1a{fp_zero(), fp_zero()} : g1_to_affine(p);
+  uint8_t out[48];
+  g1_compress(out, a, inf);
+  for (int k = 0; k < 48; ++k) out48[k] = out[k];
+}
+
+// status -> verdict bitmap (bit = 1 valid), one thread per output byte
+__global__ void k_pack_verdicts(size_t n, const uint8_t* __restrict__ status, uint8_t* __restrict__ bits) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j * 8 >= n) return;
+  uint8_t b = 0;
+  for (int k = 0; k < 8; ++k) {
+    size_t i = j * 8 + k;
+    if (i < n && status[i] == ST_OK) b |= (uint8_t)(1u << k);
+  }
+  bits[j] = b;
+}
+
+// Public key decode (48-byte compressed G1, kilic G1.FromCompressed (R)) on one thread.
+__global__ void k_decode_g1_pk(const uint8_t* __restrict__ in48, uint32_t* __restrict__ out, int* __restrict__ rc) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint8_t buf[48];
+  for (int k = 0; k < 48; ++k) buf[k] = in48[k];
+  g1a p{fp_zero(), fp_zero()};
+  int r = g1_decompress(&p, buf, GROUP_ORDER_WORDS);
+  fp nx = fp_neg(p.x);
+  for (int k = 0; k < FP_LIMBS; ++k) {
+    out[k] = nx.l[k];
+    out[FP_LIMBS + k] = p.y.l[k];
+  }
+  *rc = r;
+}
+
+}  // namespace dgpu

@@ -1,0 +1,276 @@
+// Extension tower for BLS12-381:
+//   Fp2  = Fp[u]  / (u^2 + 1)
+//   Fp6  = Fp2[v] / (v^3 - xi),  xi = 1 + u
+//   Fp12 = Fp6[w] / (w^2 - v)
+// Same tower and basis as the oracle (oracle/bls12381.py), so intermediate
+// values can be compared element by element.
+#pragma once
+#include "fp.cuh"
+
+namespace dgpu {
+
+struct fp2 {
+  fp c0, c1;
+};
+#define FP2_CONST(a, b) ::dgpu::fp2{a, b}
+
+struct fp6 {
+  fp2 c0, c1, c2;
+};
+struct fp12 {
+  fp6 c0, c1;
+};
+
+// ================================================================ Fp2
+DG_FN fp2 fp2_zero() { return fp2{fp_zero(), fp_zero()}; }
+DG_FN fp2 fp2_one() { return fp2{fp_one(), fp_zero()}; }
+DG_FN fp2 fp2_add(const fp2& a, const fp2& b) { return fp2{fp_add(a.c0, b.c0), fp_add(a.c1, b.c1)}; }
+DG_FN fp2 fp2_sub(const fp2& a, const fp2& b) { return fp2{fp_sub(a.c0, b.c0), fp_sub(a.c1, b.c1)}; }
+DG_FN fp2 fp2_neg(const fp2& a) { return fp2{fp_neg(a.c0), fp_neg(a.c1)}; }
+DG_FN fp2 fp2_dbl(const fp2& a) { return fp2_add(a, a); }
+DG_FN fp2 fp2_conj(const fp2& a) { return fp2{a.c0, fp_neg(a.c1)}; }
+DG_FN fp2 fp2_half(const fp2& a) { return fp2{fp_half(a.c0), fp_half(a.c1)}; }
+
+// Karatsuba: 3 Fp multiplications.  Lazy sums feed the third product
+// (limbs < 2^29, values < 4.02p: inside fp_mul's bounds); c1's subtrahend is
+// an unnormalized sum of two CI values, handled by fp_sub2_lz.
+DG_NOINL fp2 fp2_mul(const fp2& a, const fp2& b) {
+  fp t0 = fp_mul(a.c0, b.c0);
+  fp t1 = fp_mul(a.c1, b.c1);
+  fp t2 = fp_mul(fp_add_lz(a.c0, a.c1), fp_add_lz(b.c0, b.c1));
+  fp2 r;
+  r.c0 = fp_sub(t0, t1);
+  r.c1 = fp_reduce(fp_norm(fp_sub2_lz(t2, fp_add_lz(t0, t1))));
+  return r;
+}
+
+// (a0 + a1 u)^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u
+DG_NOINL fp2 fp2_sqr(const fp2& a) {
+  fp2 r;
+  r.c0 = fp_mul(fp_add_lz(a.c0, a.c1), fp_sub_lz(a.c0, a.c1));
+  r.c1 = fp_mul(fp_add_lz(a.c0, a.c0), a.c1);
+  return r;
+}
+
+DG_FN fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
+
+// multiply by xi = 1 + u: (a0 - a1) + (a0 + a1) u
+DG_FN fp2 fp2_mul_xi(const fp2& a) { return fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
+
+DG_FN fp2 fp2_cmov(const fp2& a, const fp2& b, bool take_b) {
+  return fp2{fp_cmov(a.c0, b.c0, take_b), fp_cmov(a.c1, b.c1, take_b)};
+}
+
+DG_FN bool fp2_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+DG_FN bool fp2_eq(const fp2& a, const fp2& b) { return fp2_is_zero(fp2_sub(a, b)); }
+
+DG_FN fp fp2_norm(const fp2& a) { return fp_add(fp_sqr(a.c0), fp_sqr(a.c1)); }
+
+DG_NOINL fp2 fp2_inv(const fp2& a) {
+  fp t = fp_inv(fp2_norm(a));
+  return fp2{fp_mul(a.c0, t), fp_neg(fp_mul(a.c1, t))};
+}
+
+// square test in Fp2: a is a square iff its norm is a square in Fp
+DG_FN bool fp2_is_square(const fp2& a) { return fp_is_square(fp2_norm(a)); }
+
+// Square root in Fp2 (p = 3 mod 4) by the norm method.  Returns false if a is
+// not a square.  Which of the two roots is returned does not matter: every
+// caller fixes the sign afterwards (RFC 9380 sgn0 / ZCash sign bit).
+DG_NOINL bool fp2_sqrt(fp2& out, const fp2& a) {
+  if (fp_is_zero(a.c1)) {
+    fp s = fp_sqrt_cand(a.c0);
+    if (fp_eq(fp_sqr(s), a.c0)) {
+      out = fp2{s, fp_zero()};
+      return true;
+    }
+    fp na = fp_neg(a.c0);
+    s = fp_sqrt_cand(na);
+    out = fp2{fp_zero(), s};
+    return fp_eq(fp_sqr(s), na);
+  }
+  fp alpha = fp2_norm(a);
+  fp g = fp_sqrt_cand(alpha);
+  if (!fp_eq(fp_sqr(g), alpha)) return false;
+  fp d = fp_half(fp_add(a.c0, g));
+  fp x0 = fp_sqrt_cand(d);
+  if (!fp_eq(fp_sqr(x0), d)) {
+    d = fp_half(fp_sub(a.c0, g));
+    x0 = fp_sqrt_cand(d);
+  }
+  fp x1 = fp_mul(a.c1, fp_inv(fp_dbl(x0)));
+  out = fp2{x0, x1};
+  return fp2_eq(fp2_sqr(out), a);
+}
+
+// canonical (non-Montgomery) components
+DG_FN void fp2_from_mont(fp& c0, fp& c1, const fp2& a) {
+  c0 = fp_from_mont(a.c0);
+  c1 = fp_from_mont(a.c1);
+}
+
+// RFC 9380 sgn0 for Fp2
+DG_NOINL uint32_t fp2_sgn0(const fp2& a) {
+  fp c0, c1;
+  fp2_from_mont(c0, c1, a);
+  uint32_t s0 = c0.l[0] & 1u;
+  uint32_t z0 = fp_is_zero_std(c0) ? 1u : 0u;
+  uint32_t s1 = c1.l[0] & 1u;
+  return s0 | (z0 & s1);
+}
+
+// ZCash "lexicographically largest" for Fp2 y
+DG_NOINL bool fp2_lexi_largest(const fp2& a) {
+  fp c0, c1;
+  fp2_from_mont(c0, c1, a);
+  if (!fp_is_zero_std(c1)) return fp_std_gt_half(c1);
+  return fp_std_gt_half(c0);
+}
+
+DG_FN fp2 fp2_frob(const fp2& a) { return fp2_conj(a); }
+
+// ================================================================ Fp6
+DG_FN fp6 fp6_zero() { return fp6{fp2_zero(), fp2_zero(), fp2_zero()}; }
+DG_FN fp6 fp6_one() { return fp6{fp2_one(), fp2_zero(), fp2_zero()}; }
+DG_NOINL fp6 fp6_add(const fp6& a, const fp6& b) {
+  return fp6{fp2_add(a.c0, b.c0), fp2_add(a.c1, b.c1), fp2_add(a.c2, b.c2)};
+}
+DG_NOINL fp6 fp6_sub(const fp6& a, const fp6& b) {
+  return fp6{fp2_sub(a.c0, b.c0), fp2_sub(a.c1, b.c1), fp2_sub(a.c2, b.c2)};
+}
+DG_NOINL fp6 fp6_neg(const fp6& a) { return fp6{fp2_neg(a.c0), fp2_neg(a.c1), fp2_neg(a.c2)}; }
+
+// Karatsuba-style, 6 Fp2 multiplications (same formula as the oracle's f6_mul)
+DG_NOINL fp6 fp6_mul(const fp6& a, const fp6& b) {
+  fp2 t0 = fp2_mul(a.c0, b.c0);
+  fp2 t1 = fp2_mul(a.c1, b.c1);
+  fp2 t2 = fp2_mul(a.c2, b.c2);
+  fp6 r;
+  r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
+  r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  return r;
+}
+
+DG_FN fp6 fp6_sqr(const fp6& a) { return fp6_mul(a, a); }
+
+// multiply by v: (a0, a1, a2) -> (xi a2, a0, a1)
+DG_FN fp6 fp6_mul_v(const fp6& a) { return fp6{fp2_mul_xi(a.c2), a.c0, a.c1}; }
+
+DG_FN fp6 fp6_mul_fp2(const fp6& a, const fp2& s) {
+  return fp6{fp2_mul(a.c0, s), fp2_mul(a.c1, s), fp2_mul(a.c2, s)};
+}
+
+// a * (b0 + b1 v)   (sparse: b2 = 0)
+DG_NOINL fp6 fp6_mul_01(const fp6& a, const fp2& b0, const fp2& b1) {
+  fp2 t0 = fp2_mul(a.c0, b0);
+  fp2 t1 = fp2_mul(a.c1, b1);
+  fp6 r;
+  // c0 = t0 + xi * (a2 * b1)
+  r.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, b1)));
+  // c1 = (a0 + a1)(b0 + b1) - t0 - t1
+  r.c1 = fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b0, b1)), fp2_add(t0, t1));
+  // c2 = a2 * b0 + t1
+  r.c2 = fp2_add(fp2_mul(a.c2, b0), t1);
+  return r;
+}
+
+// a * (b1 v)   (sparse: only b1)
+DG_NOINL fp6 fp6_mul_1(const fp6& a, const fp2& b1) {
+  return fp6{fp2_mul_xi(fp2_mul(a.c2, b1)), fp2_mul(a.c0, b1), fp2_mul(a.c1, b1)};
+}
+
+DG_NOINL fp6 fp6_inv(const fp6& a) {
+  fp2 t0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  fp2 t1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  fp2 t2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  fp2 d = fp2_add(fp2_mul(a.c0, t0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, t1), fp2_mul(a.c1, t2))));
+  fp2 di = fp2_inv(d);
+  return fp6{fp2_mul(t0, di), fp2_mul(t1, di), fp2_mul(t2, di)};
+}
+
+// ================================================================ Fp12
+DG_FN fp12 fp12_one() { return fp12{fp6_one(), fp6_zero()}; }
+
+DG_NOINL fp12 fp12_mul(const fp12& a, const fp12& b) {
+  fp6 t0 = fp6_mul(a.c0, b.c0);
+  fp6 t1 = fp6_mul(a.c1, b.c1);
+  fp12 r;
+  r.c1 = fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), fp6_add(t0, t1));
+  r.c0 = fp6_add(t0, fp6_mul_v(t1));
+  return r;
+}
+
+// complex squaring: 2 Fp6 multiplications
+DG_NOINL fp12 fp12_sqr(const fp12& a) {
+  fp6 ab = fp6_mul(a.c0, a.c1);
+  fp6 t = fp6_mul(fp6_add(a.c0, a.c1), fp6_add(a.c0, fp6_mul_v(a.c1)));
+  fp12 r;
+  r.c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_v(ab));
+  r.c1 = fp6_add(ab, ab);
+  return r;
+}
+
+DG_FN fp12 fp12_conj(const fp12& a) { return fp12{a.c0, fp6_neg(a.c1)}; }
+
+DG_NOINL fp12 fp12_inv(const fp12& a) {
+  fp6 t = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
+  fp6 ti = fp6_inv(t);
+  return fp12{fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti))};
+}
+
+// Multiply by a Miller-loop line l = c0 + c2 w^2 + c3 w^3
+//   = (c0 + c2 v) + (c3 v) w   in the Fp6[w] basis.
+DG_NOINL fp12 fp12_mul_line(const fp12& f, const fp2& c0, const fp2& c2, const fp2& c3) {
+  // (f0 + f1 w)(L0 + L1 w) = (f0 L0 + v f1 L1) + (f0 L1 + f1 L0) w,  L0 = c0 + c2 v, L1 = c3 v
+  fp6 a = fp6_mul_01(f.c0, c0, c2);
+  fp6 b = fp6_mul_1(f.c1, c3);
+  fp12 r;
+  // (f0 + f1)(L0 + L1) - a - b
+  fp2 s1 = fp2_add(c2, c3);
+  r.c1 = fp6_sub(fp6_mul_01(fp6_add(f.c0, f.c1), c0, s1), fp6_add(a, b));
+  r.c0 = fp6_add(a, fp6_mul_v(b));
+  return r;
+}
+
+// Frobenius maps f -> f^(p^k), k = 1, 2, 3, on the w-basis coefficients.
+// Basis order: 1 -> c0.c0, w -> c1.c0, w^2 -> c0.c1, w^3 -> c1.c1, w^4 -> c0.c2, w^5 -> c1.c2
+DG_NOINL fp12 fp12_frob1(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = fp2_conj(a.c0.c0);
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), C_FROB1_1);
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), C_FROB1_2);
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), C_FROB1_3);
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), C_FROB1_4);
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), C_FROB1_5);
+  return r;
+}
+
+DG_NOINL fp12 fp12_frob2(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = a.c0.c0;
+  r.c1.c0 = fp2_mul_fp(a.c1.c0, fp2(C_FROB2_1).c0);
+  r.c0.c1 = fp2_mul_fp(a.c0.c1, fp2(C_FROB2_2).c0);
+  r.c1.c1 = fp2_mul_fp(a.c1.c1, fp2(C_FROB2_3).c0);
+  r.c0.c2 = fp2_mul_fp(a.c0.c2, fp2(C_FROB2_4).c0);
+  r.c1.c2 = fp2_mul_fp(a.c1.c2, fp2(C_FROB2_5).c0);
+  return r;
+}
+
+DG_NOINL fp12 fp12_frob3(const fp12& a) {
+  fp12 r;
+  r.c0.c0 = fp2_conj(a.c0.c0);
+  r.c1.c0 = fp2_mul(fp2_conj(a.c1.c0), C_FROB3_1);
+  r.c0.c1 = fp2_mul(fp2_conj(a.c0.c1), C_FROB3_2);
+  r.c1.c1 = fp2_mul(fp2_conj(a.c1.c1), C_FROB3_3);
+  r.c0.c2 = fp2_mul(fp2_conj(a.c0.c2), C_FROB3_4);
+  r.c1.c2 = fp2_mul(fp2_conj(a.c1.c2), C_FROB3_5);
+  return r;
+}
+
+DG_NOINL bool fp12_is_one(const fp12& a) {
+  return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp2_is_zero(a.c1.c0) &&
+         fp2_is_zero(a.c1.c1) && fp2_is_zero(a.c1.c2);
+}
+
+}  // namespace dgpu

@@ -1,0 +1,154 @@
+"""Deterministic synthetic drand chains, generated on
+the GPU through the C-ABI (dgpu_derive_pubkey / dgpu_make_chain), following the
+reference's fixture generator client/test/result/mock/result.go:86-130.
+
+A chain of n rounds is built as `n_seg` independently signed segments of
+`seg_len` rounds: inside a segment PreviousSig is the previous round's
+signature (real linkage); the first round of segment 0 links to the genesis
+seed and the first round of every other segment links to a 32-byte
+seed-derived value instead of the previous segment's last signature (the
+chain is serial, so a single segment of 1M rounds would take ~1M dependent
+signing steps).  VerifyBeacon hashes PreviousSig as opaque bytes
+(chain/verify.go:24-32), so every round costs the verifier exactly what a
+fully linked chain's round costs.
+"""
+import hashlib
+import struct
+
+import numpy as np
+
+from . import _lib
+from .chain import get_context
+
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def derive_secret(seed):
+    """sk = OS2IP(SHA-256("drand-mi355x/sk/" || LE64(s0))) mod r."""
+    d = hashlib.sha256(b"drand-mi355x/sk/" + struct.pack("<Q", seed)).digest()
+    return int.from_bytes(d, "big") % R_ORDER
+
+
+def derive_genesis(seed):
+    """genesis = SHA-256("drand-mi355x/genesis/" || LE64(s0))."""
+    return hashlib.sha256(b"drand-mi355x/genesis/" + struct.pack("<Q", seed)).digest()
+
+
+def segment_seed(seed, s):
+    if s == 0:
+        return derive_genesis(seed)
+    return hashlib.sha256(b"drand-mi355x/segment/" + struct.pack("<QQ", seed, s)).digest()
+
+
+class Chain:
+    """Structure-of-arrays chain: rounds (n,), sigs (n, 96), prev (n, 96), prev_len (n,)."""
+
+    def __init__(self, scheme_code, pk, rounds, sigs, sig_len, prev, prev_len, genesis):
+        self.scheme_code = scheme_code
+        self.pk = pk
+        self.rounds = rounds
+        self.sigs = sigs
+        self.sig_len = sig_len
+        self.prev = prev
+        self.prev_len = prev_len
+        self.genesis = genesis
+
+    def __len__(self):
+        return len(self.rounds)
+
+    def beacon(self, i):
+        from .chain import Beacon
+        return Beacon(bytes(self.prev[i, : self.prev_len[i]]), int(self.rounds[i]),
+                      bytes(self.sigs[i, : self.sig_len[i]]))
+
+
+def make_chain(seed, n, scheme_code=_lib.SCHEME_CHAINED, seg_len=64, device=0, start_round=1):
+    """n rounds starting at `start_round`, in segments of `seg_len` rounds."""
+    ctx = get_context(device)
+    lib = ctx.lib
+    sk = derive_secret(seed).to_bytes(32, "big")
+    pk = np.zeros(48, dtype=np.uint8)
+    skb = np.frombuffer(sk, dtype=np.uint8).copy()
+    _lib.check(lib.dgpu_derive_pubkey(ctx.handle, scheme_code, _lib.ptr(skb), _lib.ptr(pk), 48))
+    seg_len = max(1, min(seg_len, n))
+    n_seg = (n + seg_len - 1) // seg_len
+    first = (start_round + np.arange(n_seg, dtype=np.uint64) * seg_len).astype(np.uint64)
+    seeds = np.zeros((n_seg, 96), dtype=np.uint8)
+    seed_len = np.full(n_seg, 32, dtype=np.uint32)
+    for s in range(n_seg):
+        seeds[s, :32] = np.frombuffer(segment_seed(seed, s + (start_round - 1) // seg_len), dtype=np.uint8)
+    out = np.zeros((n_seg * seg_len, 96), dtype=np.uint8)
+    _lib.check(lib.dgpu_make_chain(ctx.handle, scheme_code, _lib.ptr(skb), n_seg, seg_len, _lib.ptr(first),
+                                   _lib.ptr(seeds), _lib.ptr(seed_len), _lib.ptr(out)))
+    out = out[:n]
+    rounds = (start_round + np.arange(n, dtype=np.uint64)).astype(np.uint64)
+    prev = np.zeros((n, 96), dtype=np.uint8)
+    prev_len = np.zeros(n, dtype=np.uint32)
+    if scheme_code == _lib.SCHEME_CHAINED:
+        prev[1:] = out[:-1]
+        prev_len[:] = 96
+        starts = np.arange(0, n, seg_len)
+        prev[starts] = seeds[: len(starts)]
+        prev_len[starts] = 32
+    sig_len = np.full(n, 96, dtype=np.uint32)
+    return Chain(scheme_code, bytes(pk), rounds, out.copy(), sig_len, prev, prev_len, derive_genesis(seed))
+
+
+# ---------------------------------------------------------------- corruption catalog
+CORRUPT_X_BIT = 1        # (i) bit flip in x -> off curve / off subgroup -> decode failure
+CORRUPT_Y_SIGN = 2       # (ii) y-sign flipped (valid point -sigma) -> pairing failure
+CORRUPT_OTHER_ROUND = 3  # (iii) signature of another round -> pairing failure
+CORRUPT_PREV = 4         # (iv) PreviousSig altered (chained) -> pairing failure
+CORRUPT_INFINITY = 5     # (v) canonical infinity -> failure
+CORRUPT_TRUNCATED = 6    # (vi) empty / truncated signature -> decode failure
+ALL_CORRUPTIONS = (CORRUPT_X_BIT, CORRUPT_Y_SIGN, CORRUPT_OTHER_ROUND, CORRUPT_PREV, CORRUPT_INFINITY,
+                   CORRUPT_TRUNCATED)
+
+
+def splitmix64(x):
+    x = (x + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = x
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x, z ^ (z >> 31)
+
+
+def corrupt(chain, seed, rate=1e-3, kinds=ALL_CORRUPTIONS):
+    """Corrupt ~rate*n rounds in place (at least one of each kind).  Returns
+    {index: kind}; every other round is valid by construction."""
+    n = len(chain)
+    count = max(len(kinds), int(round(n * rate)))
+    state = (seed ^ 0xC0FFEE) & 0xFFFFFFFFFFFFFFFF
+    chosen = {}
+    chained = chain.scheme_code == _lib.SCHEME_CHAINED
+    k = 0
+    while len(chosen) < min(count, n):
+        state, r = splitmix64(state)
+        i = r % n
+        if i in chosen:
+            continue
+        kind = kinds[k % len(kinds)]
+        k += 1
+        if kind == CORRUPT_PREV and not chained:
+            kind = CORRUPT_Y_SIGN
+        if kind == CORRUPT_OTHER_ROUND and n < 2:
+            kind = CORRUPT_Y_SIGN
+        chosen[int(i)] = kind
+    for i, kind in chosen.items():
+        if kind == CORRUPT_X_BIT:
+            chain.sigs[i, 47] ^= 0x01
+        elif kind == CORRUPT_Y_SIGN:
+            chain.sigs[i, 0] ^= 0x20
+        elif kind == CORRUPT_OTHER_ROUND:
+            j = (i + 1) % n
+            chain.sigs[i] = chain.sigs[j].copy()
+            if j in chosen:  # keep the donor's original bytes irrelevant: any non-matching valid point fails
+                pass
+        elif kind == CORRUPT_PREV:
+            chain.prev[i, 0] ^= 0x01
+        elif kind == CORRUPT_INFINITY:
+            chain.sigs[i] = 0
+            chain.sigs[i, 0] = 0xC0
+        elif kind == CORRUPT_TRUNCATED:
+            chain.sig_len[i] = 48 if (i & 1) else 0
+    return chosen

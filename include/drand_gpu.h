@@ -1,0 +1,140 @@
+/*
+ * drand_gpu.h -- C ABI of the MI355X batch beacon verifier (libdrand_gpu.so).
+ *
+ * Drop-in boundary for drand's verification path.  Each entry point names the
+ * reference interface it replaces (paths relative to the reference repo):
+ *
+ *   chain.NewVerifier / Verifier.VerifyBeacon    chain/verify.go:18-20, 38-45
+ *   Verifier.DigestMessage + RoundToBytes        chain/verify.go:24-32, chain/store.go:42-46
+ *   key.Scheme.VerifyRecovered (bls.Verify (R))  chain/verify.go:44, key/curve.go:36
+ *   kyber G2 Hash (kilic HashToCurve (R))        key/curve.go:36 (pinned by key/curve_test.go:10-30)
+ *   KeyGroup.Point().UnmarshalBinary (pk)        chain/convert.go:19-38 (InfoFromProto)
+ *   scheme IDs                                   common/scheme/scheme.go:9-20
+ *
+ * Callers it serves (all only test err != nil, so one verdict bit per round
+ * carries the full reference contract): chain/beacon/sync_manager.go:212
+ * (CheckPastBeacons), :397 (tryNode), client/verify.go:162,201,
+ * lp2p/client/validator.go:66.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; all host buffers are caller-owned and are
+ *    not retained after a call returns (cgo-safe).
+ *  - Return codes: DGPU_OK (0) or a negative DGPU_E* value; the message is in
+ *    dgpu_last_error() (thread-local).
+ *  - A context is bound to one GPU and serializes its own calls internally;
+ *    any thread may call.  There is no CPU fallback: without a usable GPU,
+ *    dgpu_open fails with DGPU_EDEVICE.
+ *  - Verdict bitmaps: bit (i % 8) of byte (i / 8) is 1 iff round i verifies,
+ *    i.e. iff the reference's VerifyBeacon returns nil.
+ */
+#ifndef DRAND_GPU_H
+#define DRAND_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGPU_ABI_VERSION 1
+
+/* scheme IDs (common/scheme/scheme.go:9,12; bls-unchained-on-g1 added by this build) */
+enum {
+  DGPU_SCHEME_CHAINED = 0,      /* "pedersen-bls-chained":   msg = SHA256(prev || BE64(round)) */
+  DGPU_SCHEME_UNCHAINED = 1,    /* "pedersen-bls-unchained": msg = SHA256(BE64(round))        */
+  DGPU_SCHEME_UNCHAINED_G1 = 2  /* "bls-unchained-on-g1":    G1 signatures, G2 public key     */
+};
+
+enum {
+  DGPU_OK = 0,
+  DGPU_EINVAL = -1,
+  DGPU_EDEVICE = -2,
+  DGPU_ENOMEM = -3,
+  DGPU_EUNSUPPORTED = -4,
+  DGPU_ENOKEY = -5
+};
+
+/* per-round reason codes (optional output of the verify calls) */
+enum {
+  DGPU_REASON_OK = 0,
+  DGPU_REASON_DECODE = 1,   /* kyber UnmarshalBinary error: length, flags, x >= p, not on curve */
+  DGPU_REASON_SUBGROUP = 2, /* UnmarshalBinary error: not in the r-order subgroup              */
+  DGPU_REASON_PAIRING = 3,  /* bls: invalid signature                                          */
+  DGPU_REASON_INFINITY = 4  /* signature decodes to the identity: pairing check fails          */
+};
+
+enum { DGPU_MODE_PER_ROUND = 0, DGPU_MODE_RLC = 1 };
+
+typedef struct dgpu_ctx dgpu_ctx;
+
+int dgpu_abi_version(void);
+const char *dgpu_last_error(void);
+
+/* Open device `device` (HIP ordinal).  Replaces nothing in the reference: the
+ * Go side would hold one context per GPU inside crypto/gpu.BatchVerifier. */
+int dgpu_open(int device, dgpu_ctx **out);
+void dgpu_close(dgpu_ctx *ctx);
+
+/* Scheme name -> id, "" -> default chained (scheme.GetSchemeByIDWithDefault,
+ * common/scheme/scheme.go:37-48).  Returns the id or DGPU_EINVAL. */
+int dgpu_scheme_from_name(const char *name);
+
+/* Decode and install the group public key (chain.Info.PublicKey,
+ * chain/convert.go:20-23): 48-byte compressed G1 for the G2-signature
+ * schemes.  Rejects malformed or out-of-subgroup keys (DGPU_EINVAL). */
+int dgpu_set_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t len);
+
+/* Batch form of Verifier.VerifyBeacon (chain/verify.go:38-45) over n beacons
+ * given as fixed-stride records (host pointers):
+ *   rounds[i]                   Beacon.Round
+ *   sigs + i*sig_stride         Beacon.Signature, sig_len[i] bytes (any length
+ *                               != 96 is a decode failure, like the reference)
+ *   prev + i*prev_stride        Beacon.PreviousSig, prev_len[i] <= prev_stride
+ *                               bytes; ignored (may be NULL) for unchained schemes
+ * mode: DGPU_MODE_PER_ROUND (one pairing check per round).
+ * verdict_bits: ceil(n/8) bytes out.  reason: optional n bytes out. */
+int dgpu_verify_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *sigs,
+                      size_t sig_stride, const uint32_t *sig_len, const uint8_t *prev, size_t prev_stride,
+                      const uint32_t *prev_len, int mode, uint64_t rlc_seed, uint8_t *verdict_bits,
+                      uint8_t *reason);
+
+/* Same contract with every array already resident in device memory of the
+ * context's GPU (d_* are device pointers) and work enqueued on `stream`
+ * (a hipStream_t, NULL = the context's stream).  Asynchronous: results are
+ * valid after the stream synchronizes. */
+int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *d_rounds, const uint8_t *d_sigs,
+                             size_t sig_stride, const uint32_t *d_sig_len, const uint8_t *d_prev,
+                             size_t prev_stride, const uint32_t *d_prev_len, int mode, uint64_t rlc_seed,
+                             uint8_t *d_verdict_bits, uint8_t *d_reason, void *stream);
+
+/* Batch DigestMessage (chain/verify.go:24-32): out32 = n x 32 bytes. */
+int dgpu_digest_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *prev,
+                      size_t prev_stride, const uint32_t *prev_len, uint8_t *out32);
+
+/* Hash-to-G2 of n 32-byte messages with drand's DST (kyber G2 Hash (R)),
+ * compressed to 96 bytes each: the parity surface for hash-to-curve. */
+int dgpu_hash_to_g2(dgpu_ctx *ctx, size_t n, const uint8_t *msg32, uint8_t *out96);
+
+/* pk = sk * g1 (48-byte compressed G1) for a 32-byte big-endian secret:
+ * synthetic-chain tool (KeyGroup.Point().Mul(secret, nil),
+ * client/test/result/mock/result.go:88). */
+int dgpu_derive_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, uint8_t *pk_out, size_t pk_len);
+
+/* Synthetic chain generator (test/bench data tool; mirrors the reference's
+ * fixture generator client/test/result/mock/result.go:86-130).  Builds
+ * n_seg independent segments of seg_len rounds each, signed with the 32-byte
+ * big-endian secret scalar sk_be32 (< r):
+ *   segment s covers rounds first_round[s] .. first_round[s] + seg_len - 1;
+ *   its first round's PreviousSig is seed_prev + s*96 (seed_prev_len[s]
+ *   bytes), every later round's PreviousSig is the previous signature.
+ * Output (host pointers): sigs_out[(s*seg_len + j)*96 ...] for round
+ * first_round[s] + j.  Unchained schemes ignore the previous signature. */
+int dgpu_make_chain(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, size_t n_seg, size_t seg_len,
+                    const uint64_t *first_round, const uint8_t *seed_prev, const uint32_t *seed_prev_len,
+                    uint8_t *sigs_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRAND_GPU_H */

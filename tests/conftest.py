@@ -1,0 +1,38 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+HOSTSIM = os.path.join(ROOT, "tests", "hostsim", "libdrand_hostsim.so")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def load_golden(name):
+    import json
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def hostsim():
+    """Test-only host build of the kernel arithmetic (tests/hostsim)."""
+    import ctypes
+    src = os.path.join(ROOT, "tests", "hostsim", "hostsim.hip")
+    deps = [src] + [os.path.join(ROOT, "drand_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "drand_amd", "csrc"))]
+    if not os.path.exists(HOSTSIM) or os.path.getmtime(HOSTSIM) < max(os.path.getmtime(d) for d in deps):
+        subprocess.check_call(["hipcc", "-O2", "-std=c++17", "--cuda-host-only", "-fPIC", "-shared", "-o", HOSTSIM, src])
+    return ctypes.CDLL(HOSTSIM)
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    from drand_amd.chain import get_context
+    return get_context(0)

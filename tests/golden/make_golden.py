@@ -1,0 +1,105 @@
+"""Generate the committed golden fixtures under tests/golden/ from the oracle
+(oracle/bls12381.py, pinned by the reference KAT key/curve_test.go:10-30).
+
+    python tests/golden/make_golden.py
+
+Fixtures are data only (inputs + expected outputs).  The decode-only public
+keys are copied as hex strings from the reference's deploy/latest/group.toml
+(PublicKey.Coefficients) when /root/reference is present.
+"""
+import hashlib
+import json
+import os
+import re
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+from oracle import bls12381 as B  # noqa: E402
+from oracle import drand_ref as D  # noqa: E402
+
+
+def dump(name, obj):
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+    print("wrote", name)
+
+
+def kat():
+    sk = "643d6c704505385387a20d98aba19664e3ee81c600d21a0da910cc87f5dc4ab3"
+    msg = "7061737320746865207369676e6174757265"
+    sig = B.sign_g2(int(sk, 16), bytes.fromhex(msg)).hex()
+    assert sig == ("9940ca447bab3bab393c3a07866349343630437167eaeab063ef1e47acedc51e85c513121cf319a8832c3d136d7f3649"
+                   "0fa7241194b403a3bbbba9e7d5e73c9a86f67a9585c6fe077cd6576b2f76560efbab3550d9d5124242c728e3a7ef6989")
+    pk = B.sk_to_pk(int(sk, 16)).hex()
+    dump("kat_bls12381_compat_v112.json", {"source": "key/curve_test.go:10-30", "sk": sk, "msg": msg, "sig": sig,
+                                           "pk": pk})
+
+
+def h2g2():
+    out = []
+    for i in range(48):
+        m = hashlib.sha256(b"drand-mi355x/h2c/" + bytes([i])).digest()
+        out.append({"msg": m.hex(), "h": B.g2_compress(B.hash_to_g2(m)).hex()})
+    # drand digests of real round shapes
+    for r in (1, 2, 1969, 184348345343):
+        m = D.digest_message(D.SCHEME_UNCHAINED, r, b"")
+        out.append({"msg": m.hex(), "h": B.g2_compress(B.hash_to_g2(m)).hex()})
+    dump("hash_to_g2.json", {"dst": B.DST_G2.decode(), "cases": out})
+
+
+def chain(name, scheme, seed, n):
+    pk, ch = D.make_chain(seed, n, scheme)
+    rounds = [{"round": r, "prev": p.hex(), "sig": s.hex(), "valid": True} for r, p, s in ch]
+    pkp = B.g1_decompress(pk)
+    # corruption catalog on copies, with the oracle's verdicts
+    cases = []
+
+    def add(kind, r, prev, sig):
+        cases.append({"kind": kind, "round": r, "prev": prev.hex(), "sig": sig.hex(),
+                      "valid": D.verify_beacon(scheme, pkp, r, prev, sig)})
+
+    r, p, s = ch[1]
+    add("x_bit_flip", r, p, s[:47] + bytes([s[47] ^ 1]) + s[48:])
+    add("y_sign_flip", r, p, bytes([s[0] ^ 0x20]) + s[1:])
+    add("other_round_sig", r, p, ch[2][2])
+    if scheme == D.SCHEME_CHAINED:
+        add("prev_altered", r, bytes([p[0] ^ 1]) + p[1:], s)
+        add("prev_truncated", r, p[:95], s)
+        add("prev_nil", r, b"", s)
+    add("infinity", r, p, bytes([0xC0]) + bytes(95))
+    add("empty_sig", r, p, b"")
+    add("truncated_sig", r, p, s[:48])
+    add("wrong_round", r - 1, p, s)  # test/mock/grpcserver.go:150-155
+    add("compression_flag_clear", r, p, bytes([s[0] & 0x7F]) + s[1:])
+    add("infinity_noncanonical", r, p, bytes([0xC0]) + bytes(94) + b"\x01")
+    add("x_ge_p", r, p, bytes([0x80 | 0x1F]) + b"\xff" * 95)
+    dump(name, {"scheme": scheme, "seed": seed, "pk": pk.hex(), "genesis": D.derive_genesis(seed).hex(),
+                "rounds": rounds, "corrupted": cases})
+
+
+def group_keys():
+    path = "/root/reference/deploy/latest/group.toml"
+    if not os.path.exists(path):
+        print("reference absent; keeping existing group_toml_keys.json")
+        return
+    txt = open(path).read()
+    m = re.search(r"Coefficients\s*=\s*\[([^\]]*)\]", txt)
+    keys = re.findall(r'"([0-9a-f]+)"', m.group(1))
+    node_keys = re.findall(r'Key\s*=\s*"([0-9a-f]{96})"', txt)
+    out = []
+    for k in keys + node_keys:
+        try:
+            pt = B.g1_decompress(bytes.fromhex(k))
+            out.append({"pk": k, "decodes": True, "recompressed": B.g1_compress(pt).hex()})
+        except B.DecodeError as e:
+            out.append({"pk": k, "decodes": False, "error": str(e)})
+    dump("group_toml_keys.json", {"source": "deploy/latest/group.toml", "keys": out})
+
+
+if __name__ == "__main__":
+    kat()
+    h2g2()
+    chain("chain_chained_s1.json", D.SCHEME_CHAINED, 1, 24)
+    chain("chain_unchained_s1.json", D.SCHEME_UNCHAINED, 1, 12)
+    group_keys()

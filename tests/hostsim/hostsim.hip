@@ -1,0 +1,130 @@
+// TEST-ONLY host build of the kernels' arithmetic (drand_amd/csrc/*.cuh are
+// __host__ __device__).  Lets the CPU test suite check the exact code the
+// GPU runs against the oracle without a GPU.  Not part of the product:
+// libdrand_gpu.so never links or loads this; it is built into
+// tests/hostsim/libdrand_hostsim.so by __graft_entry__.build().
+#include <cstring>
+#include "../../drand_amd/csrc/h2c.cuh"
+#include "../../drand_amd/csrc/pairing.cuh"
+
+using namespace dgpu;
+
+static void fp_to_be(const fp& a, uint8_t* out) { fp_std_to_be48(fp_from_mont(a), out); }
+static fp fp_from_be(const uint8_t* in) { return fp_to_mont(fp_std_from_be48(in)); }
+
+extern "C" {
+
+// a*b, a+b, a-b, a^2 on canonical 48-byte big-endian inputs
+int hs_fp_ops(const uint8_t* a48, const uint8_t* b48, uint8_t* mul, uint8_t* add, uint8_t* sub, uint8_t* sqr,
+              uint8_t* inv) {
+  fp a = fp_from_be(a48), b = fp_from_be(b48);
+  fp_to_be(fp_mul(a, b), mul);
+  fp_to_be(fp_add(a, b), add);
+  fp_to_be(fp_sub(a, b), sub);
+  fp_to_be(fp_sqr(a), sqr);
+  fp_to_be(fp_inv(a), inv);
+  return 0;
+}
+
+int hs_fp2_ops(const uint8_t* a96, const uint8_t* b96, uint8_t* mul, uint8_t* sqr, uint8_t* inv, uint8_t* sqrt_out,
+               int* sqrt_ok) {
+  fp2 a{fp_from_be(a96), fp_from_be(a96 + 48)}, b{fp_from_be(b96), fp_from_be(b96 + 48)};
+  fp2 m = fp2_mul(a, b), s = fp2_sqr(a), iv = fp2_inv(a), r;
+  fp_to_be(m.c0, mul); fp_to_be(m.c1, mul + 48);
+  fp_to_be(s.c0, sqr); fp_to_be(s.c1, sqr + 48);
+  fp_to_be(iv.c0, inv); fp_to_be(iv.c1, inv + 48);
+  *sqrt_ok = fp2_sqrt(r, a) ? 1 : 0;
+  fp_to_be(r.c0, sqrt_out); fp_to_be(r.c1, sqrt_out + 48);
+  return 0;
+}
+
+void hs_digest(const uint8_t* prev, uint32_t prev_len, uint64_t round, uint8_t* out32) {
+  uint32_t m[8];
+  drand_digest(m, prev, prev_len, round);
+  for (int w = 0; w < 8; ++w)
+    for (int k = 0; k < 4; ++k) out32[4 * w + k] = (uint8_t)(m[w] >> (24 - 8 * k));
+}
+
+static void msg_words(const uint8_t* msg32, uint32_t m[8]) {
+  for (int w = 0; w < 8; ++w)
+    m[w] = ((uint32_t)msg32[4 * w] << 24) | ((uint32_t)msg32[4 * w + 1] << 16) | ((uint32_t)msg32[4 * w + 2] << 8) |
+           msg32[4 * w + 3];
+}
+
+void hs_expand_xmd(const uint8_t* msg32, uint8_t* out256) {
+  uint32_t m[8], o[64];
+  msg_words(msg32, m);
+  expand_xmd_g2(o, m);
+  for (int w = 0; w < 64; ++w)
+    for (int k = 0; k < 4; ++k) out256[4 * w + k] = (uint8_t)(o[w] >> (24 - 8 * k));
+}
+
+// u0, u1 (4 x 48 bytes canonical: u0.c0 u0.c1 u1.c0 u1.c1)
+void hs_hash_to_field(const uint8_t* msg32, uint8_t* out192) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  fp2 u0, u1;
+  hash_to_field_g2(u0, u1, m);
+  fp_to_be(u0.c0, out192); fp_to_be(u0.c1, out192 + 48); fp_to_be(u1.c0, out192 + 96); fp_to_be(u1.c1, out192 + 144);
+}
+
+// SSWU of u (96 bytes) -> affine x, y on E2' (4 x 48)
+void hs_sswu(const uint8_t* u96, uint8_t* out192) {
+  fp2 u{fp_from_be(u96), fp_from_be(u96 + 48)};
+  g2a q = map_to_curve_sswu_g2(u);
+  fp_to_be(q.x.c0, out192); fp_to_be(q.x.c1, out192 + 48); fp_to_be(q.y.c0, out192 + 96); fp_to_be(q.y.c1, out192 + 144);
+}
+
+void hs_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  g2j h = hash_to_g2(m);
+  bool inf = g2_is_inf(h);
+  g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h);
+  g2_compress(out96, a, inf);
+}
+
+int hs_decompress_g2(const uint8_t* in96, uint8_t* recompressed) {
+  g2a p{fp2_zero(), fp2_zero()};
+  int rc = g2_decompress(&p, in96, true);
+  if (rc == DEC_OK) g2_compress(recompressed, p, false);
+  return rc;
+}
+
+// full verification of one signature: returns status code (0 = valid)
+int hs_verify(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig96) {
+  g1a pk;
+  int rc = g1_decompress(&pk, pk48, GROUP_ORDER_WORDS);
+  if (rc != DEC_OK) return 100 + rc;
+  g2a s;
+  rc = g2_decompress(&s, sig96, true);
+  if (rc == DEC_INFINITY) return 4;
+  if (rc == DEC_ERR_SUBGROUP) return 2;
+  if (rc != DEC_OK) return 1;
+  uint32_t m[8];
+  msg_words(msg32, m);
+  g2a h = g2_to_affine(hash_to_g2(m));
+  fp12 f = miller_loop_2(h, fp_neg(pk.x), pk.y, s, fp_neg(C_G1_X), C_G1_NEG_Y);
+  return fp12_is_one(final_exponentiation(f)) ? 0 : 3;
+}
+
+// reduced pairing e(P, Q) = FE(f) (with the 3x hard-part exponent), as 12 x 48 bytes
+// in the oracle's f12_to_ints order
+void hs_pairing(const uint8_t* p48, const uint8_t* q96, uint8_t* out576) {
+  g1a p;
+  g1_decompress(&p, p48, GROUP_ORDER_WORDS);
+  g2a q;
+  g2_decompress(&q, q96, false);
+  // single pair: use the 2-pair loop with the second pair's line contribution
+  // neutralized is not possible; instead run pair 2 as (P, Q) too and take sqrt? No:
+  // compute f for (P,Q) twice -> e^2; callers compare against e(P,Q)^2.
+  fp12 f = miller_loop_2(q, fp_neg(p.x), p.y, q, fp_neg(p.x), p.y);
+  fp12 e = final_exponentiation(f);
+  const fp2* c[12 / 2] = {&e.c0.c0, &e.c0.c1, &e.c0.c2, &e.c1.c0, &e.c1.c1, &e.c1.c2};
+  for (int i = 0; i < 6; ++i) {
+    fp_to_be(c[i]->c0, out576 + 96 * i);
+    fp_to_be(c[i]->c1, out576 + 96 * i + 48);
+  }
+}
+
+}  // extern "C"

@@ -44,6 +44,8 @@ SYMBOLS = [
                                      _c.c_int, _c.c_uint64, _P, _P]),
     ("dgpu_verify_batch_device", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P, _c.c_size_t,
                                             _P, _c.c_int, _c.c_uint64, _P, _P, _P]),
+    ("dgpu_set_profiling", _c.c_int, [_P, _c.c_int]),
+    ("dgpu_stage_times", _c.c_int, [_P, _c.POINTER(_c.c_float), _c.c_int, _c.POINTER(_c.c_char_p)]),
     ("dgpu_digest_batch", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P]),
     ("dgpu_hash_to_g2", _c.c_int, [_P, _c.c_size_t, _P, _P]),
     ("dgpu_derive_pubkey", _c.c_int, [_P, _c.c_int, _P, _P, _c.c_size_t]),

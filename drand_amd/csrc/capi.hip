@@ -71,7 +71,18 @@ struct dgpu_ctx {
   DevBuf h_pts, sig_pts, status;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
+  // optional per-stage HIP-event timing of the last verify call
+  bool profile = false;
+  hipEvent_t ev[DGPU_MAX_STAGES + 1] = {};
+  int n_ev = 0;
 };
+
+static void mark(dgpu_ctx* c, hipStream_t s) {
+  if (!c->profile || c->n_ev > DGPU_MAX_STAGES) return;
+  if (!c->ev[c->n_ev]) hipEventCreate(&c->ev[c->n_ev]);
+  hipEventRecord(c->ev[c->n_ev], s);
+  c->n_ev++;
+}
 
 extern "C" {
 
@@ -113,6 +124,8 @@ void dgpu_close(dgpu_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  for (int i = 0; i <= DGPU_MAX_STAGES; ++i)
+    if (c->ev[i]) hipEventDestroy(c->ev[i]);
   for (DevBuf* b : {&c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
@@ -168,15 +181,21 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
   uint8_t* st = (uint8_t*)c->status.p;
   const unsigned B = 256;
+  c->n_ev = 0;
+  mark(c, s);
   hipLaunchKernelGGL(k_hash_to_g2_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
                      d_prev_len, chained ? 1 : 0, h);
   HIP_TRY(hipGetLastError());
+  mark(c, s);
   hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
   HIP_TRY(hipGetLastError());
+  mark(c, s);
   hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
   HIP_TRY(hipGetLastError());
+  mark(c, s);
   hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);
   HIP_TRY(hipGetLastError());
+  mark(c, s);
   if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, n, hipMemcpyDeviceToDevice, s));
   return DGPU_OK;
 }
@@ -233,6 +252,29 @@ int dgpu_verify_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds,
   if (reason) HIP_TRY(hipMemcpyAsync(reason, c->out_reason.p, n, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return DGPU_OK;
+}
+
+int dgpu_set_profiling(dgpu_ctx* c, int enable) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->profile = enable != 0;
+  c->n_ev = 0;
+  return DGPU_OK;
+}
+
+int dgpu_stage_times(dgpu_ctx* c, float* ms_out, int max_stages, const char** names_out) {
+  static const char* kNames[DGPU_MAX_STAGES] = {"hash_to_g2", "decode_g2", "pairing_check", "pack_verdicts"};
+  if (!c || !ms_out) return set_err(DGPU_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  int n = c->n_ev > 0 ? c->n_ev - 1 : 0;
+  if (n > max_stages) n = max_stages;
+  for (int i = 0; i < n; ++i) {
+    HIP_TRY(hipEventSynchronize(c->ev[i + 1]));
+    HIP_TRY(hipEventElapsedTime(&ms_out[i], c->ev[i], c->ev[i + 1]));
+    if (names_out) names_out[i] = kNames[i];
+  }
+  return n;
 }
 
 int dgpu_digest_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds, const uint8_t* prev,

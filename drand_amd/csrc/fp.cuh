@@ -29,6 +29,15 @@
 #define DG_NOINL __host__ __device__ __noinline__
 #endif
 
+// Operation counters for the test-only host build (tests/hostsim, tools/count_ops.py):
+// the executed algorithm's Fp mul/sqr counts feed the roofline's work figure.
+#if defined(DG_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long dg_count_mul, dg_count_sqr;
+#define DG_COUNT(x) (++(x))
+#else
+#define DG_COUNT(x)
+#endif
+
 namespace dgpu {
 
 struct fp {
@@ -49,6 +58,7 @@ DG_FN fp fp_one() { return FP_ONE_MONT; }
 // Separated operand scanning in product-scanning order: full 28-limb product,
 // then the Montgomery reduction, both column-wise into a 64-bit accumulator.
 DG_NOINL fp fp_mul(fp a, fp b) {
+  DG_COUNT(dg_count_mul);
   uint32_t t[2 * FP_LIMBS];
   uint64_t acc = 0;
 #pragma unroll
@@ -90,6 +100,7 @@ DG_NOINL fp fp_mul(fp a, fp b) {
 // Squaring: cross products computed once and doubled (98 instead of 196
 // partial products in the first half).
 DG_NOINL fp fp_sqr(fp a) {
+  DG_COUNT(dg_count_sqr);
   uint32_t t[2 * FP_LIMBS];
   uint64_t carry = 0;
 #pragma unroll

@@ -20,7 +20,7 @@ struct sha_state {
 #define DG_ROTR(x, n) (((x) >> (n)) | ((x) << (32 - (n))))
 #endif
 
-__host__ __device__ constexpr uint32_t SHA_K[64] = {
+constexpr uint32_t SHA_K[64] = {
     0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
     0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
     0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
@@ -115,7 +115,7 @@ DG_NOINL void drand_digest(uint32_t out[8], const uint8_t* prev, uint32_t prev_l
 // ================================================================ expand_message_xmd
 // DST bytes as big-endian words: "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_" (43 bytes)
 // followed by I2OSP(43, 1): DST_prime = 44 bytes = 11 words.
-__host__ __device__ constexpr uint32_t DST_G2_PRIME[11] = {0x424c535f, 0x5349475f, 0x424c5331, 0x32333831,
+constexpr uint32_t DST_G2_PRIME[11] = {0x424c535f, 0x5349475f, 0x424c5331, 0x32333831,
                                                              0x47325f58, 0x4d443a53, 0x48412d32, 0x35365f53,
                                                              0x5357555f, 0x524f5f4e, 0x554c5f2b};
 

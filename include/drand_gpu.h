@@ -108,6 +108,14 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
                              size_t prev_stride, const uint32_t *d_prev_len, int mode, uint64_t rlc_seed,
                              uint8_t *d_verdict_bits, uint8_t *d_reason, void *stream);
 
+/* Instrumentation: when enabled, every verify call records one HIP event
+ * per kernel stage on the stream it runs on; dgpu_stage_times returns the
+ * stage durations (ms) of the last call (hash_to_g2, decode_g2,
+ * pairing_check, pack_verdicts) and the number of stages written. */
+#define DGPU_MAX_STAGES 4
+int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
+int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
+
 /* Batch DigestMessage (chain/verify.go:24-32): out32 = n x 32 bytes. */
 int dgpu_digest_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *prev,
                       size_t prev_stride, const uint32_t *prev_len, uint8_t *out32);

@@ -46,6 +46,24 @@ def verify_beacon(scheme_id, pk_point, round_, prev_sig, sig):
     return B.verify_g2(pk_point, msg, sig)
 
 
+# reason codes shared with include/drand_gpu.h (DGPU_REASON_*)
+REASON_OK, REASON_DECODE, REASON_SUBGROUP, REASON_PAIRING, REASON_INFINITY = 0, 1, 2, 3, 4
+
+
+def verify_reason(scheme_id, pk_point, round_, prev_sig, sig):
+    """Like verify_beacon, but says why: the kyber error class (R)."""
+    msg = digest_message(scheme_id, round_, prev_sig)
+    try:
+        s = B.g2_decompress(sig)
+    except B.DecodeError as e:
+        return REASON_SUBGROUP if "subgroup" in str(e) else REASON_DECODE
+    if s is None:
+        return REASON_INFINITY
+    hm = B.hash_to_g2(msg)
+    ok = B.pairing_check([(pk_point, hm), (B.g1_neg(B.G1_GEN), s)])
+    return REASON_OK if ok else REASON_PAIRING
+
+
 # ------------------------------------------------------------- synthetic chains
 def derive_secret(seed):
     """sk = OS2IP(SHA-256("drand-mi355x/sk/" || LE64(s0))) mod r."""

@@ -56,8 +56,10 @@ def chain(name, scheme, seed, n):
     cases = []
 
     def add(kind, r, prev, sig):
+        reason = D.verify_reason(scheme, pkp, r, prev, sig)
+        assert (reason == D.REASON_OK) == D.verify_beacon(scheme, pkp, r, prev, sig)
         cases.append({"kind": kind, "round": r, "prev": prev.hex(), "sig": sig.hex(),
-                      "valid": D.verify_beacon(scheme, pkp, r, prev, sig)})
+                      "valid": reason == D.REASON_OK, "reason": reason})
 
     r, p, s = ch[1]
     add("x_bit_flip", r, p, s[:47] + bytes([s[47] ^ 1]) + s[48:])

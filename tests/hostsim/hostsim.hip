@@ -9,10 +9,42 @@
 
 using namespace dgpu;
 
+#ifdef DG_COUNT_OPS
+unsigned long long dg_count_mul = 0, dg_count_sqr = 0;
+#endif
+
 static void fp_to_be(const fp& a, uint8_t* out) { fp_std_to_be48(fp_from_mont(a), out); }
 static fp fp_from_be(const uint8_t* in) { return fp_to_mont(fp_std_from_be48(in)); }
 
 extern "C" {
+
+// per-stage Fp mul/sqr counts of one per-round verification (DG_COUNT_OPS builds)
+int hs_count_stages(const uint8_t* pk48, const uint8_t* prev, uint32_t prev_len, uint64_t round,
+                    const uint8_t* sig96, unsigned long long* out /* 8: mul,sqr for hash,decode,miller,fexp */) {
+#ifdef DG_COUNT_OPS
+  g1a pk;
+  if (g1_decompress(&pk, pk48, GROUP_ORDER_WORDS) != DEC_OK) return -1;
+  uint32_t m[8];
+  dg_count_mul = dg_count_sqr = 0;
+  drand_digest(m, prev, prev_len, round);
+  g2a h = g2_to_affine(hash_to_g2(m));
+  out[0] = dg_count_mul; out[1] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  g2a s;
+  int rc = g2_decompress(&s, sig96, true);
+  out[2] = dg_count_mul; out[3] = dg_count_sqr;
+  if (rc != DEC_OK) return -2;
+  dg_count_mul = dg_count_sqr = 0;
+  fp12 f = miller_loop_2(h, fp_neg(pk.x), pk.y, s, fp_neg(C_G1_X), C_G1_NEG_Y);
+  out[4] = dg_count_mul; out[5] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  bool ok = fp12_is_one(final_exponentiation(f));
+  out[6] = dg_count_mul; out[7] = dg_count_sqr;
+  return ok ? 0 : 3;
+#else
+  return -100;
+#endif
+}
 
 // a*b, a+b, a-b, a^2 on canonical 48-byte big-endian inputs
 int hs_fp_ops(const uint8_t* a48, const uint8_t* b48, uint8_t* mul, uint8_t* add, uint8_t* sub, uint8_t* sqr,

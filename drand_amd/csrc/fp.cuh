@@ -57,7 +57,20 @@ DG_FN fp fp_one() { return FP_ONE_MONT; }
 // ---------------------------------------------------------------- Montgomery
 // Separated operand scanning in product-scanning order: full 28-limb product,
 // then the Montgomery reduction, both column-wise into a 64-bit accumulator.
-DG_NOINL fp fp_mul(fp a, fp b) {
+#define DG_LIMB_PARAMS(x)                                                                                     \
+  uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6,   \
+      uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11, uint32_t x##12, uint32_t x##13
+#define DG_LIMB_ARGS(v)                                                                                       \
+  (v).l[0], (v).l[1], (v).l[2], (v).l[3], (v).l[4], (v).l[5], (v).l[6], (v).l[7], (v).l[8], (v).l[9], (v).l[10], \
+      (v).l[11], (v).l[12], (v).l[13]
+#define DG_LIMB_PACK(x) fp{{x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11, x##12, x##13}}
+
+// The out-of-line Fp kernels take limbs as scalar arguments: the AMDGPU
+// calling convention passes a second 14-dword struct byval through scratch,
+// which would put a store/load round trip (and an exposed wait) in front of
+// every multiplication.  28 scalars travel in v0..v27.
+DG_NOINL fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
+  const fp a = DG_LIMB_PACK(x), b = DG_LIMB_PACK(y);
   DG_COUNT(dg_count_mul);
   uint32_t t[2 * FP_LIMBS];
   uint64_t acc = 0;
@@ -99,7 +112,8 @@ DG_NOINL fp fp_mul(fp a, fp b) {
 
 // Squaring: cross products computed once and doubled (98 instead of 196
 // partial products in the first half).
-DG_NOINL fp fp_sqr(fp a) {
+DG_NOINL fp fp_sqr_r(DG_LIMB_PARAMS(x)) {
+  const fp a = DG_LIMB_PACK(x);
   DG_COUNT(dg_count_sqr);
   uint32_t t[2 * FP_LIMBS];
   uint64_t carry = 0;
@@ -159,7 +173,8 @@ DG_FN fp fp_norm(const fp& a) {
 
 // Input normalized, value < 2^392.  Output CI (< 2.01p): subtract q*p with
 // q = floor(top / (floor(p / 2^364) + 1)) <= floor(value / p).
-DG_NOINL fp fp_reduce(fp a) {
+DG_NOINL fp fp_reduce_r(DG_LIMB_PARAMS(x)) {
+  const fp a = DG_LIMB_PACK(x);
   constexpr uint32_t PTOP1 = FP_P[FP_LIMBS - 1] + 1;
   uint32_t q = a.l[FP_LIMBS - 1] / PTOP1;
   fp r;
@@ -173,6 +188,10 @@ DG_NOINL fp fp_reduce(fp a) {
   r.l[FP_LIMBS - 1] = (uint32_t)((int64_t)a.l[FP_LIMBS - 1] - (int64_t)q * FP_P[FP_LIMBS - 1] + c);
   return r;
 }
+
+DG_FN fp fp_mul(const fp& a, const fp& b) { return fp_mul_r(DG_LIMB_ARGS(a), DG_LIMB_ARGS(b)); }
+DG_FN fp fp_sqr(const fp& a) { return fp_sqr_r(DG_LIMB_ARGS(a)); }
+DG_FN fp fp_reduce(const fp& a) { return fp_reduce_r(DG_LIMB_ARGS(a)); }
 
 // ---------------------------------------------------------------- lazy add/sub
 DG_FN fp fp_add_lz(const fp& a, const fp& b) {
@@ -258,17 +277,36 @@ DG_FN bool fp_is_zero_std(const fp& a) {
   return acc == 0;
 }
 
-DG_FN bool fp_is_zero(const fp& a) { return fp_is_zero_std(fp_from_mont(a)); }
+// a == 0 mod p for a CI value (normalized, < 2.01p): a is one of 0, p, 2p.
+DG_FN bool fp_is_zero(const fp& a) {
+  uint32_t z = 0, zp = 0, z2p = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) {
+    z |= a.l[i];
+    zp |= a.l[i] ^ FP_P[i];
+    z2p |= a.l[i] ^ FP_2P[i];
+  }
+  return z == 0 || zp == 0 || z2p == 0;
+}
 
 DG_FN bool fp_eq(const fp& a, const fp& b) { return fp_is_zero(fp_sub(a, b)); }
 
 // ---------------------------------------------------------------- exponentiation
-// MSB-first square-and-multiply over a public constant exponent (uniform branch).
+// Fixed 4-bit-window exponentiation by a public constant exponent (uniform
+// control flow; the window table index is wave-uniform).
 DG_NOINL fp fp_pow(fp a, const uint32_t* e, int nbits) {
-  fp r = a;
-  for (int i = nbits - 2; i >= 0; --i) {
-    r = fp_sqr(r);
-    if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+  fp tbl[16];
+  tbl[1] = a;
+#pragma unroll 1
+  for (int i = 2; i < 16; ++i) tbl[i] = fp_mul(tbl[i - 1], a);
+  int nwin = (nbits + 3) / 4;
+  int top = nwin - 1;
+  uint32_t w = (e[(4 * top) >> 5] >> ((4 * top) & 31)) & 15u;
+  fp r = tbl[w];  // top window is non-zero (nbits is the exact bit length)
+  for (int k = top - 1; k >= 0; --k) {
+    r = fp_sqr(fp_sqr(fp_sqr(fp_sqr(r))));
+    w = (e[(4 * k) >> 5] >> ((4 * k) & 31)) & 15u;
+    if (w) r = fp_mul(r, tbl[w]);
   }
   return r;
 }

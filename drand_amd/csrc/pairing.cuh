@@ -79,11 +79,11 @@ DG_NOINL fp12 miller_loop_2(const g2a& Q1, const fp& nx1, const fp& y1, const g2
   return fp12_conj(f);
 }
 
-// a^|x| (square-and-multiply over the public constant)
+// a^|x| (square-and-multiply over the public constant), a in the cyclotomic subgroup
 DG_NOINL fp12 fp12_pow_absx(const fp12& a) {
   fp12 r = a;
   for (int i = 62; i >= 0; --i) {
-    r = fp12_sqr(r);
+    r = fp12_cyclo_sqr(r);
     if ((BLS_X_ABS >> i) & 1ull) r = fp12_mul(r, a);
   }
   return r;

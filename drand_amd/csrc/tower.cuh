@@ -34,7 +34,7 @@ DG_FN fp2 fp2_half(const fp2& a) { return fp2{fp_half(a.c0), fp_half(a.c1)}; }
 // Karatsuba: 3 Fp multiplications.  Lazy sums feed the third product
 // (limbs < 2^29, values < 4.02p: inside fp_mul's bounds); c1's subtrahend is
 // an unnormalized sum of two CI values, handled by fp_sub2_lz.
-DG_NOINL fp2 fp2_mul(const fp2& a, const fp2& b) {
+DG_FN fp2 fp2_mul(const fp2& a, const fp2& b) {
   fp t0 = fp_mul(a.c0, b.c0);
   fp t1 = fp_mul(a.c1, b.c1);
   fp t2 = fp_mul(fp_add_lz(a.c0, a.c1), fp_add_lz(b.c0, b.c1));
@@ -45,7 +45,7 @@ DG_NOINL fp2 fp2_mul(const fp2& a, const fp2& b) {
 }
 
 // (a0 + a1 u)^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u
-DG_NOINL fp2 fp2_sqr(const fp2& a) {
+DG_FN fp2 fp2_sqr(const fp2& a) {
   fp2 r;
   r.c0 = fp_mul(fp_add_lz(a.c0, a.c1), fp_sub_lz(a.c0, a.c1));
   r.c1 = fp_mul(fp_add_lz(a.c0, a.c0), a.c1);
@@ -217,6 +217,38 @@ DG_NOINL fp12 fp12_inv(const fp12& a) {
   fp6 t = fp6_sub(fp6_sqr(a.c0), fp6_mul_v(fp6_sqr(a.c1)));
   fp6 ti = fp6_inv(t);
   return fp12{fp6_mul(a.c0, ti), fp6_neg(fp6_mul(a.c1, ti))};
+}
+
+// (x0 + x1 s)^2 in Fp4 = Fp2[s]/(s^2 - xi): 3 Fp2 squarings
+DG_FN void fp4_sqr(fp2& r0, fp2& r1, const fp2& x0, const fp2& x1) {
+  fp2 t0 = fp2_sqr(x0);
+  fp2 t1 = fp2_sqr(x1);
+  r0 = fp2_add(t0, fp2_mul_xi(t1));
+  r1 = fp2_sub(fp2_sqr(fp2_add(x0, x1)), fp2_add(t0, t1));
+}
+
+// 3a - 2b and 3a + 2b in Fp2
+DG_FN fp2 fp2_3a_m_2b(const fp2& a, const fp2& b) { fp2 t = fp2_sub(a, b); return fp2_add(fp2_dbl(t), a); }
+DG_FN fp2 fp2_3a_p_2b(const fp2& a, const fp2& b) { fp2 t = fp2_add(a, b); return fp2_add(fp2_dbl(t), a); }
+
+// Granger-Scott squaring, valid on the cyclotomic subgroup (after the easy
+// part of the final exponentiation): view Fp12 = Fp4[w]/(w^3 - s), s = w^3,
+// f = A + B w + C w^2 with A = (f0, f3), B = (f1, f4), C = (f2, f5):
+//   A' = 3A^2 - 2 conj(A),  B' = 3 s C^2 + 2 conj(B),  C' = 3B^2 - 2 conj(C).
+// 9 Fp2 squarings instead of 2 Fp6 multiplications (checked in tests).
+DG_NOINL fp12 fp12_cyclo_sqr(const fp12& f) {
+  fp2 a0, a1, b0, b1, c0, c1;
+  fp4_sqr(a0, a1, f.c0.c0, f.c1.c1);
+  fp4_sqr(b0, b1, f.c1.c0, f.c0.c2);
+  fp4_sqr(c0, c1, f.c0.c1, f.c1.c2);
+  fp12 r;
+  r.c0.c0 = fp2_3a_m_2b(a0, f.c0.c0);
+  r.c1.c1 = fp2_3a_p_2b(a1, f.c1.c1);
+  r.c1.c0 = fp2_3a_p_2b(fp2_mul_xi(c1), f.c1.c0);
+  r.c0.c2 = fp2_3a_m_2b(c0, f.c0.c2);
+  r.c0.c1 = fp2_3a_m_2b(b0, f.c0.c1);
+  r.c1.c2 = fp2_3a_p_2b(b1, f.c1.c2);
+  return r;
 }
 
 // Multiply by a Miller-loop line l = c0 + c2 w^2 + c3 w^3

@@ -160,3 +160,20 @@ void hs_pairing(const uint8_t* p48, const uint8_t* q96, uint8_t* out576) {
 }
 
 }  // extern "C"
+
+extern "C" int hs_cyclo_sqr_check(const uint8_t* p48, const uint8_t* q96) {
+  // easy-part output is cyclotomic: compare Granger-Scott against the generic squaring
+  g1a p;
+  g1_decompress(&p, p48, GROUP_ORDER_WORDS);
+  g2a q;
+  g2_decompress(&q, q96, false);
+  fp12 f = miller_loop_2(q, fp_neg(p.x), p.y, q, fp_neg(p.x), p.y);
+  fp12 t = fp12_mul(fp12_conj(f), fp12_inv(f));
+  t = fp12_mul(fp12_frob2(t), t);
+  fp12 a = fp12_cyclo_sqr(t), b = fp12_sqr(t);
+  const fp2* x[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  const fp2* y[6] = {&b.c0.c0, &b.c0.c1, &b.c0.c2, &b.c1.c0, &b.c1.c1, &b.c1.c2};
+  for (int i = 0; i < 6; ++i)
+    if (!fp2_eq(*x[i], *y[i])) return 1;
+  return 0;
+}

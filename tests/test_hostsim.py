@@ -116,3 +116,20 @@ def test_non_subgroup_rejected(hostsim):
     q = B.iso_map_g2(B.map_to_curve_sswu_g2((rnd.randrange(P), rnd.randrange(P))))
     k = load_golden("kat_bls12381_compat_v112.json")
     assert hostsim.hs_verify(bytes.fromhex(k["pk"]), bytes(32), B.g2_compress(q)) == 2
+
+
+def test_cyclotomic_squaring(hostsim):
+    k = load_golden("kat_bls12381_compat_v112.json")
+    assert hostsim.hs_cyclo_sqr_check(bytes.fromhex(k["pk"]), bytes.fromhex(k["sig"])) == 0
+
+
+def test_pairing_value_matches_generic(hostsim):
+    """Full reduced pairing value e(P,Q)^2 (both pairs = (P,Q)) equals the
+    generic definition's, element by element."""
+    sk = 0x1234567
+    P1 = B.g1_mul(B.G1_GEN, sk)
+    Q1 = B.g2_mul(B.G2_GEN, 77)
+    out = buf(576)
+    hostsim.hs_pairing(B.g1_compress(P1), B.g2_compress(Q1), out)
+    e = B.f12_pow(B.pairing(P1, Q1), 2)
+    assert [ib(out.raw[48 * i:48 * (i + 1)]) for i in range(12)] == B.f12_to_ints(e)

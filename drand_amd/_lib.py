@@ -8,7 +8,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdrand_gpu.so")
+# DRAND_GPU_LIB selects an alternative in-tree build (A/B experiments only)
+LIB_PATH = os.environ.get("DRAND_GPU_LIB") or os.path.join(_HERE, "libdrand_gpu.so")
 
 DGPU_OK = 0
 DGPU_EINVAL = -1

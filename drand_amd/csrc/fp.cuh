@@ -28,6 +28,13 @@
 #ifndef DG_NOINL
 #define DG_NOINL __host__ __device__ __noinline__
 #endif
+// The Fp multiply/square/reduce kernels: out of line by default; with
+// DG_INLINE_FP they are inlined into their (out-of-line) callers.
+#ifdef DG_INLINE_FP
+#define DG_FPK DG_FN
+#else
+#define DG_FPK DG_NOINL
+#endif
 
 // Operation counters for the test-only host build (tests/hostsim, tools/count_ops.py):
 // the executed algorithm's Fp mul/sqr counts feed the roofline's work figure.
@@ -69,7 +76,7 @@ DG_FN fp fp_one() { return FP_ONE_MONT; }
 // calling convention passes a second 14-dword struct byval through scratch,
 // which would put a store/load round trip (and an exposed wait) in front of
 // every multiplication.  28 scalars travel in v0..v27.
-DG_NOINL fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
+DG_FPK fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
   const fp a = DG_LIMB_PACK(x), b = DG_LIMB_PACK(y);
   DG_COUNT(dg_count_mul);
   uint32_t t[2 * FP_LIMBS];
@@ -112,7 +119,7 @@ DG_NOINL fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
 
 // Squaring: cross products computed once and doubled (98 instead of 196
 // partial products in the first half).
-DG_NOINL fp fp_sqr_r(DG_LIMB_PARAMS(x)) {
+DG_FPK fp fp_sqr_r(DG_LIMB_PARAMS(x)) {
   const fp a = DG_LIMB_PACK(x);
   DG_COUNT(dg_count_sqr);
   uint32_t t[2 * FP_LIMBS];
@@ -173,7 +180,7 @@ DG_FN fp fp_norm(const fp& a) {
 
 // Input normalized, value < 2^392.  Output CI (< 2.01p): subtract q*p with
 // q = floor(top / (floor(p / 2^364) + 1)) <= floor(value / p).
-DG_NOINL fp fp_reduce_r(DG_LIMB_PARAMS(x)) {
+DG_FPK fp fp_reduce_r(DG_LIMB_PARAMS(x)) {
   const fp a = DG_LIMB_PACK(x);
   constexpr uint32_t PTOP1 = FP_P[FP_LIMBS - 1] + 1;
   uint32_t q = a.l[FP_LIMBS - 1] / PTOP1;

@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["per-round", "rlc"], default="per-round",
+                    help="per-round: configs[1]; rlc: configs[2] (random linear combination + bisection)")
+    ap.add_argument("--rlc-seed", type=int, default=3)
     return ap.parse_args()
 
 
@@ -96,11 +99,12 @@ def main():
     lib = ctx.lib
     _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, chain.pk, 48))
     stream = torch.cuda.current_stream(dev)
+    mode = _lib.MODE_RLC if args.mode == "rlc" else _lib.MODE_PER_ROUND
 
     def step():
         _lib.check(lib.dgpu_verify_batch_device(
             ctx.handle, _lib.SCHEME_CHAINED, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96, d_sig_len.data_ptr(),
-            d_prev.data_ptr(), 96, d_prev_len.data_ptr(), _lib.MODE_PER_ROUND, 0, d_bits.data_ptr(), None,
+            d_prev.data_ptr(), 96, d_prev_len.data_ptr(), mode, args.rlc_seed, d_bits.data_ptr(), None,
             ctypes.c_void_p(stream.cuda_stream)))
 
     for _ in range(args.warmup):
@@ -110,9 +114,9 @@ def main():
     # per-stage kernel timing (HIP events on the launch stream), one profiled pass
     _lib.check(lib.dgpu_set_profiling(ctx.handle, 1))
     step()
-    ms = (ctypes.c_float * 4)()
-    names = (ctypes.c_char_p * 4)()
-    ns = lib.dgpu_stage_times(ctx.handle, ms, 4, names)
+    ms = (ctypes.c_float * 8)()
+    names = (ctypes.c_char_p * 8)()
+    ns = lib.dgpu_stage_times(ctx.handle, ms, 8, names)
     stage_ms = {names[i].decode(): float(ms[i]) for i in range(max(ns, 0))}
     _lib.check(lib.dgpu_set_profiling(ctx.handle, 0))
     torch.cuda.synchronize()
@@ -151,7 +155,7 @@ def main():
         ops, counts = fp_ops_per_round()
         pair_ms = stage_ms.get("pairing_check")
         roofline = None
-        if ops and stage_ms:
+        if ops and stage_ms and args.mode == "per-round":
             step_ms = sum(stage_ms.values())
             achieved = n * ops * PRODUCTS_PER_FP_MUL / (step_ms * 1e-3) / 1e12
             roofline = {"bound": "valu-int32", "unit": "T mad_u64_u32/s", "achieved": achieved,
@@ -177,9 +181,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u32 (14x28-bit limb Fp, int32 VALU)",
             "data": "synthetic chained chain generated on GPU (seeded), 0.1% corrupted",
-            "config": {"workload": "configs[1]: chained G2 chain, per-round pairing verify",
+            "config": {"workload": ("configs[1]: chained G2 chain, per-round pairing verify" if args.mode == "per-round"
+                                    else "configs[2]: chained G2 chain, RLC batch verify + bisection, 0.1% corrupted"),
                        "rounds_per_gpu": n, "seg_len": args.seg_len, "scheme": "pedersen-bls-chained",
-                       "mode": "per-round", "parallelism": f"shard{world}"},
+                       "mode": args.mode, "parallelism": f"shard{world}"},
+            "stage_ms": stage_ms,
             "verdict_mismatches": mismatches,
             "corrupted_rounds_per_gpu": len(bad),
             "chain_gen_s": t_gen,

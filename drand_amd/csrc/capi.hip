@@ -69,18 +69,24 @@ struct dgpu_ctx {
   g1_key pk{};
   // scratch
   DevBuf h_pts, sig_pts, status;
+  // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
+  DevBuf rlc_tree, rlc_idx, rlc_fail;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call
   bool profile = false;
   hipEvent_t ev[DGPU_MAX_STAGES + 1] = {};
+  const char* stage_name[DGPU_MAX_STAGES] = {};
   int n_ev = 0;
 };
 
-static void mark(dgpu_ctx* c, hipStream_t s) {
+// Stage markers: mark(c, s, name) records an event that *starts* stage `name`
+// (and ends the previous one); mark(c, s, nullptr) closes the last stage.
+static void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
   if (!c->profile || c->n_ev > DGPU_MAX_STAGES) return;
   if (!c->ev[c->n_ev]) hipEventCreate(&c->ev[c->n_ev]);
   hipEventRecord(c->ev[c->n_ev], s);
+  if (c->n_ev < DGPU_MAX_STAGES) c->stage_name[c->n_ev] = name;
   c->n_ev++;
 }
 
@@ -126,7 +132,7 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (int i = 0; i <= DGPU_MAX_STAGES; ++i)
     if (c->ev[i]) hipEventDestroy(c->ev[i]);
-  for (DevBuf* b : {&c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+  for (DevBuf* b : {&c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -160,6 +166,88 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
   return DGPU_OK;
 }
 
+// RLC batch verification with exact per-round verdicts (mode DGPU_MODE_RLC).
+// 1. R_i = pre-cofactor H(m_i) (Jacobian), sig_i decoded (+ subgroup), status.
+// 2. Leaves P_i = r_i R_i, S_i = r_i sig_i; segment tree of sums up to the root.
+// 3. Top-down bisection: check every node of the first level with <= 512
+//    nodes, then both children of each failing node, down to the leaves; a
+//    failing leaf is an invalid round (ST_PAIRING).  Host-synchronous per level.
+// Stage events: hash, decode, leaves+tree, bisection.
+static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs, size_t sig_stride,
+                      const uint32_t* d_sig_len, const uint8_t* d_prev, size_t prev_stride, const uint32_t* d_prev_len,
+                      bool chained, uint64_t seed, hipStream_t s) {
+  const unsigned B = 256;
+  // level sizes
+  std::vector<size_t> sz{n};
+  while (sz.back() > 1) sz.push_back((sz.back() + 1) / 2);
+  size_t total = 0;
+  for (size_t v : sz) total += v;
+  int rc;
+  if ((rc = c->rlc_tree.ensure(2 * total * G2J_WORDS * 4 + n * G2J_WORDS * 4))) return rc;
+  if ((rc = c->rlc_idx.ensure(2 * 1024 * 4 + 2 * n * 4))) return rc;
+  if ((rc = c->rlc_fail.ensure(2 * n + 1024))) return rc;
+  uint32_t* tree = (uint32_t*)c->rlc_tree.p;
+  std::vector<uint32_t*> P(sz.size()), S(sz.size());
+  size_t off = 0;
+  for (size_t l = 0; l < sz.size(); ++l) {
+    P[l] = tree + off;
+    off += sz[l] * G2J_WORDS;
+    S[l] = tree + off;
+    off += sz[l] * G2J_WORDS;
+  }
+  uint32_t* rpts = tree + off;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  mark(c, s, "rlc_hash_to_g2_raw");
+  hipLaunchKernelGGL(k_hash_to_g2_raw, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
+                     d_prev_len, chained ? 1 : 0, rpts);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "decode_g2");
+  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "rlc_leaves_tree");
+  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, seed, rpts, sg, st, P[0], S[0]);
+  HIP_TRY(hipGetLastError());
+  for (size_t l = 0; l + 1 < sz.size(); ++l) {
+    hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(sz[l + 1], B)), dim3(B), 0, s, sz[l], P[l], S[l], sz[l + 1],
+                       P[l + 1], S[l + 1]);
+    HIP_TRY(hipGetLastError());
+  }
+  mark(c, s, "rlc_bisection");
+  // bisection
+  int top = (int)sz.size() - 1;
+  while (top > 0 && sz[top - 1] <= 512) --top;
+  std::vector<uint32_t> cand(sz[top]);
+  for (size_t j = 0; j < sz[top]; ++j) cand[j] = (uint32_t)j;
+  uint32_t* d_idx = (uint32_t*)c->rlc_idx.p;
+  uint8_t* d_fail = (uint8_t*)c->rlc_fail.p;
+  std::vector<uint8_t> fail;
+  for (int l = top; l >= 0 && !cand.empty(); --l) {
+    size_t m = cand.size();
+    HIP_TRY(hipMemcpyAsync(d_idx, cand.data(), m * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_rlc_check, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], c->pk, d_fail);
+    HIP_TRY(hipGetLastError());
+    if (l == 0) {
+      hipLaunchKernelGGL(k_rlc_mark, dim3(grid_for(m, B)), dim3(B), 0, s, m, d_idx, d_fail, st);
+      HIP_TRY(hipGetLastError());
+      break;
+    }
+    fail.resize(m);
+    HIP_TRY(hipMemcpyAsync(fail.data(), d_fail, m, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint32_t> next;
+    for (size_t k = 0; k < m; ++k) {
+      if (!fail[k]) continue;
+      size_t a = 2 * (size_t)cand[k];
+      next.push_back((uint32_t)a);
+      if (a + 1 < sz[l - 1]) next.push_back((uint32_t)(a + 1));
+    }
+    if (next.size() * 4 > c->rlc_idx.cap) return set_err(DGPU_ENOMEM, "bisection candidate overflow");
+    cand.swap(next);
+  }
+  return DGPU_OK;
+}
+
 static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
                                 size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev,
                                 size_t prev_stride, const uint32_t* d_prev_len, int mode, uint64_t rlc_seed,
@@ -167,7 +255,7 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
   (void)rlc_seed;
   if (scheme == DGPU_SCHEME_UNCHAINED_G1) return set_err(DGPU_EUNSUPPORTED, "bls-unchained-on-g1 not built yet");
   if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
-  if (mode != DGPU_MODE_PER_ROUND) return set_err(DGPU_EUNSUPPORTED, "mode %d not built yet", mode);
+  if (mode != DGPU_MODE_PER_ROUND && mode != DGPU_MODE_RLC) return set_err(DGPU_EINVAL, "bad mode %d", mode);
   if (!c->have_key) return set_err(DGPU_ENOKEY, "no public key installed (dgpu_set_pubkey)");
   if (n == 0) return DGPU_OK;
   bool chained = scheme == DGPU_SCHEME_CHAINED;
@@ -182,17 +270,23 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
   uint8_t* st = (uint8_t*)c->status.p;
   const unsigned B = 256;
   c->n_ev = 0;
-  mark(c, s);
-  hipLaunchKernelGGL(k_hash_to_g2_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
-                     d_prev_len, chained ? 1 : 0, h);
-  HIP_TRY(hipGetLastError());
-  mark(c, s);
-  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
-  HIP_TRY(hipGetLastError());
-  mark(c, s);
-  hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
-  HIP_TRY(hipGetLastError());
-  mark(c, s);
+  if (mode == DGPU_MODE_RLC) {
+    rc = rlc_locked(c, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len, chained, rlc_seed,
+                    s);
+    if (rc) return rc;
+  } else {
+    mark(c, s, "hash_to_g2");
+    hipLaunchKernelGGL(k_hash_to_g2_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
+                       d_prev_len, chained ? 1 : 0, h);
+    HIP_TRY(hipGetLastError());
+    mark(c, s, "decode_g2");
+    hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
+    HIP_TRY(hipGetLastError());
+    mark(c, s, "pairing_check");
+    hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
+    HIP_TRY(hipGetLastError());
+  }
+  mark(c, s, "pack_verdicts");
   hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);
   HIP_TRY(hipGetLastError());
   mark(c, s);
@@ -263,7 +357,6 @@ int dgpu_set_profiling(dgpu_ctx* c, int enable) {
 }
 
 int dgpu_stage_times(dgpu_ctx* c, float* ms_out, int max_stages, const char** names_out) {
-  static const char* kNames[DGPU_MAX_STAGES] = {"hash_to_g2", "decode_g2", "pairing_check", "pack_verdicts"};
   if (!c || !ms_out) return set_err(DGPU_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
@@ -272,7 +365,7 @@ int dgpu_stage_times(dgpu_ctx* c, float* ms_out, int max_stages, const char** na
   for (int i = 0; i < n; ++i) {
     HIP_TRY(hipEventSynchronize(c->ev[i + 1]));
     HIP_TRY(hipEventElapsedTime(&ms_out[i], c->ev[i], c->ev[i + 1]));
-    if (names_out) names_out[i] = kNames[i];
+    if (names_out) names_out[i] = c->stage_name[i] ? c->stage_name[i] : "?";
   }
   return n;
 }

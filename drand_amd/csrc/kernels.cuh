@@ -181,6 +181,126 @@ __global__ void k_derive_pubkey(scalar256 sk, uint8_t* __restrict__ out48) {
   for (int k = 0; k < 48; ++k) out48[k] = out[k];
 }
 
+// ================================================================ RLC batching
+// Shared-key collapse of the random linear combination:
+//   prod_i d_i^{r_i} = e(pk, h_eff * sum_i r_i R_i) * e(-g1, sum_i r_i sig_i),
+// with R_i the pre-cofactor hash point (h_eff applied once per checked node,
+// by linearity) and d_i = e(pk, H_i) e(-g1, sig_i).  Jacobian G2 arrays are
+// SoA [6 Fp][limb][index].
+constexpr int G2J_WORDS = 6 * FP_WORDS;
+
+__device__ __forceinline__ void st_g2j(uint32_t* base, size_t n, size_t i, const g2j& p) {
+  st_fp(base, n, i, p.x.c0);
+  st_fp(base + FP_WORDS * n, n, i, p.x.c1);
+  st_fp(base + 2 * FP_WORDS * n, n, i, p.y.c0);
+  st_fp(base + 3 * FP_WORDS * n, n, i, p.y.c1);
+  st_fp(base + 4 * FP_WORDS * n, n, i, p.z.c0);
+  st_fp(base + 5 * FP_WORDS * n, n, i, p.z.c1);
+}
+__device__ __forceinline__ g2j ld_g2j(const uint32_t* base, size_t n, size_t i) {
+  g2j p;
+  p.x.c0 = ld_fp(base, n, i);
+  p.x.c1 = ld_fp(base + FP_WORDS * n, n, i);
+  p.y.c0 = ld_fp(base + 2 * FP_WORDS * n, n, i);
+  p.y.c1 = ld_fp(base + 3 * FP_WORDS * n, n, i);
+  p.z.c0 = ld_fp(base + 4 * FP_WORDS * n, n, i);
+  p.z.c1 = ld_fp(base + 5 * FP_WORDS * n, n, i);
+  return p;
+}
+
+// SplitMix64-derived nonzero 64-bit coefficient for round `round` under `seed`.
+__device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t round) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (round + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z ? z : 1ull;
+}
+
+// Pre-cofactor hash point R (Jacobian) for m = DigestMessage(round, prev).
+__global__ void __launch_bounds__(256) k_hash_to_g2_raw(size_t n, const uint64_t* __restrict__ rounds,
+                                                         const uint8_t* __restrict__ prev, size_t prev_stride,
+                                                         const uint32_t* __restrict__ prev_len, int chained,
+                                                         uint32_t* __restrict__ r_out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t msg[8];
+  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, chained ? prev_len[i] : 0u, rounds[i]);
+  fp2 u0, u1;
+  hash_to_field_g2(u0, u1, msg);
+  g2j q = g2_add(iso3_map(map_to_curve_sswu_g2(u0)), iso3_map(map_to_curve_sswu_g2(u1)));
+  st_g2j(r_out, n, i, q);
+}
+
+// Leaves of the RLC tree: P_i = r_i R_i, S_i = r_i sig_i (infinity for rounds
+// whose decode verdict is already final).
+__global__ void __launch_bounds__(256) k_rlc_leaves(size_t n, const uint64_t* __restrict__ rounds, uint64_t seed,
+                                                     const uint32_t* __restrict__ r_pts,
+                                                     const uint32_t* __restrict__ sig_pts,
+                                                     const uint8_t* __restrict__ status, uint32_t* __restrict__ p_out,
+                                                     uint32_t* __restrict__ s_out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g2j P = g2_infinity(), S = g2_infinity();
+  if (status[i] == ST_OK) {
+    uint64_t r = rlc_coeff(seed, rounds[i]);
+    uint32_t k[2] = {(uint32_t)r, (uint32_t)(r >> 32)};
+    P = g2_mul_words(ld_g2j(r_pts, n, i), k, 2);
+    S = g2_mul_words(g2_from_affine(ld_g2a(sig_pts, n, i)), k, 2);
+  }
+  st_g2j(p_out, n, i, P);
+  st_g2j(s_out, n, i, S);
+}
+
+// One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied).
+__global__ void __launch_bounds__(256) k_rlc_level(size_t n_in, const uint32_t* __restrict__ p_in,
+                                                    const uint32_t* __restrict__ s_in, size_t n_out,
+                                                    uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_out) return;
+  size_t a = 2 * j, b = 2 * j + 1;
+  g2j P = ld_g2j(p_in, n_in, a), S = ld_g2j(s_in, n_in, a);
+  if (b < n_in) {
+    P = g2_add(P, ld_g2j(p_in, n_in, b));
+    S = g2_add(S, ld_g2j(s_in, n_in, b));
+  }
+  st_g2j(p_out, n_out, j, P);
+  st_g2j(s_out, n_out, j, S);
+}
+
+// Check candidate nodes of one level: fail[c] = 1 iff
+// e(pk, h_eff * P) * e(-g1, S) != 1 for node idx[c].
+__global__ void __launch_bounds__(256) k_rlc_check(size_t n_cand, const uint32_t* __restrict__ idx, size_t n_level,
+                                                    const uint32_t* __restrict__ p_lvl,
+                                                    const uint32_t* __restrict__ s_lvl, g1_key pk,
+                                                    uint8_t* __restrict__ fail) {
+  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;
+  size_t j = idx[c];
+  g2j P = g2_clear_cofactor(ld_g2j(p_lvl, n_level, j));
+  g2j S = ld_g2j(s_lvl, n_level, j);
+  bool pi = g2_is_inf(P), si = g2_is_inf(S);
+  bool ok;
+  if (pi && si) {
+    ok = true;
+  } else if (pi || si) {
+    ok = false;  // e(Q, .) of a non-trivial prime-order point alone is never 1
+  } else {
+    g2a Pa = g2_to_affine(P), Sa = g2_to_affine(S);
+    fp12 f = miller_loop_2(Pa, pk.neg_x, pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);
+    ok = fp12_is_one(final_exponentiation(f));
+  }
+  fail[c] = ok ? 0 : 1;
+}
+
+// Mark the rounds of failing leaves.
+__global__ void k_rlc_mark(size_t n_cand, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ fail,
+                           uint8_t* __restrict__ status) {
+  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;
+  if (fail[c]) status[idx[c]] = ST_PAIRING;
+}
+
 // status -> verdict bitmap (bit = 1 valid), one thread per output byte
 __global__ void k_pack_verdicts(size_t n, const uint8_t* __restrict__ status, uint8_t* __restrict__ bits) {
   size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

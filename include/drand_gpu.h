@@ -92,7 +92,11 @@ int dgpu_set_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t len);
  *                               != 96 is a decode failure, like the reference)
  *   prev + i*prev_stride        Beacon.PreviousSig, prev_len[i] <= prev_stride
  *                               bytes; ignored (may be NULL) for unchained schemes
- * mode: DGPU_MODE_PER_ROUND (one pairing check per round).
+ * mode: DGPU_MODE_PER_ROUND (one pairing check per round) or DGPU_MODE_RLC
+ *       (random linear combination over the batch with coefficients derived
+ *       from rlc_seed, exact per-round verdicts by bisection; the verdicts are
+ *       identical to per-round mode except with probability <= 2^-64 per
+ *       failing check; pass a fresh unpredictable seed for adversarial input).
  * verdict_bits: ceil(n/8) bytes out.  reason: optional n bytes out. */
 int dgpu_verify_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *sigs,
                       size_t sig_stride, const uint32_t *sig_len, const uint8_t *prev, size_t prev_stride,
@@ -110,9 +114,11 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
 
 /* Instrumentation: when enabled, every verify call records one HIP event
  * per kernel stage on the stream it runs on; dgpu_stage_times returns the
- * stage durations (ms) of the last call (hash_to_g2, decode_g2,
- * pairing_check, pack_verdicts) and the number of stages written. */
-#define DGPU_MAX_STAGES 4
+ * stage durations (ms) and names of the last call (per-round mode:
+ * hash_to_g2, decode_g2, pairing_check, pack_verdicts; RLC mode:
+ * rlc_hash_to_g2_raw, decode_g2, rlc_leaves_tree, rlc_bisection,
+ * pack_verdicts) and returns the number of stages written. */
+#define DGPU_MAX_STAGES 8
 int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
 

@@ -177,3 +177,32 @@ extern "C" int hs_cyclo_sqr_check(const uint8_t* p48, const uint8_t* q96) {
     if (!fp2_eq(*x[i], *y[i])) return 1;
   return 0;
 }
+
+// RLC collapse check over a whole batch (same device functions as k_rlc_*):
+// returns 0 if e(pk, h_eff * sum r_i R_i) * e(-g1, sum r_i sig_i) == 1.
+extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, const uint8_t* sigs96, int n,
+                                  uint64_t seed, const uint64_t* rounds) {
+  g1a pk;
+  if (g1_decompress(&pk, pk48, GROUP_ORDER_WORDS) != DEC_OK) return -1;
+  g2j P = g2_infinity(), S = g2_infinity();
+  for (int i = 0; i < n; ++i) {
+    uint32_t m[8];
+    msg_words(msgs32 + 32 * i, m);
+    fp2 u0, u1;
+    hash_to_field_g2(u0, u1, m);
+    g2j R = g2_add(iso3_map(map_to_curve_sswu_g2(u0)), iso3_map(map_to_curve_sswu_g2(u1)));
+    g2a s;
+    if (g2_decompress(&s, sigs96 + 96 * i, true) != DEC_OK) return -2;
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (rounds[i] + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (!z) z = 1;
+    uint32_t k[2] = {(uint32_t)z, (uint32_t)(z >> 32)};
+    P = g2_add(P, g2_mul_words(R, k, 2));
+    S = g2_add(S, g2_mul_words(g2_from_affine(s), k, 2));
+  }
+  g2a Pa = g2_to_affine(g2_clear_cofactor(P)), Sa = g2_to_affine(S);
+  fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);
+  return fp12_is_one(final_exponentiation(f)) ? 0 : 1;
+}

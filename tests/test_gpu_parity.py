@@ -136,3 +136,37 @@ def test_large_chain_by_construction(chained):
     for i in list(bad.keys())[:3] + [0, 1, 64, 4095]:
         b = beacons[i]
         assert D.verify_beacon(D.SCHEME_CHAINED, pk, b.round, b.previous_sig, b.signature) == bool(got[i])
+
+
+@pytest.mark.parametrize("name", ["chain_chained_s1.json", "chain_unchained_s1.json"])
+def test_rlc_mode_equals_per_round_golden(name, chained, unchained):
+    from drand_amd import _lib
+    from drand_amd.chain import Beacon
+    g = load_golden(name)
+    v = chained if g["scheme"] == "pedersen-bls-chained" else unchained
+    pk = bytes.fromhex(g["pk"])
+    beacons = [Beacon(bytes.fromhex(r["prev"]), r["round"], bytes.fromhex(r["sig"])) for r in g["rounds"]]
+    beacons += [Beacon(bytes.fromhex(c["prev"]), c["round"], bytes.fromhex(c["sig"])) for c in g["corrupted"]]
+    per = v.verify_reasons(beacons, pk).tolist()
+    for seed in (1, 0xDEADBEEF):
+        assert v.verify_reasons(beacons, pk, mode=_lib.MODE_RLC, rlc_seed=seed).tolist() == per
+    # edge cases: single beacon, all valid, all invalid-by-pairing, decode failures only
+    for sub in (beacons[:1], beacons[: len(g["rounds"])], beacons[-3:], [beacons[-1]]):
+        assert (v.verify_reasons(sub, pk, mode=_lib.MODE_RLC, rlc_seed=5).tolist()
+                == v.verify_reasons(sub, pk).tolist())
+
+
+def test_rlc_mode_large_chain(chained):
+    """3000 rounds (not a power of two), 1% corrupted: RLC verdicts/reasons ==
+    per-round verdicts/reasons == construction."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    c = make_chain(11, 3000, _lib.SCHEME_CHAINED, seg_len=32)
+    bad = corrupt(c, 11, rate=1e-2)
+    beacons = [c.beacon(i) for i in range(len(c))]
+    per = chained.verify_reasons(beacons, c.pk)
+    rlc = chained.verify_reasons(beacons, c.pk, mode=_lib.MODE_RLC, rlc_seed=12345)
+    assert rlc.tolist() == per.tolist()
+    expect = np.ones(len(c), dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(per == 0, expect)

@@ -133,3 +133,17 @@ def test_pairing_value_matches_generic(hostsim):
     hostsim.hs_pairing(B.g1_compress(P1), B.g2_compress(Q1), out)
     e = B.f12_pow(B.pairing(P1, Q1), 2)
     assert [ib(out.raw[48 * i:48 * (i + 1)]) for i in range(12)] == B.f12_to_ints(e)
+
+
+def test_rlc_collapse_algebra(hostsim):
+    """sum r_i R_i with h_eff applied once == sum r_i H_i: a valid batch passes,
+    one altered round (valid point, wrong message) fails."""
+    g = load_golden("chain_chained_s1.json")
+    pk = bytes.fromhex(g["pk"])
+    rs = g["rounds"][:5]
+    msgs = b"".join(D.digest_message(g["scheme"], r["round"], bytes.fromhex(r["prev"])) for r in rs)
+    sigs = b"".join(bytes.fromhex(r["sig"]) for r in rs)
+    rounds = (ctypes.c_uint64 * 5)(*[r["round"] for r in rs])
+    assert hostsim.hs_rlc_batch_check(pk, msgs, sigs, 5, ctypes.c_uint64(99), rounds) == 0
+    bad = sigs[:96] + sigs[192:288] + sigs[96:192] + sigs[288:]  # swap rounds 1 and 2
+    assert hostsim.hs_rlc_batch_check(pk, msgs, bad, 5, ctypes.c_uint64(99), rounds) == 1

@@ -2,6 +2,7 @@
 // kernels.  Host side of the product path: device memory, streams, launches.
 // There is deliberately no CPU fallback anywhere in this file.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -169,9 +170,9 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
 // RLC batch verification with exact per-round verdicts (mode DGPU_MODE_RLC).
 // 1. R_i = pre-cofactor H(m_i) (Jacobian), sig_i decoded (+ subgroup), status.
 // 2. Leaves P_i = r_i R_i, S_i = r_i sig_i; segment tree of sums up to the root.
-// 3. Top-down bisection: check every node of the first level with <= 512
-//    nodes, then both children of each failing node, down to the leaves; a
-//    failing leaf is an invalid round (ST_PAIRING).  Host-synchronous per level.
+// 3. Descent: check the nodes of one level, then the descendants of failing
+//    nodes D levels down, to the leaves; a failing leaf is an invalid round
+//    (ST_PAIRING).  Host-synchronous per descent step.
 // Stage events: hash, decode, leaves+tree, bisection.
 static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs, size_t sig_stride,
                       const uint32_t* d_sig_len, const uint8_t* d_prev, size_t prev_stride, const uint32_t* d_prev_len,
@@ -184,8 +185,8 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
   for (size_t v : sz) total += v;
   int rc;
   if ((rc = c->rlc_tree.ensure(2 * total * G2J_WORDS * 4 + n * G2J_WORDS * 4))) return rc;
-  if ((rc = c->rlc_idx.ensure(2 * 1024 * 4 + 2 * n * 4))) return rc;
-  if ((rc = c->rlc_fail.ensure(2 * n + 1024))) return rc;
+  if ((rc = c->rlc_idx.ensure(65536 * 4))) return rc;
+  if ((rc = c->rlc_fail.ensure(65536))) return rc;
   uint32_t* tree = (uint32_t*)c->rlc_tree.p;
   std::vector<uint32_t*> P(sz.size()), S(sz.size());
   size_t off = 0;
@@ -214,16 +215,27 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
     HIP_TRY(hipGetLastError());
   }
   mark(c, s, "rlc_bisection");
-  // bisection
+  // Wide descent: check every node of level S (a multiple of D = 5 with
+  // <= 64Ki nodes), then all level-(l-D) descendants of each failing node,
+  // down to the leaves: 2-3 sequential launches at 1M-10M rounds, each one
+  // wide enough to fill the GPU; with uniform corruption at rate rho the
+  // pairings spent are ~n/32 + (bad rounds) * 32.
+  const int D = 5;
   int top = (int)sz.size() - 1;
-  while (top > 0 && sz[top - 1] <= 512) --top;
-  std::vector<uint32_t> cand(sz[top]);
-  for (size_t j = 0; j < sz[top]; ++j) cand[j] = (uint32_t)j;
+  int S0 = 0;
+  while (S0 + D <= top && sz[S0] > 65536) S0 += D;
+  if (sz[S0] > 65536 && S0 < top) S0 = top;
+  std::vector<uint32_t> cand(sz[S0]);
+  for (size_t j = 0; j < sz[S0]; ++j) cand[j] = (uint32_t)j;
   uint32_t* d_idx = (uint32_t*)c->rlc_idx.p;
   uint8_t* d_fail = (uint8_t*)c->rlc_fail.p;
   std::vector<uint8_t> fail;
-  for (int l = top; l >= 0 && !cand.empty(); --l) {
+  for (int l = S0; l >= 0 && !cand.empty();) {
     size_t m = cand.size();
+    if ((rc = c->rlc_idx.ensure(m * 4))) return rc;
+    if ((rc = c->rlc_fail.ensure(m))) return rc;
+    d_idx = (uint32_t*)c->rlc_idx.p;
+    d_fail = (uint8_t*)c->rlc_fail.p;
     HIP_TRY(hipMemcpyAsync(d_idx, cand.data(), m * 4, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_rlc_check, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], c->pk, d_fail);
     HIP_TRY(hipGetLastError());
@@ -235,15 +247,16 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
     fail.resize(m);
     HIP_TRY(hipMemcpyAsync(fail.data(), d_fail, m, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    int nl = l >= D ? l - D : 0;
+    size_t span = (size_t)1 << (l - nl);
     std::vector<uint32_t> next;
     for (size_t k = 0; k < m; ++k) {
       if (!fail[k]) continue;
-      size_t a = 2 * (size_t)cand[k];
-      next.push_back((uint32_t)a);
-      if (a + 1 < sz[l - 1]) next.push_back((uint32_t)(a + 1));
+      size_t lo = (size_t)cand[k] * span, hi = std::min(lo + span, sz[nl]);
+      for (size_t j = lo; j < hi; ++j) next.push_back((uint32_t)j);
     }
-    if (next.size() * 4 > c->rlc_idx.cap) return set_err(DGPU_ENOMEM, "bisection candidate overflow");
     cand.swap(next);
+    l = nl;
   }
   return DGPU_OK;
 }

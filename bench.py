@@ -57,10 +57,10 @@ def fp_ops_per_round():
     return None, None
 
 
-def cpu_baseline(chain, seconds, cores):
+def cpu_baseline(chain, seconds, cores, expect_valid):
     """Oracle timed on this host over a bounded sample of the same chain."""
     from oracle import cpu_baseline as cb
-    return cb.run(chain, seconds, cores)
+    return cb.run(chain, seconds, cores, expect_valid)
 
 
 def main():
@@ -165,7 +165,7 @@ def main():
         cpu = None
         if not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(chain, args.cpu_seconds, min(16, os.cpu_count() or 1))
+                cpu = cpu_baseline(chain, args.cpu_seconds, min(16, os.cpu_count() or 1), expect)
             except Exception as e:  # reported, never fatal
                 cpu = {"error": repr(e)}
         out = {

@@ -1,0 +1,56 @@
+"""The C restatement (oracle/c) against the golden vectors and the Python
+oracle (CPU)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import bls12381 as B
+
+
+@pytest.fixture(scope="module")
+def cref():
+    from oracle import c_ref
+    c_ref.load()
+    return c_ref
+
+
+def test_hash_to_g2_golden(cref):
+    for c in load_golden("hash_to_g2.json")["cases"]:
+        assert cref.hash_to_g2(bytes.fromhex(c["msg"])).hex() == c["h"]
+
+
+def test_hash_to_g2_vs_python(cref):
+    for i in range(4):
+        m = hashlib.sha256(b"c-vs-py" + bytes([i])).digest()
+        assert cref.hash_to_g2(m) == B.g2_compress(B.hash_to_g2(m))
+
+
+@pytest.mark.parametrize("name", ["chain_chained_s1.json", "chain_unchained_s1.json"])
+def test_golden_verdicts_and_reasons(cref, name):
+    g = load_golden(name)
+    pk = bytes.fromhex(g["pk"])
+    chained = g["scheme"] == "pedersen-bls-chained"
+    for r in g["rounds"]:
+        assert cref.verify_beacon(chained, pk, r["round"], bytes.fromhex(r["prev"]), bytes.fromhex(r["sig"])) == 0
+    for c in g["corrupted"]:
+        got = cref.verify_beacon(chained, pk, c["round"], bytes.fromhex(c["prev"]), bytes.fromhex(c["sig"]))
+        assert got == c["reason"], c["kind"]
+
+
+def test_batch_threads(cref):
+    g = load_golden("chain_chained_s1.json")
+    rs = g["rounds"][:8]
+    n = len(rs)
+    rounds = np.array([r["round"] for r in rs], dtype=np.uint64)
+    sigs = np.stack([np.frombuffer(bytes.fromhex(r["sig"]), dtype=np.uint8) for r in rs])
+    prev = np.zeros((n, 96), dtype=np.uint8)
+    plen = np.zeros(n, dtype=np.uint32)
+    for i, r in enumerate(rs):
+        p = bytes.fromhex(r["prev"])
+        prev[i, : len(p)] = np.frombuffer(p, dtype=np.uint8)
+        plen[i] = len(p)
+    sigs[3, 0] ^= 0x20
+    reason = cref.verify_batch(True, bytes.fromhex(g["pk"]), rounds, sigs, np.full(n, 96, dtype=np.uint32), prev, plen, 4)
+    assert reason.tolist() == [0, 0, 0, 3, 0, 0, 0, 0]

@@ -57,6 +57,43 @@ def fp_ops_per_round():
     return None, None
 
 
+# stage name (dgpu_stage_times) -> op_counts.json stages it executes
+STAGE_OPS = {"hash_to_g2": ["hash_to_g2"], "decode_g2": ["decode_g2"], "pairing_check": ["miller_loop", "final_exp"]}
+
+
+def roofline_for(stage_ms, n, mode):
+    """Roofline of the dominant kernel: achieved = algorithmic 32x32 products
+    per launch (Fp mul+sqr count x 288) / measured launch time
+    (HIP events on the launch stream); traffic = PMC FETCH+WRITE bytes per
+    round (profiles/*_traffic.json) x rounds per launch."""
+    if not stage_ms:
+        return None
+    name = max(stage_ms, key=stage_ms.get)
+    ms = stage_ms[name]
+    ops, counts = fp_ops_per_round()
+    out = {"bound": "valu-int32", "unit": "T mad_u64_u32/s", "kernel": name, "launch_ms": ms,
+           "peak": PEAK_MAD_U64_PER_S / 1e12, "achieved": None, "frac": None, "traffic": None,
+           "stage_ms": stage_ms}
+    if counts and mode == "per-round" and name in STAGE_OPS:
+        st = counts["per_round_verify"]["stages"]
+        k_ops = sum(st[s]["fp_mul"] + st[s]["fp_sqr"] for s in STAGE_OPS[name])
+        achieved = n * k_ops * PRODUCTS_PER_FP_MUL / (ms * 1e-3)
+        out.update(achieved=achieved / 1e12, frac=achieved / PEAK_MAD_U64_PER_S,
+                   work_per_round_products=k_ops * PRODUCTS_PER_FP_MUL,
+                   pipeline_products_per_round=ops * PRODUCTS_PER_FP_MUL)
+    import glob
+    tr = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if tr:
+        with open(tr[-1]) as f:
+            t = json.load(f)["kernels"]
+        kname = {"hash_to_g2": "dgpu::k_hash_to_g2_beacons", "decode_g2": "dgpu::k_decode_g2_sigs",
+                 "pairing_check": "dgpu::k_pairing_check"}.get(name)
+        if kname in t:
+            out["traffic"] = n * (t[kname]["fetch_bytes_per_round"] + t[kname]["write_bytes_per_round"])
+            out["traffic_unit"] = "bytes per launch (PMC FETCH_SIZE+WRITE_SIZE, " + os.path.basename(tr[-1]) + ")"
+    return out
+
+
 def cpu_baseline(chain, seconds, cores, expect_valid):
     """Oracle timed on this host over a bounded sample of the same chain."""
     from oracle import cpu_baseline as cb
@@ -152,16 +189,7 @@ def main():
     if rank == 0:
         total_rounds = n * world * args.steps
         value = total_rounds / elapsed
-        ops, counts = fp_ops_per_round()
-        pair_ms = stage_ms.get("pairing_check")
-        roofline = None
-        if ops and stage_ms and args.mode == "per-round":
-            step_ms = sum(stage_ms.values())
-            achieved = n * ops * PRODUCTS_PER_FP_MUL / (step_ms * 1e-3) / 1e12
-            roofline = {"bound": "valu-int32", "unit": "T mad_u64_u32/s", "achieved": achieved,
-                        "peak": PEAK_MAD_U64_PER_S / 1e12, "frac": achieved * 1e12 / PEAK_MAD_U64_PER_S,
-                        "traffic": None, "kernel": "verify pipeline (all stages)",
-                        "stage_ms": stage_ms, "work_per_round_products": ops * PRODUCTS_PER_FP_MUL}
+        roofline = roofline_for(stage_ms, n, args.mode)
         cpu = None
         if not args.no_cpu_baseline:
             try:

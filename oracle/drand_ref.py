@@ -102,7 +102,7 @@ def check_past_beacons(store, up_to, verify):
     progress_calls)."""
     if not store:
         raise ValueError("empty store")
-    last = max(store)
+    last = store[max(store)][0]  # store.Last() (bolt: value under the largest key), its Round field
     if last < up_to:  # :180-184
         up_to = last
     faulty = []

@@ -1,0 +1,98 @@
+"""CheckPastBeacons batch mirror (drand_amd/sync.py) against the oracle's
+restatement of chain/beacon/sync_manager.go:171-232: identical faulty lists,
+progress callbacks and stopping rule for every window size.  The CPU tests
+use a stand-in verifier (verdict = a marker in the signature bytes); the GPU
+test runs the real HIP verifier over a golden chain with missing rows."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from drand_amd.chain import Beacon
+from drand_amd.sync import MemoryStore, beacon_marshal, beacon_unmarshal, check_past_beacons
+from oracle import drand_ref as D
+
+
+class MarkerVerifier:
+    """Stand-in for chain.Verifier in CPU tests: a beacon is valid iff its
+    signature does not start with b"BAD"."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def verify_reasons(self, beacons, pubkey, mode=0):
+        self.calls += 1
+        return np.array([3 if b.signature.startswith(b"BAD") else 0 for b in beacons], dtype=np.uint8)
+
+
+def _random_store(rng, n):
+    st = MemoryStore()
+    table = {}
+    st.put(Beacon(b"", 0, b"genesis"))
+    table[0] = (0, b"", b"genesis")
+    for r in range(1, n + 1):
+        if rng.random() < 0.05:
+            continue  # missing row
+        rr = r if rng.random() > 0.03 else r + 1000  # stored beacon with a different Round field
+        sig = (b"BAD" if rng.random() < 0.1 else b"ok") + bytes([r & 0xFF])
+        st.put_raw(r, beacon_marshal(Beacon(b"p", rr, sig)))
+        table[r] = (rr, b"p", sig)
+    return st, table
+
+
+def test_hexjson_roundtrip():
+    b = Beacon(bytes(range(96)), 184348345343, bytes(range(96, 192)))
+    enc = beacon_marshal(b)
+    assert b'"Round":184348345343' in enc and bytes(range(4)).hex().encode() in enc
+    assert beacon_unmarshal(enc) == b
+    assert beacon_unmarshal(b'{"Round":7}') == Beacon(b"", 7, b"")
+
+
+@pytest.mark.parametrize("window", [1, 3, 16, 1 << 16])
+def test_check_past_beacons_matches_oracle(window):
+    rng = random.Random(window)
+    for trial in range(40):
+        n = rng.randint(1, 60)
+        st, table = _random_store(rng, n)
+        last = st.last().round
+        for up_to in (0, 1, rng.randint(1, n + 5), n, n + 10, last + 5):
+            calls = []
+            got = check_past_beacons(st, MarkerVerifier(), b"pk", up_to, cb=lambda i, u: calls.append((i, u)),
+                                     window=window)
+            exp, progress = D.check_past_beacons(table, up_to, lambda b: not b[2].startswith(b"BAD"))
+            assert got == exp, (trial, up_to)
+            assert calls == progress, (trial, up_to)
+
+
+def test_check_past_beacons_batches():
+    st, table = _random_store(random.Random(5), 200)
+    v = MarkerVerifier()
+    check_past_beacons(st, v, b"pk", 10**9, window=64)
+    assert v.calls == -(-(st.len() - 1) // 64)  # one GPU batch per window, not one call per round
+
+
+@pytest.mark.gpu
+def test_check_past_beacons_gpu_golden():
+    """Real verifier: a golden chained chain with corrupted rows and holes;
+    the faulty list equals the oracle restatement's."""
+    from drand_amd.chain import Verifier
+    from drand_amd.scheme import get_scheme_by_id_with_default
+    g = load_golden("chain_chained_s1.json")
+    pk = bytes.fromhex(g["pk"])
+    st = MemoryStore()
+    table = {0: (0, b"", bytes.fromhex(g["genesis"]))}
+    st.put(Beacon(b"", 0, bytes.fromhex(g["genesis"])))
+    bad = {c["round"]: c for c in g["corrupted"] if c["kind"] in ("x_bit_flip", "y_sign", "other_round_sig")}
+    for r in g["rounds"]:
+        if r["round"] == 5:
+            continue  # hole
+        src = bad.get(r["round"], r)
+        b = Beacon(bytes.fromhex(src["prev"]), r["round"], bytes.fromhex(src["sig"]))
+        st.put(b)
+        table[r["round"]] = (b.round, b.previous_sig, b.signature)
+    v = Verifier(get_scheme_by_id_with_default("pedersen-bls-chained"))
+    got = check_past_beacons(st, v, pk, 10**9, window=7)
+    exp, _ = D.check_past_beacons(table, 10**9, lambda b: b[2] == bytes.fromhex(
+        next(x["sig"] for x in g["rounds"] if x["round"] == b[0])))
+    assert got == exp and 5 in got

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -12,6 +13,7 @@
 
 #include "../../include/drand_gpu.h"
 #include "kernels.cuh"
+#include "pairing_engine.cuh"
 
 using namespace dgpu;
 
@@ -59,6 +61,9 @@ struct DevBuf {
 
 inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
+// rounds per pairing-engine chunk: the line buffer takes 45.7 KB per round (6 GB at 128Ki)
+constexpr size_t ENG_CHUNK = 131072;
+
 }  // namespace
 
 struct dgpu_ctx {
@@ -72,6 +77,9 @@ struct dgpu_ctx {
   DevBuf h_pts, sig_pts, status;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
   DevBuf rlc_tree, rlc_idx, rlc_fail;
+  // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
+  DevBuf eng_consts, eng_lines, eng_f, eng_n1, eng_pre;
+  bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call
@@ -118,6 +126,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   dgpu_ctx* c = new dgpu_ctx();
   c->device = device;
+  const char* pm = getenv("DGPU_PAIRING");
+  c->legacy_pairing = pm && !strcmp(pm, "legacy");
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete c;
@@ -133,7 +143,7 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (int i = 0; i <= DGPU_MAX_STAGES; ++i)
     if (c->ev[i]) hipEventDestroy(c->ev[i]);
-  for (DevBuf* b : {&c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+  for (DevBuf* b : {&c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -162,6 +172,24 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
   if (drc != DEC_OK) return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
   memcpy(c->pk.neg_x.l, host, FP_LIMBS * 4);
   memcpy(c->pk.y.l, host + FP_LIMBS, FP_LIMBS * 4);
+  // engine block constants (slot order of tools/gen_engine.py: ONE, the two
+  // pairing points (-x, y), gamma1_1..5, gamma2_1..5)
+  eng_const_block cb;
+  const fp2 g1c[5] = {C_FROB1_1, C_FROB1_2, C_FROB1_3, C_FROB1_4, C_FROB1_5};
+  const fp2 g2c[5] = {C_FROB2_1, C_FROB2_2, C_FROB2_3, C_FROB2_4, C_FROB2_5};
+  auto put = [&](int slot, const fp& v) { memcpy(cb.w + (slot - 64) * ENG_SLOT_WORDS, v.l, FP_LIMBS * 4); };
+  put(ENG_C_ONE, fp_one());
+  put(ENG_C_NXP0, c->pk.neg_x);
+  put(ENG_C_YP0, c->pk.y);
+  put(ENG_C_NXP1, fp_neg(C_G1_X));
+  put(ENG_C_YP1, C_G1_NEG_Y);
+  for (int k = 0; k < 5; ++k) {
+    put(ENG_C_G1 + 2 * k, g1c[k].c0);
+    put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
+    put(ENG_C_G2 + k, g2c[k].c0);
+  }
+  if ((rc = c->eng_consts.ensure(sizeof cb))) return rc;
+  HIP_TRY(hipMemcpy(c->eng_consts.p, &cb, sizeof cb, hipMemcpyHostToDevice));
   c->have_key = true;
   c->key_scheme = scheme;
   return DGPU_OK;
@@ -261,6 +289,36 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
   return DGPU_OK;
 }
 
+// Per-round pairing checks on the lane-cooperative engine, chunk by chunk
+// (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
+// final exponentiation.  Decode verdicts in `st` stay final.
+static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
+                              hipStream_t s) {
+  const size_t cap = std::min<size_t>(n, ENG_CHUNK);
+  int rc;
+  if ((rc = c->eng_lines.ensure(cap * (size_t)ENG_LINE_STEPS * 12 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->eng_f.ensure(cap * 24 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->eng_n1.ensure(cap * FP_LIMBS * 4))) return rc;
+  const uint32_t* consts = (const uint32_t*)c->eng_consts.p;
+  uint32_t* lines = (uint32_t*)c->eng_lines.p;
+  uint32_t* f = (uint32_t*)c->eng_f.p;
+  uint32_t* n1 = (uint32_t*)c->eng_n1.p;
+  for (size_t r0 = 0; r0 < n; r0 += cap) {
+    const size_t cnt = std::min(cap, n - r0);
+    const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
+    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, sg, consts, lines);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
+    HIP_TRY(hipGetLastError());
+    const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
+    hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, lines, st);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
+    HIP_TRY(hipGetLastError());
+  }
+  return DGPU_OK;
+}
+
 static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
                                 size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev,
                                 size_t prev_stride, const uint32_t* d_prev_len, int mode, uint64_t rlc_seed,
@@ -296,8 +354,12 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
     hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
     HIP_TRY(hipGetLastError());
     mark(c, s, "pairing_check");
-    hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
-    HIP_TRY(hipGetLastError());
+    if (c->legacy_pairing) {
+      hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
+      HIP_TRY(hipGetLastError());
+    } else if ((rc = eng_pairing_locked(c, n, h, sg, st, s))) {
+      return rc;
+    }
   }
   mark(c, s, "pack_verdicts");
   hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);

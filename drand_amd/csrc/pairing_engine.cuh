@@ -1,0 +1,213 @@
+// Per-round pairing check e(pk, H) * e(-g1, sig) == 1 on the lane-cooperative
+// engine (engine.cuh), as four launches over a chunk of rounds:
+//
+//   k_eng_lines   T-steps of both Miller loops (pairs (pk, H) and (-g1, sig)):
+//                 68 steps x 2 lines x 6 Fp of line coefficients -> HBM
+//   k_eng_miller  f = prod of lines (shared squaring), then N1 = Norm(f) in Fp
+//   k_eng_inv     batch inversion of N1 (Montgomery's trick, 1 exponentiation
+//                 per 64 rounds)
+//   k_eng_fe      f^-1 from N1^-1, final exponentiation, f == 1 -> verdict
+//
+// Reference: chain/verify.go:44 -> kyber bls.Verify -> ValidatePairing ->
+// kilic Engine AddPair/AddPairInv/Check (R).  The conjugation of the Miller
+// value (x < 0) is skipped: FE(conj f) = FE(f)^-1, equal to 1 iff FE(f) is.
+//
+// HBM layouts (chunk-local round index i, chunk capacity cap):
+//   lines  [step 0..67][export 0..11][limb][i]     (export 6p + e: pair p, l0.re .. l3.im)
+//   fbuf   [component 0..23][limb][i]              (f, later t and t2 of the FE)
+//   n1     [limb][i]
+#pragma once
+#include "engine.cuh"
+#include "kernels.cuh"
+
+namespace dgpu {
+
+constexpr int ENG_BLOCK = 64;                                  // one wave: 5 rounds
+constexpr int ENG_ROUNDS_PER_BLOCK = ENG_GROUPS_PER_WAVE;
+constexpr int ENG_LINE_STEPS = 68;
+
+// block constant region, host-built (capi.hip: eng_consts_for)
+struct eng_const_block {
+  uint32_t w[ENG_NCONST * ENG_SLOT_WORDS];
+};
+
+struct eng_lane {
+  int g, k;      // group in the wave, lane in the group
+  size_t i;      // chunk-local round (clamped)
+  bool valid;
+};
+
+__device__ __forceinline__ eng_lane eng_lane_id(size_t cnt) {
+  const int lane = threadIdx.x & 63;
+  eng_lane L;
+  L.g = lane < 60 ? lane / 12 : 4;
+  L.k = lane < 60 ? lane % 12 : lane - 60;
+  const size_t gi = (size_t)blockIdx.x * ENG_ROUNDS_PER_BLOCK + L.g;
+  L.valid = gi < cnt;
+  L.i = L.valid ? gi : cnt - 1;
+  return L;
+}
+
+__device__ __forceinline__ void eng_load_consts(uint32_t* c, const uint32_t* src) {
+  for (int t = threadIdx.x; t < ENG_NCONST * ENG_SLOT_WORDS; t += blockDim.x) c[t] = src[t];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void st_soa(uint32_t* base, size_t stride, size_t i, const fp& a) {
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) base[(size_t)l * stride + i] = a.l[l];
+}
+__device__ __forceinline__ fp ld_soa(const uint32_t* base, size_t stride, size_t i) {
+  fp a;
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) a.l[l] = base[(size_t)l * stride + i];
+  return a;
+}
+
+// HBM side of a kernel program (chunk-local SoA buffers, stride cnt).
+struct eng_io {
+  uint32_t* lines;   // [step][12][limb][cnt]
+  uint32_t* fbuf;    // [24][limb][cnt]
+  uint32_t* n1;      // [limb][cnt]
+  size_t cnt;
+};
+
+// The program interpreter (one inlined copy of the op interpreter per kernel).
+__device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
+                                         const eng_lane& L, const eng_io& io) {
+  int step = 0;
+  auto sink = [&](uint32_t e, const fp& v) {
+    if (!L.valid) return;
+    if (e < 12) st_soa(io.lines + ((size_t)(step * 12 + e) * FP_LIMBS) * io.cnt, io.cnt, L.i, v);
+    else st_soa(io.n1, io.cnt, L.i, v);
+  };
+#pragma unroll 1
+  for (int pc = 0; pc < len; ++pc) {
+    const uint32_t ins = prog[pc];
+    const uint32_t opc = ins >> 24, a = ins & 0xFFu, b = (ins >> 8) & 0xFFu;
+    if (opc == ENG_OPC_RUN) {
+      eng_run((int)a, g, c, L.k, sink);
+    } else if (opc == ENG_OPC_STEP) {
+      ++step;
+    } else if (opc == ENG_OPC_LDLINE) {
+      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_soa(io.lines + ((size_t)(step * 12 + L.k) * FP_LIMBS) * io.cnt, io.cnt, L.i));
+      ++step;
+    } else if (opc == ENG_OPC_LD12) {
+      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_soa(io.fbuf + (size_t)(b + L.k) * FP_LIMBS * io.cnt, io.cnt, L.i));
+    } else if (opc == ENG_OPC_ST12) {
+      if (L.valid) st_soa(io.fbuf + (size_t)(b + L.k) * FP_LIMBS * io.cnt, io.cnt, L.i, eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
+    }
+    asm volatile("" ::: "memory");
+  }
+}
+
+// x == K mod p for x < 2.01p (normalized) and a canonical constant K < p
+__device__ __forceinline__ bool eng_eq_canon(const fp& x, const fp& K) {
+  fp k1 = fp_norm(fp_add_lz(K, fp{{FP_P[0], FP_P[1], FP_P[2], FP_P[3], FP_P[4], FP_P[5], FP_P[6], FP_P[7], FP_P[8],
+                                    FP_P[9], FP_P[10], FP_P[11], FP_P[12], FP_P[13]}}));
+  fp k2 = fp_norm(fp_add_lz(k1, fp{{FP_P[0], FP_P[1], FP_P[2], FP_P[3], FP_P[4], FP_P[5], FP_P[6], FP_P[7], FP_P[8],
+                                     FP_P[9], FP_P[10], FP_P[11], FP_P[12], FP_P[13]}}));
+  uint32_t d0 = 0, d1 = 0, d2 = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) {
+    d0 |= x.l[i] ^ K.l[i];
+    d1 |= x.l[i] ^ k1.l[i];
+    d2 |= x.l[i] ^ k2.l[i];
+  }
+  return d0 == 0 || d1 == 0 || d2 == 0;
+}
+
+// ---------------------------------------------------------------- k_eng_lines
+// h_pts / sig_pts: affine G2 SoA [x.c0, x.c1, y.c0, y.c1][limb][n], rounds r0 + i.
+__global__ void __launch_bounds__(ENG_BLOCK) k_eng_lines(size_t n, size_t r0, size_t cnt,
+                                                         const uint32_t* __restrict__ h_pts,
+                                                         const uint32_t* __restrict__ sig_pts,
+                                                         const uint32_t* __restrict__ consts,
+                                                         uint32_t* __restrict__ lines) {
+  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_LINES) * ENG_SLOT_WORDS];
+  uint32_t* c = lds;
+  eng_load_consts(c, consts);
+  const eng_lane L = eng_lane_id(cnt);
+  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_LINES) * ENG_SLOT_WORDS;
+  const size_t r = r0 + L.i;
+  if (L.k < 8) {  // Q coordinates: X, Y of T and the affine copy (xQ, yQ)
+    const int p = L.k >> 2, comp = L.k & 3;
+    const fp q = ld_soa((p ? sig_pts : h_pts) + (size_t)comp * FP_LIMBS * n, n, r);
+    eng_st(g + (p * ENG_LINE_PAIR_SLOTS + comp) * ENG_SLOT_WORDS, q);
+    eng_st(g + (p * ENG_LINE_PAIR_SLOTS + 6 + comp) * ENG_SLOT_WORDS, q);
+  } else {        // Z = 1
+    const int p = (L.k - 8) >> 1, comp = (L.k - 8) & 1;
+    eng_st(g + (p * ENG_LINE_PAIR_SLOTS + 4 + comp) * ENG_SLOT_WORDS, comp ? fp_zero() : fp_one());
+  }
+  asm volatile("" ::: "memory");
+  eng_exec(ENG_PROG_LINES, ENG_PROG_LINES_LEN, g, c, L, eng_io{lines, nullptr, nullptr, cnt});
+}
+
+// ---------------------------------------------------------------- k_eng_miller
+__global__ void __launch_bounds__(ENG_BLOCK) k_eng_miller(size_t cnt, const uint32_t* __restrict__ consts,
+                                                          uint32_t* __restrict__ lines,
+                                                          uint32_t* __restrict__ fbuf, uint32_t* __restrict__ n1) {
+  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS];
+  uint32_t* c = lds;
+  eng_load_consts(c, consts);
+  const eng_lane L = eng_lane_id(cnt);
+  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS;
+  eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
+  asm volatile("" ::: "memory");
+  eng_exec(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
+  if (L.valid) st_soa(fbuf + (size_t)L.k * FP_LIMBS * cnt, cnt, L.i, eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
+}
+
+// ---------------------------------------------------------------- k_eng_inv
+// Thread t inverts the N1 of rounds t, t + T, t + 2T, ... (T = threads in the
+// grid) by Montgomery's trick; prefix products go to `pre` (same layout).
+// A zero N1 (f not invertible: FE(f) = 0 != 1) fails its round.
+__global__ void __launch_bounds__(256) k_eng_inv(size_t cnt, size_t r0, uint32_t* __restrict__ n1,
+                                                 uint32_t* __restrict__ pre, uint8_t* __restrict__ status) {
+  const size_t T = (size_t)gridDim.x * blockDim.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= cnt) return;
+  fp acc = fp_one();
+  size_t last = t;
+  for (size_t i = t; i < cnt; i += T) {
+    fp v = ld_soa(n1, cnt, i);
+    if (fp_is_zero(v)) {
+      v = fp_one();
+      if (status[r0 + i] == ST_OK) status[r0 + i] = ST_PAIRING;
+      st_soa(n1, cnt, i, v);
+    }
+    acc = fp_mul(acc, v);
+    st_soa(pre, cnt, i, acc);
+    last = i;
+  }
+  fp inv = fp_inv(acc);
+  for (size_t i = last;; i -= T) {
+    const fp v = ld_soa(n1, cnt, i);
+    const fp out = i >= t + T ? fp_mul(inv, ld_soa(pre, cnt, i - T)) : inv;
+    st_soa(n1, cnt, i, out);
+    if (i < t + T) break;
+    inv = fp_mul(inv, v);
+  }
+}
+
+// ---------------------------------------------------------------- k_eng_fe
+__global__ void __launch_bounds__(ENG_BLOCK) k_eng_fe(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
+                                                      uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ n1inv,
+                                                      uint8_t* __restrict__ status) {
+  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_FE) * ENG_SLOT_WORDS];
+  uint32_t* c = lds;
+  eng_load_consts(c, consts);
+  const eng_lane L = eng_lane_id(cnt);
+  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_FE) * ENG_SLOT_WORDS;
+  eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_soa(fbuf + (size_t)L.k * FP_LIMBS * cnt, cnt, L.i));
+  if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
+  asm volatile("" ::: "memory");
+  eng_exec(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});
+  const fp v = eng_ld(g + (ENG_E_R + L.k) * ENG_SLOT_WORDS);
+  const bool ok = eng_eq_canon(v, L.k == 0 ? fp_one() : fp_zero());
+  const uint64_t m = __ballot(ok);
+  const bool all = ((m >> (12 * L.g)) & 0xFFFull) == 0xFFFull;
+  if (L.valid && L.k == 0 && !all && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_PAIRING;
+}
+
+}  // namespace dgpu

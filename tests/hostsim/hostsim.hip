@@ -206,3 +206,124 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
   fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);
   return fp12_is_one(final_exponentiation(f)) ? 0 : 1;
 }
+
+// ---------------------------------------------------------------- pairing engine (host emulation)
+// The device interpreter's per-lane compute (eng_compute) run for the 12
+// lanes of one group in turn: all lanes of a sub-op read, then all write --
+// the semantics the device gets from one wavefront's in-order LDS queue.
+#define DG_HOSTSIM
+#include <vector>
+#include "../../drand_amd/csrc/engine.cuh"
+
+namespace {
+struct HostGroup {
+  uint32_t s[64 * ENG_SLOT_WORDS];
+  uint32_t c[ENG_NCONST * ENG_SLOT_WORDS];
+  std::vector<fp> lines = std::vector<fp>(68 * 12);
+  fp fbuf[24];
+  fp n1;
+  int step = 0;
+  fp get(int slot) const { return eng_ld(s + slot * ENG_SLOT_WORDS); }
+  void set(int slot, const fp& v) { eng_st(s + slot * ENG_SLOT_WORDS, v); }
+};
+
+void host_run_op(HostGroup& G, int op) {
+  const uint32_t s0 = ENG_OP_TAB[op][0], ns = ENG_OP_TAB[op][1];
+  for (uint32_t sb = s0; sb < s0 + ns; ++sb) {
+    const uint32_t off = ENG_SUB_TAB[sb][0], nt = ENG_SUB_TAB[sb][1];
+    fp outs[ENG_LANES];
+    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_compute(G.s, G.c, ENG_WORDS + off + k * (4 + nt), nt);
+    for (int k = 0; k < ENG_LANES; ++k) {
+      const uint32_t* rec = ENG_WORDS + off + k * (4 + nt);
+      if (eng_dst(rec) != 0xFF) G.set(eng_dst(rec), outs[k]);
+      const uint32_t e = eng_exp(rec);
+      if (e != 0xFF) {
+        if (e < 12) G.lines[G.step * 12 + e] = outs[k];
+        else G.n1 = outs[k];
+      }
+    }
+  }
+}
+
+void host_exec(HostGroup& G, const uint32_t* prog, int len) {
+  for (int pc = 0; pc < len; ++pc) {
+    const uint32_t ins = prog[pc], opc = ins >> 24, a = ins & 0xFF, b = (ins >> 8) & 0xFF;
+    if (opc == ENG_OPC_RUN) host_run_op(G, (int)a);
+    else if (opc == ENG_OPC_STEP) G.step++;
+    else if (opc == ENG_OPC_LDLINE) {
+      for (int k = 0; k < 12; ++k) G.set(a + k, G.lines[G.step * 12 + k]);
+      G.step++;
+    } else if (opc == ENG_OPC_LD12) {
+      for (int k = 0; k < 12; ++k) G.set(a + k, G.fbuf[b + k]);
+    } else if (opc == ENG_OPC_ST12) {
+      for (int k = 0; k < 12; ++k) G.fbuf[b + k] = G.get(a + k);
+    }
+  }
+}
+
+void host_consts(HostGroup& G, const g1a& pk) {
+  const fp2 g1c[5] = {C_FROB1_1, C_FROB1_2, C_FROB1_3, C_FROB1_4, C_FROB1_5};
+  const fp2 g2c[5] = {C_FROB2_1, C_FROB2_2, C_FROB2_3, C_FROB2_4, C_FROB2_5};
+  auto put = [&](int slot, const fp& v) { eng_st(G.c + (slot - 64) * ENG_SLOT_WORDS, v); };
+  put(ENG_C_ONE, fp_one());
+  put(ENG_C_NXP0, fp_neg(pk.x));
+  put(ENG_C_YP0, pk.y);
+  put(ENG_C_NXP1, fp_neg(C_G1_X));
+  put(ENG_C_YP1, C_G1_NEG_Y);
+  for (int k = 0; k < 5; ++k) {
+    put(ENG_C_G1 + 2 * k, g1c[k].c0);
+    put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
+    put(ENG_C_G2 + k, g2c[k].c0);
+  }
+}
+}  // namespace
+
+// Engine pairing check e(pk, H(msg)) e(-g1, sig) == 1 through the generated
+// programs (k_eng_lines -> k_eng_miller -> inversion -> k_eng_fe).  out576:
+// FE(f) as 12 canonical 48-byte Fp (w-basis order).  Returns 1 valid, 0 invalid.
+extern "C" int hs_eng_pairing(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig96, uint8_t* out576) {
+  g1a pk;
+  if (g1_decompress(&pk, pk48, GROUP_ORDER_WORDS) != DEC_OK) return -1;
+  g2a s;
+  if (g2_decompress(&s, sig96, true) != DEC_OK) return -2;
+  uint32_t m[8];
+  for (int w = 0; w < 8; ++w)
+    m[w] = ((uint32_t)msg32[4 * w] << 24) | ((uint32_t)msg32[4 * w + 1] << 16) | ((uint32_t)msg32[4 * w + 2] << 8) | msg32[4 * w + 3];
+  g2a h = g2_to_affine(hash_to_g2(m));
+  static HostGroup G;
+  G = HostGroup();
+  host_consts(G, pk);
+  const g2a q[2] = {h, s};
+  for (int p = 0; p < 2; ++p) {
+    const fp v[4] = {q[p].x.c0, q[p].x.c1, q[p].y.c0, q[p].y.c1};
+    for (int comp = 0; comp < 4; ++comp) {
+      G.set(p * ENG_LINE_PAIR_SLOTS + comp, v[comp]);
+      G.set(p * ENG_LINE_PAIR_SLOTS + 6 + comp, v[comp]);
+    }
+    G.set(p * ENG_LINE_PAIR_SLOTS + 4, fp_one());
+    G.set(p * ENG_LINE_PAIR_SLOTS + 5, fp_zero());
+  }
+  G.step = 0;
+  host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
+  for (int k = 0; k < 12; ++k) G.set(ENG_M_F + k, k == 0 ? fp_one() : fp_zero());
+  G.step = 0;
+  host_exec(G, ENG_PROG_MILLER, ENG_PROG_MILLER_LEN);
+  fp f[12];
+  for (int k = 0; k < 12; ++k) f[k] = G.get(ENG_M_F + k);
+  const fp n1inv = fp_inv(G.n1);
+  for (int k = 0; k < 12; ++k) G.set(ENG_E_F + k, f[k]);
+  G.set(ENG_E_N1I, n1inv);
+  host_exec(G, ENG_PROG_FE, ENG_PROG_FE_LEN);
+  bool one = true;
+  for (int k = 0; k < 12; ++k) {
+    fp v = fp_csub_p(fp_csub_p(G.get(ENG_E_R + k)));
+    fp_to_be(v, out576 + 48 * k);
+    fp cv = fp_from_mont(G.get(ENG_E_R + k));
+    bool want_one = k == 0;
+    fp_std_to_be48(cv, out576 + 48 * k);
+    uint32_t acc = 0;
+    for (int i = 0; i < FP_LIMBS; ++i) acc |= cv.l[i] ^ (want_one && i == 0 ? 1u : 0u);
+    one = one && acc == 0;
+  }
+  return one ? 1 : 0;
+}

@@ -147,3 +147,22 @@ def test_rlc_collapse_algebra(hostsim):
     assert hostsim.hs_rlc_batch_check(pk, msgs, sigs, 5, ctypes.c_uint64(99), rounds) == 0
     bad = sigs[:96] + sigs[192:288] + sigs[96:192] + sigs[288:]  # swap rounds 1 and 2
     assert hostsim.hs_rlc_batch_check(pk, msgs, bad, 5, ctypes.c_uint64(99), rounds) == 1
+
+
+def test_engine_pairing_host_emulation(hostsim):
+    """The device engine's per-lane arithmetic (engine.cuh) run by the host
+    emulation over the generated programs: verdict and the exact GT value
+    against the oracle, valid and invalid."""
+    sk = D.derive_secret(11)
+    pk = B.g1_mul(B.G1_GEN, sk)
+    pk48 = B.g1_compress(pk)
+    for msg, other in ((b"\x05" * 32, None), (b"\x06" * 32, b"\x07" * 32)):
+        sig_pt = B.g2_mul(B.hash_to_g2(other or msg), sk)
+        out = buf(576)
+        rc = hostsim.hs_eng_pairing(pk48, msg, B.g2_compress(sig_pt), out)
+        assert rc == (1 if other is None else 0)
+        fo = B.f12_mul(B.miller_loop(pk, B.hash_to_g2(msg)), B.miller_loop(B.g1_neg(B.G1_GEN), sig_pt))
+        exp = B.f12_conj(B.final_exponentiation(fo))
+        w = [exp[0][0], exp[1][0], exp[0][1], exp[1][1], exp[0][2], exp[1][2]]
+        got = [ib(out.raw[48 * k:48 * k + 48]) for k in range(12)]
+        assert got == [c % P for pair in w for c in pair]

@@ -1,0 +1,810 @@
+#!/usr/bin/env python3
+"""Generator (and executable model) of the lane-cooperative pairing engine.
+
+Design: a pairing is worked on by a GROUP of 12 lanes
+of one wavefront (5 groups per wave64).  Every Fp12 / G2 value of the group
+lives in LDS "slots" (one slot = one Fp element, 14 x 28-bit limbs,
+Montgomery form).  An OP is a list of SUB-OPS; in a sub-op every lane k of
+the group computes ONE Fp output
+
+    out = reduce( cm * redc( sum_t coef_t * a_t * b'_t )  +  sum_u d_u * s_u )
+
+where a_t, b_t, s_u are slots, b'_t is b_t or (8p - b_t) (negated), coef_t is
+1 or 2, cm and d_u are small signed integers; the product sum is
+accumulated double-width (28 limbs, no intermediate reduction: lazy
+reduction) and Montgomery-reduced once.  The output is written to a slot
+and/or exported (to HBM by the kernel).  All lanes of a sub-op read before
+any lane writes, so ops may update in place.
+
+This file
+  * builds the op tables for the three kernels (k_lines, k_miller, k_fe),
+  * emits drand_amd/csrc/engine_tables.h,
+  * provides `Model`, a Python interpreter with exactly the device
+    semantics (mod p), which tests/test_engine_model.py runs against the
+    oracle's tower arithmetic (TEST INFRASTRUCTURE only).
+
+Fp12 layout: Fp12 = Fp2[w]/(w^6 - xi), xi = 1 + u; an Fp12 value occupies 12
+consecutive slots, w^k coefficient k at slots (2k, 2k+1) = (re, im).  (The
+tower basis of tower.cuh is the same basis: c0.cj = w^(2j), c1.cj = w^(2j+1).)
+"""
+import os
+import sys
+
+LANES = 12
+MAX_GROUP_SLOTS = 64
+MAX_TERMS = 12        # engine.cuh prefetches a lane's term words into a 12-entry FIFO
+
+# ---------------------------------------------------------------- block constant slots (>= 64)
+C_ONE = 64
+C_NXP0, C_YP0, C_NXP1, C_YP1 = 65, 66, 67, 68      # pairing points (-x, y): pair 0 = pk, pair 1 = -g1
+C_G1 = 69                                         # gamma1_k, k = 1..5: (re, im) at 69 + 2(k-1)
+C_G2 = 79                                         # gamma2_k (Fp), k = 1..5 at 79 + (k-1)
+N_CONST = 20
+
+# export ids (k_lines): pair p line component e (l0.re, l0.im, l2.re, l2.im, l3.re, l3.im) -> 6p + e
+# export ids (k_miller): 0..11 = f components, 12 = N1 (the Fp norm of f)
+EXP_N1 = 12
+
+
+class Rec:
+    __slots__ = ("dst", "exp", "cm", "terms", "post")
+
+    def __init__(self, dst=None, exp=None, cm=1, terms=(), post=()):
+        self.dst, self.exp, self.cm = dst, exp, cm
+        self.terms = list(terms)   # (a, b, sign, coef)   sign in {+1,-1}, coef in {1,2}
+        self.post = list(post)     # (slot, d)
+        if not self.terms:
+            self.cm = 0
+
+
+def T(a, b, sign=1, coef=1):
+    return (a, b, sign, coef)
+
+
+# ---------------------------------------------------------------- Fp2 helpers (slot pairs)
+def fp2(base):
+    return (base, base + 1)
+
+
+def mul_terms(x, y, sign=1, coef=1):
+    """(x*y).re and (x*y).im as term lists; x, y slot pairs."""
+    re = [T(x[0], y[0], sign, coef), T(x[1], y[1], -sign, coef)]
+    im = [T(x[0], y[1], sign, coef), T(x[1], y[0], sign, coef)]
+    return re, im
+
+
+def sqr_terms(x, sign=1, coef=1):
+    """(x^2).re = x0^2 - x1^2, (x^2).im = 2 x0 x1"""
+    re = [T(x[0], x[0], sign, coef), T(x[1], x[1], -sign, coef)]
+    if coef == 1:
+        im = [T(x[0], x[1], sign, 2)]
+    else:
+        im = [T(x[0], x[1], sign, 2), T(x[0], x[1], sign, 2)]
+    return re, im
+
+
+def fp12(base):
+    return [fp2(base + 2 * k) for k in range(6)]
+
+
+# ---------------------------------------------------------------- op builders
+class Op:
+    def __init__(self, name, subs):
+        self.name = name
+        self.subs = subs  # list of list[Rec] (<= 12 each)
+        for s in subs:
+            assert len(s) <= LANES, (name, len(s))
+
+
+def pack(name, recs):
+    """Split a flat list of records into sub-ops of <= 12 lanes."""
+    return Op(name, [recs[i:i + LANES] for i in range(0, len(recs), LANES)])
+
+
+def op_xi_copy(name, src_base, dst_base, ks):
+    """dst[j] = xi * src[k] for k in ks (j-th copy), LIN."""
+    recs = []
+    for j, k in enumerate(ks):
+        s = fp2(src_base + 2 * k)
+        d = fp2(dst_base + 2 * j)
+        recs.append(Rec(dst=d[0], post=[(s[0], 1), (s[1], -1)]))
+        recs.append(Rec(dst=d[1], post=[(s[0], 1), (s[1], 1)]))
+    return pack(name, recs)
+
+
+def op_sqr12(name, F, XF, conj=False):
+    """F <- F^2 (conj: F <- conj(F)^2 = conj(F^2)), in place; XF = xi*F[1..5]."""
+    f = fp12(F)
+    xf = {k: fp2(XF + 2 * (k - 1)) for k in range(1, 6)}
+    recs = []
+    for k in range(6):
+        re, im = [], []
+        for i in range(6):
+            for j in range(i, 6):
+                if (i + j) % 6 != k:
+                    continue
+                wrap = i + j >= 6
+                y = xf[j] if wrap else f[j]
+                if i == j and not wrap:
+                    r, m = sqr_terms(f[i])
+                elif i == j:
+                    r, m = mul_terms(f[i], y)
+                else:
+                    r, m = mul_terms(f[i], y, coef=2)
+                re += r
+                im += m
+        sgn = -1 if (conj and k % 2) else 1
+        recs.append(Rec(dst=f[k][0], cm=sgn, terms=re))
+        recs.append(Rec(dst=f[k][1], cm=sgn, terms=im))
+    return pack(name, recs)
+
+
+def op_line_mul(name, F, L, XL):
+    """F <- F * (l0 + l2 w^2 + l3 w^3); L = (l0, l2, l3) at L..L+5, XL = (xi l2, xi l3)."""
+    f = fp12(F)
+    l0, l2, l3 = fp2(L), fp2(L + 2), fp2(L + 4)
+    xl2, xl3 = fp2(XL), fp2(XL + 2)
+    recs = []
+    for k in range(6):
+        re, im = [], []
+        for src, coeff, xcoeff, sh in ((k, l0, l0, 0), ((k - 2) % 6, l2, xl2, 2), ((k - 3) % 6, l3, xl3, 3)):
+            y = xcoeff if k < sh else coeff
+            r, m = mul_terms(f[src], y)
+            re += r
+            im += m
+        recs.append(Rec(dst=f[k][0], terms=re))
+        recs.append(Rec(dst=f[k][1], terms=im))
+    return pack(name, recs)
+
+
+def op_mul12(name, R, A, XA, conj_a=False):
+    """R <- R * A (conj_a: R * conj(A)); XA = xi*A[1..5]."""
+    r, a = fp12(R), fp12(A)
+    xa = {k: fp2(XA + 2 * (k - 1)) for k in range(1, 6)}
+    recs = []
+    for k in range(6):
+        re, im = [], []
+        for i in range(6):
+            j = (k - i) % 6
+            y = a[j] if i <= k else xa[j]
+            s = -1 if (conj_a and j % 2) else 1
+            rr, mm = mul_terms(r[i], y, sign=s)
+            re += rr
+            im += mm
+        recs.append(Rec(dst=r[k][0], terms=re))
+        recs.append(Rec(dst=r[k][1], terms=im))
+    return pack(name, recs)
+
+
+def op_mul_fp6(name, R, N, XN, out=None):
+    """out <- R * n, n = n0 + n1 w^2 + n2 w^4 (slots N: n0, n1, n2), XN = (xi n1, xi n2)."""
+    r = fp12(R)
+    o = fp12(out if out is not None else R)
+    n = [fp2(N + 2 * j) for j in range(3)]
+    xn = {1: fp2(XN), 2: fp2(XN + 2)}
+    recs = []
+    for k in range(6):
+        re, im = [], []
+        for j in range(3):
+            i = (k - 2 * j) % 6
+            y = xn[j] if 2 * j > k else n[j]
+            rr, mm = mul_terms(r[i], y)
+            re += rr
+            im += mm
+        recs.append(Rec(dst=o[k][0], terms=re))
+        recs.append(Rec(dst=o[k][1], terms=im))
+    return pack(name, recs)
+
+
+def op_norm6(name, F, XF, N):
+    """N <- f * conj(f) (in Fp6: coefficients of w^0, w^2, w^4)."""
+    f = fp12(F)
+    xf = {k: fp2(XF + 2 * (k - 1)) for k in range(1, 6)}
+    recs = []
+    for jj, k in enumerate((0, 2, 4)):
+        re, im = [], []
+        for i in range(6):
+            for m in range(i, 6):
+                if (i + m) % 6 != k:
+                    continue
+                wrap = i + m >= 6
+                y = xf[m] if wrap else f[m]
+                s = -1 if m % 2 else 1
+                if i == m:
+                    rr, mm = (sqr_terms(f[i], sign=s) if not wrap else mul_terms(f[i], y, sign=s))
+                else:
+                    rr, mm = mul_terms(f[i], y, sign=s, coef=2)
+                re += rr
+                im += mm
+        d = fp2(N + 2 * jj)
+        recs.append(Rec(dst=d[0], terms=re))
+        recs.append(Rec(dst=d[1], terms=im))
+    return pack(name, recs)
+
+
+def fp2_out(recs, dst, re, im, exp=None, cm=1):
+    recs.append(Rec(dst=dst[0] if dst else None, exp=None if exp is None else exp, cm=cm, terms=re))
+    recs.append(Rec(dst=dst[1] if dst else None, exp=None if exp is None else exp + 1, cm=cm, terms=im))
+
+
+def op_fp6_inv_t(name, N, XN2, Tt):
+    """t0 = n0^2 - n1 (xi n2), t1 = n2 (xi n2) - n0 n1, t2 = n1^2 - n0 n2  ->  Tt (6 slots)"""
+    n0, n1, n2 = fp2(N), fp2(N + 2), fp2(N + 4)
+    xn2 = fp2(XN2)
+    recs = []
+    a, b = sqr_terms(n0)
+    c, d = mul_terms(n1, xn2, sign=-1)
+    fp2_out(recs, fp2(Tt), a + c, b + d)
+    a, b = mul_terms(n2, xn2)
+    c, d = mul_terms(n0, n1, sign=-1)
+    fp2_out(recs, fp2(Tt + 2), a + c, b + d)
+    a, b = sqr_terms(n1)
+    c, d = mul_terms(n0, n2, sign=-1)
+    fp2_out(recs, fp2(Tt + 4), a + c, b + d)
+    return pack(name, recs)
+
+
+def op_fp6_inv_d(name, N, Tt, XT, D):
+    """d = n0 t0 + n2 (xi t1) + n1 (xi t2)"""
+    n0, n1, n2 = fp2(N), fp2(N + 2), fp2(N + 4)
+    t0 = fp2(Tt)
+    xt1, xt2 = fp2(XT), fp2(XT + 2)
+    recs = []
+    a, b = mul_terms(n0, t0)
+    c, d = mul_terms(n2, xt1)
+    e, f = mul_terms(n1, xt2)
+    fp2_out(recs, fp2(D), a + c + e, b + d + f)
+    return pack(name, recs)
+
+
+def op_n1(name, D, N1, exp=None):
+    d = fp2(D)
+    return pack(name, [Rec(dst=N1, exp=exp, terms=[T(d[0], d[0]), T(d[1], d[1])])])
+
+
+def op_ninv(name, D, N1I, Tt, DI, NI):
+    """dinv = conj(d) * n1inv, then Ninv_j = t_j * dinv (two ops)"""
+    d = fp2(D)
+    op1 = pack(name + "_d", [Rec(dst=DI, terms=[T(d[0], N1I)]), Rec(dst=DI + 1, terms=[T(d[1], N1I, -1)])])
+    recs = []
+    for j in range(3):
+        a, b = mul_terms(fp2(Tt + 2 * j), fp2(DI))
+        fp2_out(recs, fp2(NI + 2 * j), a, b)
+    return op1, pack(name, recs)
+
+
+def op_frob(name, A, power, out=None):
+    """out <- A^(p^power), power in (1, 2)."""
+    a = fp12(A)
+    o = fp12(out if out is not None else A)
+    recs = []
+    for k in range(6):
+        x = a[k]
+        if k == 0:
+            if power == 1:
+                recs.append(Rec(dst=o[0][0], post=[(x[0], 1)]))
+                recs.append(Rec(dst=o[0][1], post=[(x[1], -1)]))
+            else:
+                recs.append(Rec(dst=o[0][0], post=[(x[0], 1)]))
+                recs.append(Rec(dst=o[0][1], post=[(x[1], 1)]))
+            continue
+        if power == 1:
+            g = fp2(C_G1 + 2 * (k - 1))
+            # conj(x) * g: re = x0 g0 + x1 g1, im = x0 g1 - x1 g0
+            recs.append(Rec(dst=o[k][0], terms=[T(x[0], g[0]), T(x[1], g[1])]))
+            recs.append(Rec(dst=o[k][1], terms=[T(x[0], g[1]), T(x[1], g[0], -1)]))
+        else:
+            g = C_G2 + (k - 1)
+            recs.append(Rec(dst=o[k][0], terms=[T(x[0], g)]))
+            recs.append(Rec(dst=o[k][1], terms=[T(x[1], g)]))
+    return pack(name, recs)
+
+
+def op_copy(name, A, B, conj=False):
+    recs = []
+    for k in range(6):
+        s = -1 if (conj and k % 2) else 1
+        for c in range(2):
+            recs.append(Rec(dst=B + 2 * k + c, post=[(A + 2 * k + c, s)]))
+    return pack(name, recs)
+
+
+def op_conj(name, R):
+    recs = []
+    for k in (1, 3, 5):
+        for c in range(2):
+            recs.append(Rec(dst=R + 2 * k + c, post=[(R + 2 * k + c, -1)]))
+    return pack(name, recs)
+
+
+def op_cyclo_sqr(name, R, TMP):
+    """Granger-Scott squaring in the cyclotomic subgroup, in place.
+    Fp4 pairs A = (f0, f3), B = (f1, f4), C = (f2, f5):
+      f0' = 3(f0^2 + xi f3^2) - 2 f0     f3' = 6 f0 f3 + 2 f3
+      f1' = 6 xi f2 f5 + 2 f1            f4' = 3(f2^2 + xi f5^2) - 2 f4
+      f2' = 3(f1^2 + xi f4^2) - 2 f2     f5' = 6 f1 f4 + 2 f5
+    Two sub-ops: a LIN pass writes a+b, a-b, c+d, c-d for each pair
+    (x0 = a + bu, x1 = c + du) to TMP, so that every output needs at most 3
+    products:  (x0^2 + xi x1^2).re = (a+b)(a-b) + (c+d)(c-d) - 2cd,
+               (x0^2 + xi x1^2).im = 2ab + (c+d)(c-d) + 2cd,
+               (2 x0 x1).re = 2ac - 2bd,  (2 x0 x1).im = 2ad + 2bc."""
+    f = fp12(R)
+    pairs = {0: (0, 3), 1: (1, 4), 2: (2, 5)}   # Fp4 pair j = (f_j, f_{j+3})
+    lin = []
+    tmp = {}
+    for j, (i0, i1) in pairs.items():
+        a, b = f[i0]
+        c_, d = f[i1]
+        base = TMP + 4 * j
+        tmp[j] = (base, base + 1, base + 2, base + 3)  # a+b, a-b, c+d, c-d
+        lin.append(Rec(dst=base, post=[(a, 1), (b, 1)]))
+        lin.append(Rec(dst=base + 1, post=[(a, 1), (b, -1)]))
+        lin.append(Rec(dst=base + 2, post=[(c_, 1), (d, 1)]))
+        lin.append(Rec(dst=base + 3, post=[(c_, 1), (d, -1)]))
+
+    def s_terms(j, xi_outer=False):
+        (i0, i1) = pairs[j]
+        a, b = f[i0]
+        c_, d = f[i1]
+        apb, amb, cpd, cmd = tmp[j]
+        re = [T(apb, amb), T(cpd, cmd), T(c_, d, -1, 2)]
+        im = [T(a, b, 1, 2), T(cpd, cmd), T(c_, d, 1, 2)]
+        return re, im
+
+    def t_terms(j):
+        (i0, i1) = pairs[j]
+        a, b = f[i0]
+        c_, d = f[i1]
+        re = [T(a, c_, 1, 2), T(b, d, -1, 2)]
+        im = [T(a, d, 1, 2), T(b, c_, 1, 2)]
+        return re, im
+
+    recs = []
+    # f0' = 3 S(A) - 2 f0 ; f3' = 3 T(A) + 2 f3
+    for k, (re, im), cm, dd in ((0, s_terms(0), 3, -2), (3, t_terms(0), 3, 2),
+                                (4, s_terms(2), 3, -2), (2, s_terms(1), 3, -2), (5, t_terms(1), 3, 2)):
+        recs.append(Rec(dst=f[k][0], cm=cm, terms=re, post=[(f[k][0], dd)]))
+        recs.append(Rec(dst=f[k][1], cm=cm, terms=im, post=[(f[k][1], dd)]))
+    # f1' = 3 xi T(C) + 2 f1: xi (r + s u) = (r - s) + (r + s) u with T(C) = 2 x0 x1 (x0 = f2, x1 = f5)
+    (i0, i1) = pairs[2]
+    a, b = f[i0]
+    c_, d = f[i1]
+    tr = [T(a, c_, 1, 2), T(b, d, -1, 2)]
+    ti = [T(a, d, 1, 2), T(b, c_, 1, 2)]
+    neg = lambda ts: [(x, y, -sg, cf) for (x, y, sg, cf) in ts]  # noqa: E731
+    recs.append(Rec(dst=f[1][0], cm=3, terms=tr + neg(ti), post=[(f[1][0], 2)]))
+    recs.append(Rec(dst=f[1][1], cm=3, terms=tr + ti, post=[(f[1][1], 2)]))
+    return Op(name, [lin, recs])
+
+
+# ---------------------------------------------------------------- k_lines: T steps for two pairs
+# per pair p (slot base 24 p): X 0,1  Y 2,3  Z 4,5  xQ 6,7  yQ 8,9  temporaries 10..23
+LINE_PAIR_SLOTS = 24
+
+
+def _pb(p, off):
+    return LINE_PAIR_SLOTS * p + off
+
+
+def lines_dbl_op():
+    """Doubling step on T = (X, Y, Z) (homogeneous projective, T scaled by 4
+    relative to oracle/pairing_formulas.dbl_step: a subfield factor), with
+    line l = (Y^2 - 3b'Z^2) + (-3X^2 xP) w^2 + (2YZ yP) w^3:
+      t0 = Y^2, t1 = Z^2, w = 12 xi t1 (= 3b' Z^2), u = t0 - 3w, v = t0 + 3w
+      X4 = 2 XY u,  Y4 = v^2 - 12 w^2,  Z4 = 8 t0 YZ
+      l0 = t0 - w,  l2 = 3 X^2 (-xP),  l3 = 2 YZ yP"""
+    S1, S2, S3, S4, S5 = [], [], [], [], []
+    for p in range(2):
+        X, Y, Z = fp2(_pb(p, 0)), fp2(_pb(p, 2)), fp2(_pb(p, 4))
+        X2, XY, YZ = fp2(_pb(p, 10)), fp2(_pb(p, 12)), fp2(_pb(p, 14))
+        W, U, V = fp2(_pb(p, 16)), fp2(_pb(p, 18)), fp2(_pb(p, 20))
+        nxp, yp = (C_NXP0, C_YP0) if p == 0 else (C_NXP1, C_YP1)
+        # S1: X2 = X^2, XY = X Y, YZ = Y Z
+        fp2_out(S1, X2, *sqr_terms(X))
+        fp2_out(S1, XY, *mul_terms(X, Y))
+        fp2_out(S1, YZ, *mul_terms(Y, Z))
+        # S2: t0 = Y^2 -> X slot, t1 = Z^2 -> Y slot; l2 = 3 X2 (-xP) (export)
+        fp2_out(S2, X, *sqr_terms(Y))
+        fp2_out(S2, Y, *sqr_terms(Z))
+        S2.append(Rec(exp=6 * p + 2, cm=3, terms=[T(X2[0], nxp)]))
+        S2.append(Rec(exp=6 * p + 3, cm=3, terms=[T(X2[1], nxp)]))
+        t0, t1 = X, Y
+        # S3 (LIN): w = 12 xi t1, u = t0 - 36 xi t1, v = t0 + 36 xi t1
+        S3.append(Rec(dst=W[0], post=[(t1[0], 12), (t1[1], -12)]))
+        S3.append(Rec(dst=W[1], post=[(t1[0], 12), (t1[1], 12)]))
+        S3.append(Rec(dst=U[0], post=[(t0[0], 1), (t1[0], -36), (t1[1], 36)]))
+        S3.append(Rec(dst=U[1], post=[(t0[1], 1), (t1[0], -36), (t1[1], -36)]))
+        S3.append(Rec(dst=V[0], post=[(t0[0], 1), (t1[0], 36), (t1[1], -36)]))
+        S3.append(Rec(dst=V[1], post=[(t0[1], 1), (t1[0], 36), (t1[1], 36)]))
+        # S4: l0 = t0 - w (export), w12 = 12 w -> Y slot (t1 dead), l3 = 2 YZ yP (export)
+        S4.append(Rec(exp=6 * p + 0, post=[(t0[0], 1), (W[0], -1)]))
+        S4.append(Rec(exp=6 * p + 1, post=[(t0[1], 1), (W[1], -1)]))
+        S4.append(Rec(dst=Y[0], post=[(W[0], 12)]))
+        S4.append(Rec(dst=Y[1], post=[(W[1], 12)]))
+        S4.append(Rec(exp=6 * p + 4, cm=2, terms=[T(YZ[0], yp)]))
+        S4.append(Rec(exp=6 * p + 5, cm=2, terms=[T(YZ[1], yp)]))
+        W12 = Y
+        # S5: X4 = 2 XY u -> X, Y4 = v^2 - w w12 -> Y, Z4 = 8 t0 YZ -> Z
+        fp2_out(S5, X, *mul_terms(XY, U, coef=2))
+        a, b = sqr_terms(V)
+        c, d = mul_terms(W, W12, sign=-1)
+        fp2_out(S5, Y, a + c, b + d)
+        fp2_out(S5, Z, *mul_terms(t0, YZ), cm=8)
+    return Op("LDBL", [S1, S2, S3, S4, S5])
+
+
+def lines_add_op():
+    """Mixed addition T + Q (Q affine at xQ, yQ):
+      theta = Y - yQ Z, lam = X - xQ Z, C = theta^2, D = lam^2, E = lam D,
+      F = Z C, G = X D, H = E + F - 2G,
+      X' = lam H, Y' = theta (G - H) - Y E, Z' = Z E,
+      l0 = theta xQ - lam yQ, l2 = theta (-xP), l3 = lam yP"""
+    S1, S2, S3, S4, S5, S6 = [], [], [], [], [], []
+    for p in range(2):
+        X, Y, Z = fp2(_pb(p, 0)), fp2(_pb(p, 2)), fp2(_pb(p, 4))
+        xQ, yQ = fp2(_pb(p, 6)), fp2(_pb(p, 8))
+        TH, LA, C, D = fp2(_pb(p, 10)), fp2(_pb(p, 12)), fp2(_pb(p, 14)), fp2(_pb(p, 16))
+        E, F, G = fp2(_pb(p, 18)), fp2(_pb(p, 20)), fp2(_pb(p, 22))
+        H, GH = C, D
+        nxp, yp = (C_NXP0, C_YP0) if p == 0 else (C_NXP1, C_YP1)
+        # S1: theta = Y - yQ Z, lam = X - xQ Z
+        a, b = mul_terms(yQ, Z)
+        S1.append(Rec(dst=TH[0], cm=-1, terms=a, post=[(Y[0], 1)]))
+        S1.append(Rec(dst=TH[1], cm=-1, terms=b, post=[(Y[1], 1)]))
+        a, b = mul_terms(xQ, Z)
+        S1.append(Rec(dst=LA[0], cm=-1, terms=a, post=[(X[0], 1)]))
+        S1.append(Rec(dst=LA[1], cm=-1, terms=b, post=[(X[1], 1)]))
+        # S2: C = theta^2, D = lam^2, l2 = theta (-xP)
+        fp2_out(S2, C, *sqr_terms(TH))
+        fp2_out(S2, D, *sqr_terms(LA))
+        S2.append(Rec(exp=6 * p + 2, terms=[T(TH[0], nxp)]))
+        S2.append(Rec(exp=6 * p + 3, terms=[T(TH[1], nxp)]))
+        # S3: l0 = theta xQ - lam yQ, l3 = lam yP
+        a, b = mul_terms(TH, xQ)
+        c, d = mul_terms(LA, yQ, sign=-1)
+        S3.append(Rec(exp=6 * p + 0, terms=a + c))
+        S3.append(Rec(exp=6 * p + 1, terms=b + d))
+        S3.append(Rec(exp=6 * p + 4, terms=[T(LA[0], yp)]))
+        S3.append(Rec(exp=6 * p + 5, terms=[T(LA[1], yp)]))
+        # S4: E = lam D, F = Z C, G = X D
+        fp2_out(S4, E, *mul_terms(LA, D))
+        fp2_out(S4, F, *mul_terms(Z, C))
+        fp2_out(S4, G, *mul_terms(X, D))
+        # S5 (LIN): H = E + F - 2G -> C slot, GH = G - H = 3G - E - F -> D slot
+        for c_ in range(2):
+            S5.append(Rec(dst=H[c_], post=[(E[c_], 1), (F[c_], 1), (G[c_], -2)]))
+        for c_ in range(2):
+            S5.append(Rec(dst=GH[c_], post=[(G[c_], 3), (E[c_], -1), (F[c_], -1)]))
+        # S6: X' = lam H, Y' = theta GH - Y E, Z' = Z E
+        fp2_out(S6, X, *mul_terms(LA, H))
+        a, b = mul_terms(TH, GH)
+        c, d = mul_terms(Y, E, sign=-1)
+        fp2_out(S6, Y, a + c, b + d)
+        fp2_out(S6, Z, *mul_terms(Z, E))
+    return Op("LADD", [S1, S2, S3, S4, S5, S6])
+
+
+# ---------------------------------------------------------------- k_miller slots
+M_F, M_X, M_L1, M_L2 = 0, 12, 22, 28      # F (12), xi-copies (10), line 1 (6), line 2 (6)
+M_N, M_XN2, M_T, M_XT, M_D, M_N1 = 22, 12, 14, 28, 20, 12  # norm epilogue (after the loop)
+
+# ---------------------------------------------------------------- k_fe slots
+E_F, E_X, E_N, E_XN2, E_T, E_XT, E_D, E_N1I, E_DI = 0, 12, 22, 28, 30, 36, 40, 42, 43
+E_NI, E_XNI = 22, 28          # Ninv (6, over N), xi Ninv1, xi Ninv2 (4, over XN2 and t0)
+E_R, E_A, E_XA, E_CT = 0, 12, 24, 34   # hard part: R (12), A (12), xi A (10), cyclotomic-squaring temps (12)
+
+
+def build_ops():
+    ops = []
+    # k_lines
+    ops.append(lines_dbl_op())
+    ops.append(lines_add_op())
+    # k_miller
+    ops.append(op_xi_copy("M_XIF", M_F, M_X, [1, 2, 3, 4, 5]))
+    ops.append(op_sqr12("M_SQR", M_F, M_X))
+    # xi l2, xi l3 for both lines: L1 (l0, l2, l3) at 22, L2 at 28 -> X 12..15 and 16..19
+    ops.append(pack("M_XIL", op_xi_copy("_a", M_L1, M_X, [1, 2]).subs[0] + op_xi_copy("_b", M_L2, M_X + 4, [1, 2]).subs[0]))
+    ops.append(op_line_mul("M_LM1", M_F, M_L1, M_X))
+    ops.append(op_line_mul("M_LM2", M_F, M_L2, M_X + 4))
+    ops.append(op_norm6("M_NRM", M_F, M_X, M_N))
+    ops.append(op_xi_copy("M_XIN2", M_N, M_XN2, [2]))
+    ops.append(op_fp6_inv_t("M_T012", M_N, M_XN2, M_T))
+    ops.append(op_xi_copy("M_XIT", M_T, M_XT, [1, 2]))
+    ops.append(op_fp6_inv_d("M_D", M_N, M_T, M_XT, M_D))
+    ops.append(op_n1("M_N1", M_D, M_N1, exp=EXP_N1))
+    # k_fe: easy part
+    ops.append(op_xi_copy("E_XIF", E_F, E_X, [1, 2, 3, 4, 5]))
+    ops.append(op_norm6("E_NRM", E_F, E_X, E_N))
+    ops.append(op_xi_copy("E_XIN2", E_N, E_XN2, [2]))
+    ops.append(op_fp6_inv_t("E_T012", E_N, E_XN2, E_T))
+    ops.append(op_xi_copy("E_XIT", E_T, E_XT, [1, 2]))
+    ops.append(op_fp6_inv_d("E_D", E_N, E_T, E_XT, E_D))
+    o1, o2 = op_ninv("E_NINV", E_D, E_N1I, E_T, E_DI, E_NI)
+    ops.append(o1)
+    ops.append(o2)
+    ops.append(op_xi_copy("E_XINI", E_NI, E_XNI, [1, 2]))
+    ops.append(op_sqr12("E_SQRC", E_F, E_X, conj=True))          # F <- conj(f)^2
+    ops.append(op_mul_fp6("E_MULN", E_F, E_NI, E_XNI))           # F <- F * Ninv  (= f^(p^6-1))
+    # (F = R from here on: E_R == E_F == 0)
+    ops.append(op_frob("E_FROB2A", E_R, 2, out=E_A))             # A <- frob2(R)
+    ops.append(op_xi_copy("E_XIA", E_A, E_XA, [1, 2, 3, 4, 5]))
+    ops.append(op_mul12("E_MUL", E_R, E_A, E_XA))                # R <- R * A
+    ops.append(op_mul12("E_MULCJ", E_R, E_A, E_XA, conj_a=True)) # R <- R * conj(A)
+    ops.append(op_copy("E_COPYRA", E_R, E_A))                    # A <- R
+    ops.append(op_conj("E_CONJ", E_R))                           # R <- conj(R)
+    ops.append(op_cyclo_sqr("E_CYC", E_R, E_CT))                 # R <- R^2 (cyclotomic)
+    ops.append(op_cyclo_sqr("E_CYCA", E_A, E_CT))                # A <- A^2 (cyclotomic)
+    ops.append(op_frob("E_FROB1", E_A, 1))                       # A <- frob1(A)
+    ops.append(op_frob("E_FROB2", E_A, 2))                       # A <- frob2(A)
+    return ops
+
+
+# ---------------------------------------------------------------- kernel programs
+# Each engine kernel executes one linear program (a single interpreter loop on
+# the device, so the interpreter is inlined once).  Instructions:
+#   ("run", op)           run op; its exports go to lines[step][e] (e < 12) or n1 (e == 12)
+#   ("step",)             step += 1 (line index of exports and ldline)
+#   ("ldline", slot)      lane k: slot + k <- lines[step][k]; step += 1
+#   ("ld12", slot, comp)  lane k: slot + k <- fbuf[comp + k]
+#   ("st12", slot, comp)  lane k: fbuf[comp + k] <- slot + k
+OPC = {"run": 0, "step": 1, "ldline": 2, "ld12": 3, "st12": 4}
+BITS = [(0xD201000000010000 >> i) & 1 for i in range(62, -1, -1)]
+
+
+def prog_lines():
+    prog = []
+    for b in BITS:
+        prog += [("run", "LDBL"), ("step",)]
+        if b:
+            prog += [("run", "LADD"), ("step",)]
+    return prog
+
+
+def prog_miller():
+    prog = []
+    line = [("ldline", M_L1), ("run", "M_XIL"), ("run", "M_LM1"), ("run", "M_LM2")]
+    for j, b in enumerate(BITS):
+        if j:
+            prog += [("run", "M_XIF"), ("run", "M_SQR")]
+        prog += line
+        if b:
+            prog += line
+    prog += [("run", n) for n in ("M_XIF", "M_NRM", "M_XIN2", "M_T012", "M_XIT", "M_D", "M_N1")]
+    return prog
+
+
+def prog_fe():
+    """Final exponentiation; on entry F = f (slots 0..11), slot E_N1I = 1/N1.
+    On exit R = FE(f).  fbuf components 0..11 hold t, 12..23 t2."""
+    run = lambda *names: [("run", n) for n in names]  # noqa: E731
+    prog = run("E_XIF", "E_NRM", "E_XIN2", "E_T012", "E_XIT", "E_D", "E_NINV_d", "E_NINV", "E_XINI",
+               "E_SQRC", "E_MULN", "E_FROB2A", "E_XIA", "E_MUL")
+    prog += [("st12", E_R, 0)]
+
+    def exp_x():  # A <- R, R <- conj(R^|x|)
+        p = run("E_COPYRA", "E_XIA")
+        for b in BITS:
+            p += run("E_CYC")
+            if b:
+                p += run("E_MUL")
+        return p + run("E_CONJ")
+
+    prog += exp_x() + run("E_MULCJ")                      # t0 = t^x conj(t)
+    prog += exp_x() + run("E_MULCJ")                      # t1 = t0^x conj(t0)
+    prog += exp_x() + run("E_FROB1", "E_XIA", "E_MUL")    # t2 = t1^x t1^p
+    prog += [("st12", E_R, 12)]
+    prog += exp_x() + exp_x()
+    prog += [("ld12", E_A, 12)] + run("E_FROB2", "E_XIA", "E_MUL")
+    prog += [("ld12", E_A, 12)] + run("E_XIA", "E_MULCJ")  # t3 = t2^(x^2) t2^(p^2) conj(t2)
+    prog += [("ld12", E_A, 0)] + run("E_XIA", "E_MUL", "E_CYCA", "E_XIA", "E_MUL")  # t3 t^3
+    return prog
+
+
+def encode_prog(prog, op_index):
+    out = []
+    for ins in prog:
+        opc = OPC[ins[0]]
+        a = op_index[ins[1]] if ins[0] == "run" else (ins[1] if len(ins) > 1 else 0)
+        b = ins[2] if len(ins) > 2 else 0
+        out.append((opc << 24) | (b << 8) | a)
+    return out
+
+
+class ProgramRunner:
+    """Executes a kernel program on a Model (one group) with simulated HBM."""
+
+    def __init__(self, model):
+        self.m = model
+        self.step = 0
+        self.lines = {}   # (step, e) -> value
+        self.fbuf = {}
+        self.n1 = None
+
+    def run(self, prog):
+        m = self.m
+        for ins in prog:
+            kind = ins[0]
+            if kind == "run":
+                m.exports = {}
+                m.run(ins[1])
+                for e, v in m.exports.items():
+                    if e < 12:
+                        self.lines[(self.step, e)] = v
+                    else:
+                        self.n1 = v
+            elif kind == "step":
+                self.step += 1
+            elif kind == "ldline":
+                for k in range(LANES):
+                    m.s[ins[1] + k] = self.lines[(self.step, k)]
+                self.step += 1
+            elif kind == "ld12":
+                for k in range(LANES):
+                    m.s[ins[1] + k] = self.fbuf[ins[2] + k]
+            elif kind == "st12":
+                for k in range(LANES):
+                    self.fbuf[ins[2] + k] = m.s[ins[1] + k]
+
+
+# ---------------------------------------------------------------- table emission
+def encode(ops):
+    words = []
+    op_tab = []
+    sub_tab = []
+    for op in ops:
+        op_tab.append((len(sub_tab), len(op.subs)))
+        for sub in op.subs:
+            nt = max([len(r.terms) for r in sub] + [0])
+            assert nt <= MAX_TERMS, (op.name, nt)
+            sub_tab.append((len(words), nt))
+            for k in range(LANES):
+                r = sub[k] if k < len(sub) else None
+                if r is None:
+                    words += [0xFFFF, 0, 0, 0] + [0] * nt
+                    continue
+                assert len(r.post) <= 3 and -16 < r.cm < 16
+                dst = 0xFF if r.dst is None else r.dst
+                exp = 0xFF if r.exp is None else r.exp
+                h0 = dst | (exp << 8) | ((r.cm & 0xFF) << 16) | (len(r.post) << 24)
+                posts = [((s & 0xFF) | ((d & 0xFFFF) << 16)) for s, d in r.post] + [0] * (3 - len(r.post))
+                words += [h0] + posts
+                for t in range(nt):
+                    if t < len(r.terms):
+                        a, b, sg, cf = r.terms[t]
+                        assert cf in (1, 2) and sg in (1, -1)
+                        words.append((a & 0xFF) | ((b & 0xFF) << 8) | ((sg < 0) << 16) | ((cf == 2) << 17) | (1 << 31))
+                    else:
+                        words.append(0)
+    return op_tab, sub_tab, words
+
+
+def check_bounds(ops):
+    """Static bounds the device arithmetic relies on (see engine.cuh):
+    slot values < 2.01p; product sum < 2048 p^2 so redc < 1.8p; the post
+    linear combination stays < 2^392."""
+    for op in ops:
+        for sub in op.subs:
+            for r in sub:
+                # negated operands are 8p - b (FP_SUBK), < 8p
+                prod = sum(cf * 2.01 * (8.0 if sg < 0 else 2.01) for _, _, sg, cf in r.terms)
+                assert prod < 2048, (op.name, prod)
+                # redc output < 1.8p; negative multipliers act on 8p - x
+                lin = abs(r.cm) * (8.0 if r.cm < 0 else 1.8) + sum(abs(d) * (8.0 if d < 0 else 2.01) for _, d in r.post)
+                assert lin < 2500, (op.name, lin)
+                for a, b, _, _ in r.terms:
+                    assert a < 64 + N_CONST and b < 64 + N_CONST
+                for s, _ in r.post:
+                    assert s < 64 + N_CONST
+
+
+def emit(path):
+    ops = build_ops()
+    check_bounds(ops)
+    op_tab, sub_tab, words = encode(ops)
+    nslots = {}
+    for op in ops:
+        m = 0
+        for sub in op.subs:
+            for r in sub:
+                for s in [r.dst] + [t[0] for t in r.terms] + [t[1] for t in r.terms] + [p[0] for p in r.post]:
+                    if s is not None and s < 64:
+                        m = max(m, s + 1)
+        nslots[op.name] = m
+    lines = [
+        "// GENERATED by tools/gen_engine.py -- do not edit.",
+        "// Micro-op tables of the lane-cooperative pairing engine (engine.cuh).",
+        "#pragma once",
+        "#include <cstdint>",
+        "",
+        "namespace dgpu {",
+        "",
+        f"constexpr int ENG_LANES = {LANES};",
+        f"constexpr int ENG_MAX_TERMS = {MAX_TERMS};",
+        f"constexpr int ENG_NCONST = {N_CONST};",
+        f"constexpr int ENG_C_ONE = {C_ONE}, ENG_C_NXP0 = {C_NXP0}, ENG_C_YP0 = {C_YP0}, ENG_C_NXP1 = {C_NXP1}, ENG_C_YP1 = {C_YP1};",
+        f"constexpr int ENG_C_G1 = {C_G1}, ENG_C_G2 = {C_G2};",
+        f"constexpr int ENG_LINE_PAIR_SLOTS = {LINE_PAIR_SLOTS};",
+        f"constexpr int ENG_M_F = {M_F}, ENG_M_L1 = {M_L1}, ENG_M_L2 = {M_L2}, ENG_EXP_N1 = {EXP_N1};",
+        f"constexpr int ENG_E_F = {E_F}, ENG_E_N1I = {E_N1I}, ENG_E_R = {E_R}, ENG_E_A = {E_A};",
+        "",
+        "enum EngOp : int {",
+    ]
+    for i, op in enumerate(ops):
+        lines.append(f"  OP_{op.name} = {i},  // {len(op.subs)} sub-op(s), slots < {nslots[op.name]}")
+    lines.append("};")
+    nsl = {
+        "LINES": max(nslots["LDBL"], nslots["LADD"]),
+        "MILLER": max(v for k, v in nslots.items() if k.startswith("M_")),
+        "FE": max(v for k, v in nslots.items() if k.startswith("E_")),
+    }
+    for k, v in nsl.items():
+        lines.append(f"constexpr int ENG_SLOTS_{k} = {v};")
+    lines.append("")
+    lines.append("#ifndef ENG_TABLE_QUAL")
+    lines.append("#define ENG_TABLE_QUAL static const")
+    lines.append("#endif")
+    lines.append(f"ENG_TABLE_QUAL uint32_t ENG_OP_TAB[{len(op_tab)}][2] = {{")
+    lines.append("  " + ", ".join(f"{{{a}, {b}}}" for a, b in op_tab))
+    lines.append("};")
+    lines.append(f"ENG_TABLE_QUAL uint32_t ENG_SUB_TAB[{len(sub_tab)}][2] = {{")
+    lines.append("  " + ", ".join(f"{{{a}, {b}}}" for a, b in sub_tab))
+    lines.append("};")
+    lines.append(f"ENG_TABLE_QUAL uint32_t ENG_WORDS[{len(words)}] = {{")
+    for i in range(0, len(words), 12):
+        lines.append("  " + ", ".join(f"0x{w:08x}u" for w in words[i:i + 12]) + ",")
+    lines.append("};")
+    op_index = {op.name: i for i, op in enumerate(ops)}
+    lines.append(f"constexpr uint32_t ENG_OPC_RUN = {OPC['run']}, ENG_OPC_STEP = {OPC['step']}, ENG_OPC_LDLINE = {OPC['ldline']}, "
+                 f"ENG_OPC_LD12 = {OPC['ld12']}, ENG_OPC_ST12 = {OPC['st12']};")
+    for pname, prog in (("LINES", prog_lines()), ("MILLER", prog_miller()), ("FE", prog_fe())):
+        code = encode_prog(prog, op_index)
+        lines.append(f"constexpr int ENG_PROG_{pname}_LEN = {len(code)};")
+        lines.append(f"ENG_TABLE_QUAL uint32_t ENG_PROG_{pname}[{len(code)}] = {{")
+        for i in range(0, len(code), 12):
+            lines.append("  " + ", ".join(f"0x{w:08x}u" for w in code[i:i + 12]) + ",")
+        lines.append("};")
+    lines.append("")
+    lines.append("}  // namespace dgpu")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return ops, nsl
+
+
+# ---------------------------------------------------------------- executable model (mod p)
+class Model:
+    """Device semantics over Python ints mod p (slot values as plain field
+    elements; the device keeps them in Montgomery form, which commutes with
+    every operation here).  One instance models one group."""
+
+    def __init__(self, ops, p, const):
+        self.ops = {op.name: op for op in ops}
+        self.p = p
+        self.s = [0] * 64
+        self.const = const            # dict slot -> value
+        self.exports = {}
+
+    def get(self, s):
+        return self.s[s] if s < 64 else self.const[s]
+
+    def run(self, name):
+        p = self.p
+        for sub in self.ops[name].subs:
+            outs = []
+            for r in sub:
+                acc = 0
+                for a, b, sg, cf in r.terms:
+                    acc += cf * sg * self.get(a) * self.get(b)
+                v = r.cm * acc + sum(d * self.get(s) for s, d in r.post)
+                outs.append((r, v % p))
+            for r, v in outs:
+                if r.dst is not None:
+                    self.s[r.dst] = v
+                if r.exp is not None:
+                    self.exports[r.exp] = v
+
+
+if __name__ == "__main__":
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = os.path.join(root, "drand_amd", "csrc", "engine_tables.h")
+    ops, nsl = emit(out)
+    print("wrote", out, "ops:", len(ops), "slots:", nsl, file=sys.stderr)

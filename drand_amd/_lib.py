@@ -51,6 +51,8 @@ SYMBOLS = [
     ("dgpu_hash_to_g2", _c.c_int, [_P, _c.c_size_t, _P, _P]),
     ("dgpu_derive_pubkey", _c.c_int, [_P, _c.c_int, _P, _P, _c.c_size_t]),
     ("dgpu_make_chain", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _P, _P]),
+    ("dgpu_set_group", _c.c_int, [_P, _c.c_int, _c.c_int, _P]),
+    ("dgpu_recover_batch", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P]),
 ]
 
 

@@ -14,6 +14,7 @@
 #include "../../include/drand_gpu.h"
 #include "kernels.cuh"
 #include "pairing_engine.cuh"
+#include "recover.cuh"
 
 using namespace dgpu;
 
@@ -80,6 +81,9 @@ struct dgpu_ctx {
   // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
   DevBuf eng_consts, eng_lines, eng_f, eng_n1, eng_pre;
   bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
+  // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
+  int grp_t = 0, grp_n = 0;
+  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call
@@ -97,6 +101,30 @@ static void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
   hipEventRecord(c->ev[c->n_ev], s);
   if (c->n_ev < DGPU_MAX_STAGES) c->stage_name[c->n_ev] = name;
   c->n_ev++;
+}
+
+// Engine block constants (slot order of tools/gen_engine.py: ONE, the two
+// pairing points (-x, y) -- the group key (zero until dgpu_set_pubkey) and
+// -g1 --, gamma1_1..5, gamma2_1..5).
+static int upload_eng_consts(dgpu_ctx* c) {
+  eng_const_block cb;
+  const fp2 g1c[5] = {C_FROB1_1, C_FROB1_2, C_FROB1_3, C_FROB1_4, C_FROB1_5};
+  const fp2 g2c[5] = {C_FROB2_1, C_FROB2_2, C_FROB2_3, C_FROB2_4, C_FROB2_5};
+  auto put = [&](int slot, const fp& v) { memcpy(cb.w + (slot - 64) * ENG_SLOT_WORDS, v.l, FP_LIMBS * 4); };
+  put(ENG_C_ONE, fp_one());
+  put(ENG_C_NXP0, c->pk.neg_x);
+  put(ENG_C_YP0, c->pk.y);
+  put(ENG_C_NXP1, fp_neg(C_G1_X));
+  put(ENG_C_YP1, C_G1_NEG_Y);
+  for (int k = 0; k < 5; ++k) {
+    put(ENG_C_G1 + 2 * k, g1c[k].c0);
+    put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
+    put(ENG_C_G2 + k, g2c[k].c0);
+  }
+  int rc;
+  if ((rc = c->eng_consts.ensure(sizeof cb))) return rc;
+  HIP_TRY(hipMemcpy(c->eng_consts.p, &cb, sizeof cb, hipMemcpyHostToDevice));
+  return DGPU_OK;
 }
 
 extern "C" {
@@ -133,6 +161,11 @@ int dgpu_open(int device, dgpu_ctx** out) {
     delete c;
     return set_err(DGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
   }
+  if (upload_eng_consts(c) != DGPU_OK) {
+    std::string msg = g_last_error;
+    dgpu_close(c);
+    return set_err(DGPU_EDEVICE, "%s", msg.c_str());
+  }
   *out = c;
   return DGPU_OK;
 }
@@ -143,7 +176,8 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (int i = 0; i <= DGPU_MAX_STAGES; ++i)
     if (c->ev[i]) hipEventDestroy(c->ev[i]);
-  for (DevBuf* b : {&c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+  for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -172,24 +206,7 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
   if (drc != DEC_OK) return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
   memcpy(c->pk.neg_x.l, host, FP_LIMBS * 4);
   memcpy(c->pk.y.l, host + FP_LIMBS, FP_LIMBS * 4);
-  // engine block constants (slot order of tools/gen_engine.py: ONE, the two
-  // pairing points (-x, y), gamma1_1..5, gamma2_1..5)
-  eng_const_block cb;
-  const fp2 g1c[5] = {C_FROB1_1, C_FROB1_2, C_FROB1_3, C_FROB1_4, C_FROB1_5};
-  const fp2 g2c[5] = {C_FROB2_1, C_FROB2_2, C_FROB2_3, C_FROB2_4, C_FROB2_5};
-  auto put = [&](int slot, const fp& v) { memcpy(cb.w + (slot - 64) * ENG_SLOT_WORDS, v.l, FP_LIMBS * 4); };
-  put(ENG_C_ONE, fp_one());
-  put(ENG_C_NXP0, c->pk.neg_x);
-  put(ENG_C_YP0, c->pk.y);
-  put(ENG_C_NXP1, fp_neg(C_G1_X));
-  put(ENG_C_YP1, C_G1_NEG_Y);
-  for (int k = 0; k < 5; ++k) {
-    put(ENG_C_G1 + 2 * k, g1c[k].c0);
-    put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
-    put(ENG_C_G2 + k, g2c[k].c0);
-  }
-  if ((rc = c->eng_consts.ensure(sizeof cb))) return rc;
-  HIP_TRY(hipMemcpy(c->eng_consts.p, &cb, sizeof cb, hipMemcpyHostToDevice));
+  if ((rc = upload_eng_consts(c))) return rc;
   c->have_key = true;
   c->key_scheme = scheme;
   return DGPU_OK;
@@ -293,7 +310,9 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
 // (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
 // final exponentiation.  Decode verdicts in `st` stay final.
 static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
-                              hipStream_t s) {
+                              hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
+                              const uint32_t* pk_items = nullptr) {
+  if (!h_stride) h_stride = n;
   const size_t cap = std::min<size_t>(n, ENG_CHUNK);
   int rc;
   if ((rc = c->eng_lines.ensure(cap * (size_t)ENG_LINE_STEPS * 12 * FP_LIMBS * 4))) return rc;
@@ -306,7 +325,8 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
   for (size_t r0 = 0; r0 < n; r0 += cap) {
     const size_t cnt = std::min(cap, n - r0);
     const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
-    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, sg, consts, lines);
+    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg, pk_items,
+                       consts, lines);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
     HIP_TRY(hipGetLastError());
@@ -561,6 +581,100 @@ int dgpu_make_chain(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n_se
   if (e != hipSuccess) ret = set_err(DGPU_EDEVICE, "make_chain: %s", hipGetErrorString(e));
   d_first.release(); d_prev.release(); d_plen.release(); d_sigs.release();
   return ret;
+}
+
+int dgpu_set_group(dgpu_ctx* c, int t, int n, const uint8_t* commits48) {
+  if (!c || !commits48) return set_err(DGPU_EINVAL, "null argument");
+  if (t < 1 || t > RECOVER_MAX_T) return set_err(DGPU_EINVAL, "threshold t=%d outside [1, %d]", t, RECOVER_MAX_T);
+  if (n < t || n > 65536) return set_err(DGPU_EINVAL, "group size n=%d invalid for t=%d", n, t);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  if ((rc = c->misc.ensure(t * 48 + t * 4))) return rc;
+  if ((rc = c->grp_commits.ensure((size_t)t * 2 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->grp_table.ensure((size_t)n * 2 * FP_LIMBS * 4))) return rc;
+  uint8_t* d_in = (uint8_t*)c->misc.p;
+  int* d_rc = (int*)(d_in + t * 48);
+  HIP_TRY(hipMemcpyAsync(d_in, commits48, (size_t)t * 48, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_decode_commits, dim3(grid_for(t, 64)), dim3(64), 0, s, t, d_in, (uint32_t*)c->grp_commits.p, d_rc);
+  HIP_TRY(hipGetLastError());
+  std::vector<int> hrc(t);
+  HIP_TRY(hipMemcpyAsync(hrc.data(), d_rc, t * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (int j = 0; j < t; ++j)
+    if (hrc[j] != DEC_OK) return set_err(DGPU_EINVAL, "group commitment %d rejected (decode code %d)", j, hrc[j]);
+  hipLaunchKernelGGL(k_pubpoly_table, dim3(grid_for(n, 64)), dim3(64), 0, s, n, t, (const uint32_t*)c->grp_commits.p,
+                     (uint32_t*)c->grp_table.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(s));
+  c->grp_t = t;
+  c->grp_n = n;
+  return DGPU_OK;
+}
+
+int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size_t m, const uint8_t* partials,
+                       size_t partial_stride, const uint32_t* partial_len, uint8_t* out_sigs96, uint8_t* ok_bits,
+                       uint8_t* partial_valid) {
+  if (!c || !msgs32 || !partials || !partial_len || !out_sigs96 || !ok_bits) return set_err(DGPU_EINVAL, "null argument");
+  if (n_rounds == 0) return DGPU_OK;
+  if (m == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const size_t items = n_rounds * m;
+  for (size_t i = 0; i < items; ++i)
+    if (partial_len[i] > partial_stride) return set_err(DGPU_EINVAL, "partial_len[%zu] > stride", i);
+  int rc;
+  if ((rc = c->rec_msgs.ensure(n_rounds * 32))) return rc;
+  if ((rc = c->rec_parts.ensure(items * partial_stride))) return rc;
+  if ((rc = c->rec_plen.ensure(items * 4))) return rc;
+  if ((rc = c->rec_hidx.ensure(items * 4))) return rc;
+  if ((rc = c->rec_pk.ensure(items * 2 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->rec_idx.ensure(items * 4))) return rc;
+  if ((rc = c->rec_lam.ensure(n_rounds * RECOVER_MAX_T * 8 * 4))) return rc;
+  if ((rc = c->rec_out.ensure(n_rounds * 96))) return rc;
+  if ((rc = c->rec_ok.ensure(n_rounds))) return rc;
+  if ((rc = c->h_pts.ensure(n_rounds * G2A_WORDS * 4))) return rc;
+  if ((rc = c->sig_pts.ensure(items * G2A_WORDS * 4))) return rc;
+  if ((rc = c->status.ensure(items))) return rc;
+  std::vector<uint32_t> hidx(items);
+  for (size_t i = 0; i < items; ++i) hidx[i] = (uint32_t)(i / m);
+  HIP_TRY(hipMemcpyAsync(c->rec_msgs.p, msgs32, n_rounds * 32, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->rec_parts.p, partials, items * partial_stride, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->rec_plen.p, partial_len, items * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->rec_hidx.p, hidx.data(), items * 4, hipMemcpyHostToDevice, s));
+  uint32_t* h = (uint32_t*)c->h_pts.p;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  hipLaunchKernelGGL(k_hash_to_g2_msgs_pts, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds,
+                     (const uint8_t*)c->rec_msgs.p, h);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_decode_partials, dim3(grid_for(items, 256)), dim3(256), 0, s, items,
+                     (const uint8_t*)c->rec_parts.p, partial_stride, (const uint32_t*)c->rec_plen.p, c->grp_n, c->grp_t,
+                     (const uint32_t*)c->grp_table.p, (const uint32_t*)c->grp_commits.p, sg, (uint32_t*)c->rec_pk.p,
+                     (uint32_t*)c->rec_idx.p, st);
+  HIP_TRY(hipGetLastError());
+  // VerifyPartial of every partial: e(Eval(i), H(msg)) e(-g1, sig) == 1 on the engine
+  if ((rc = eng_pairing_locked(c, items, h, sg, st, s, n_rounds, (const uint32_t*)c->rec_hidx.p,
+                               (const uint32_t*)c->rec_pk.p)))
+    return rc;
+  hipLaunchKernelGGL(k_recover_rounds, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, m, c->grp_t,
+                     (const uint32_t*)c->rec_idx.p, (const uint8_t*)st, (const uint32_t*)sg, items,
+                     (uint32_t*)c->rec_lam.p, (uint8_t*)c->rec_out.p, (uint8_t*)c->rec_ok.p);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint8_t> okv(n_rounds), stv(partial_valid ? items : 0);
+  HIP_TRY(hipMemcpyAsync(out_sigs96, c->rec_out.p, n_rounds * 96, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(okv.data(), c->rec_ok.p, n_rounds, hipMemcpyDeviceToHost, s));
+  if (partial_valid) HIP_TRY(hipMemcpyAsync(stv.data(), st, items, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  memset(ok_bits, 0, (n_rounds + 7) / 8);
+  for (size_t r = 0; r < n_rounds; ++r)
+    if (okv[r]) ok_bits[r >> 3] |= (uint8_t)(1u << (r & 7));
+  if (partial_valid)
+    for (size_t i = 0; i < items; ++i) partial_valid[i] = stv[i] == ST_OK;
+  return DGPU_OK;
 }
 
 }  // extern "C"

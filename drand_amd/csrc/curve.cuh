@@ -74,6 +74,29 @@ DG_NOINL g2j g2_add(const g2j& p, const g2j& q) {
   return r;
 }
 
+// Mixed addition p + q with q affine (madd-2007-bl: 7M + 4S), exceptional
+// cases resolved (p == q -> dbl, p == -q -> infinity, p infinity -> q).
+DG_NOINL g2j g2_add_affine(const g2j& p, const g2a& q) {
+  fp2 z1z1 = fp2_sqr(p.z);
+  fp2 u2 = fp2_mul(q.x, z1z1);
+  fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
+  fp2 h = fp2_sub(u2, p.x);
+  fp2 rr = fp2_dbl(fp2_sub(s2, p.y));
+  bool p_inf = g2_is_inf(p);
+  bool h0 = fp2_is_zero(h), r0 = fp2_is_zero(rr);
+  fp2 hh = fp2_sqr(h);
+  fp2 i = fp2_dbl(fp2_dbl(hh));
+  fp2 j = fp2_mul(h, i);
+  fp2 v = fp2_mul(p.x, i);
+  g2j r;
+  r.x = fp2_sub(fp2_sub(fp2_sqr(rr), j), fp2_dbl(v));
+  r.y = fp2_sub(fp2_mul(rr, fp2_sub(v, r.x)), fp2_dbl(fp2_mul(p.y, j)));
+  r.z = fp2_sub(fp2_sqr(fp2_add(p.z, h)), fp2_add(z1z1, hh));
+  if (h0 && !p_inf) r = r0 ? g2_dbl(g2_from_affine(q)) : g2_infinity();
+  if (p_inf) r = g2_from_affine(q);
+  return r;
+}
+
 // [|x|] p for the BLS parameter |x| = 0xd201000000010000 (MSB-first double-and-add)
 DG_NOINL g2j g2_mul_absx(const g2j& p) {
   g2j r = p;

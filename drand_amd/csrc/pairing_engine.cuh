@@ -118,10 +118,15 @@ __device__ __forceinline__ bool eng_eq_canon(const fp& x, const fp& K) {
 }
 
 // ---------------------------------------------------------------- k_eng_lines
-// h_pts / sig_pts: affine G2 SoA [x.c0, x.c1, y.c0, y.c1][limb][n], rounds r0 + i.
+// Item i (chunk-local; global item r0 + i) checks e(P_i, H_i) e(-g1, S_i):
+//   H_i = h_pts[h_idx ? h_idx[r0 + i] : r0 + i], S_i = sig_pts[r0 + i]
+//   (affine G2 SoA [x.c0, x.c1, y.c0, y.c1][limb][stride]),
+//   P_i = pk_items ? pk_items[r0 + i] ((-x, y) SoA [2][limb][n]) : the block constant key.
 __global__ void __launch_bounds__(ENG_BLOCK) k_eng_lines(size_t n, size_t r0, size_t cnt,
-                                                         const uint32_t* __restrict__ h_pts,
+                                                         const uint32_t* __restrict__ h_pts, size_t h_stride,
+                                                         const uint32_t* __restrict__ h_idx,
                                                          const uint32_t* __restrict__ sig_pts,
+                                                         const uint32_t* __restrict__ pk_items,
                                                          const uint32_t* __restrict__ consts,
                                                          uint32_t* __restrict__ lines) {
   __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_LINES) * ENG_SLOT_WORDS];
@@ -132,12 +137,18 @@ __global__ void __launch_bounds__(ENG_BLOCK) k_eng_lines(size_t n, size_t r0, si
   const size_t r = r0 + L.i;
   if (L.k < 8) {  // Q coordinates: X, Y of T and the affine copy (xQ, yQ)
     const int p = L.k >> 2, comp = L.k & 3;
-    const fp q = ld_soa((p ? sig_pts : h_pts) + (size_t)comp * FP_LIMBS * n, n, r);
+    const fp q = p ? ld_soa(sig_pts + (size_t)comp * FP_LIMBS * n, n, r)
+                   : ld_soa(h_pts + (size_t)comp * FP_LIMBS * h_stride, h_stride, h_idx ? (size_t)h_idx[r] : r);
     eng_st(g + (p * ENG_LINE_PAIR_SLOTS + comp) * ENG_SLOT_WORDS, q);
     eng_st(g + (p * ENG_LINE_PAIR_SLOTS + 6 + comp) * ENG_SLOT_WORDS, q);
   } else {        // Z = 1
     const int p = (L.k - 8) >> 1, comp = (L.k - 8) & 1;
     eng_st(g + (p * ENG_LINE_PAIR_SLOTS + 4 + comp) * ENG_SLOT_WORDS, comp ? fp_zero() : fp_one());
+  }
+  if (L.k < 2) {  // pair 0's G1 point
+    const fp v = pk_items ? ld_soa(pk_items + (size_t)L.k * FP_LIMBS * n, n, r)
+                          : eng_ld(c + (ENG_C_NXP0 + L.k - 64) * ENG_SLOT_WORDS);
+    eng_st(g + (ENG_L_NXP0 + L.k) * ENG_SLOT_WORDS, v);
   }
   asm volatile("" ::: "memory");
   eng_exec(ENG_PROG_LINES, ENG_PROG_LINES_LEN, g, c, L, eng_io{lines, nullptr, nullptr, cnt});

@@ -1,0 +1,165 @@
+// Batch threshold recovery: kyber tbls.Recover + share.RecoverCommit (R), as
+// called by drand's aggregator chain/beacon/chain.go:158-168 (and the
+// partial check node.go:117-125 -> VerifyPartial).
+//
+// Per round: walk the partials in order, keep those whose index parses
+// (>= 2 bytes) and that verify against PubPoly.Eval(index) (decode +
+// subgroup + pairing: the pairing runs on the lane-cooperative engine over
+// all partial "items" of the batch), stop after t good ones; dedup by index
+// (xyCommit); fewer than t distinct -> failure; otherwise Lagrange at 0 over
+// Fr (x_i = index + 1) and the G2 multi-scalar multiplication
+// sum_j lambda_j sig_j (Straus: one shared doubling chain, mixed additions),
+// compressed to 96 bytes.
+#pragma once
+#include "fr.cuh"
+#include "kernels.cuh"
+
+namespace dgpu {
+
+constexpr int RECOVER_MAX_T = 32;
+
+// Group commitments C_j (48-byte compressed G1) -> affine SoA [x, y][limb][t]
+// (Montgomery); rc[j] = decode code.  kyber UnmarshalBinary semantics (R).
+__global__ void k_decode_commits(int t, const uint8_t* __restrict__ in48, uint32_t* __restrict__ pts,
+                                 int* __restrict__ rc) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= t) return;
+  uint8_t buf[48];
+  for (int k = 0; k < 48; ++k) buf[k] = in48[(size_t)j * 48 + k];
+  g1a p{fp_zero(), fp_zero()};
+  int r = g1_decompress(&p, buf, GROUP_ORDER_WORDS);
+  st_fp(pts, t, j, p.x);
+  st_fp(pts + FP_LIMBS * t, t, j, p.y);
+  rc[j] = r;
+}
+
+// PubPoly.Eval(i) = sum_j C_j (i+1)^j by Horner (kyber share/poly.go (R)),
+// returned as the pairing engine wants it: (-x, y), Montgomery.
+__device__ void pubpoly_eval(const uint32_t* commits, int t, uint32_t i, fp& neg_x, fp& y) {
+  const uint32_t x = i + 1;
+  g1j acc = g1_infinity();
+  for (int j = t - 1; j >= 0; --j) {
+    acc = g1_mul_words(acc, &x, 1);
+    const g1a cj{ld_fp(commits, t, j), ld_fp(commits + FP_LIMBS * t, t, j)};
+    acc = g1_add(acc, g1j{cj.x, cj.y, fp_one()});
+  }
+  const g1a a = g1_to_affine(acc);
+  neg_x = fp_neg(a.x);
+  y = a.y;
+}
+
+// Table of PubPoly.Eval(i) for i < n: SoA [(-x), y][limb][n]
+__global__ void k_pubpoly_table(int n, int t, const uint32_t* __restrict__ commits, uint32_t* __restrict__ table) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp nx, y;
+  pubpoly_eval(commits, t, (uint32_t)i, nx, y);
+  st_fp(table, n, i, nx);
+  st_fp(table + FP_LIMBS * n, n, i, y);
+}
+
+// Partials -> engine items.  Item i = partial i (round i / m, slot i % m):
+// index (BE16 of the first two bytes; 0xFFFFFFFF if fewer than 2), the
+// signature decoded (96 bytes after the index; other lengths are a decode
+// error), the share key PubPoly.Eval(index) (table for index < n, else
+// evaluated here), status ST_* (ST_OK -> still to be pairing-checked).
+__global__ void __launch_bounds__(256) k_decode_partials(size_t n_items, const uint8_t* __restrict__ partials,
+                                                          size_t stride, const uint32_t* __restrict__ plen, int n_group,
+                                                          int t, const uint32_t* __restrict__ table,
+                                                          const uint32_t* __restrict__ commits,
+                                                          uint32_t* __restrict__ sig_pts, uint32_t* __restrict__ pk_items,
+                                                          uint32_t* __restrict__ idx_out, uint8_t* __restrict__ status) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  const uint8_t* src = partials + i * stride;
+  const uint32_t len = plen[i];
+  uint32_t idx = 0xFFFFFFFFu;
+  uint8_t st = ST_DECODE;
+  g2a p{fp2_zero(), fp2_zero()};
+  if (len >= 2) {
+    idx = ((uint32_t)src[0] << 8) | src[1];
+    if (len == 98) {
+      uint8_t buf[96];
+      for (int k = 0; k < 96; ++k) buf[k] = src[2 + k];
+      const int rc = g2_decompress(&p, buf, true);
+      st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
+    }
+  }
+  fp nx = fp_zero(), y = fp_zero();
+  if (st == ST_OK) {
+    if (idx < (uint32_t)n_group) {
+      nx = ld_fp(table, n_group, idx);
+      y = ld_fp(table + FP_LIMBS * n_group, n_group, idx);
+    } else {
+      pubpoly_eval(commits, t, idx, nx, y);
+    }
+  }
+  st_g2a(sig_pts, n_items, i, p);
+  st_fp(pk_items, n_items, i, nx);
+  st_fp(pk_items + FP_LIMBS * n_items, n_items, i, y);
+  idx_out[i] = idx;
+  status[i] = st;
+}
+
+// Affine hash points H(msg) of raw 32-byte messages (SoA, stride n).
+__global__ void __launch_bounds__(256) k_hash_to_g2_msgs_pts(size_t n, const uint8_t* __restrict__ msgs,
+                                                              uint32_t* __restrict__ h_out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t msg[8];
+  for (int w = 0; w < 8; ++w) {
+    const uint8_t* b = msgs + i * 32 + 4 * w;
+    msg[w] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+  }
+  st_g2a(h_out, n, i, g2_to_affine(hash_to_g2(msg)));
+}
+
+// One thread per round: selection (first t good in input order, dedup by
+// index), Lagrange coefficients (scratch: [round][j][8 words]), Straus MSM,
+// compression.  ok[r] = 1 iff recovery succeeded (else out96 is zeroed).
+__global__ void __launch_bounds__(64) k_recover_rounds(size_t n_rounds, size_t m, int t,
+                                                       const uint32_t* __restrict__ idx,
+                                                       const uint8_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ sig_pts, size_t n_items,
+                                                       uint32_t* __restrict__ lam, uint8_t* __restrict__ out96,
+                                                       uint8_t* __restrict__ ok) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rounds) return;
+  uint32_t sel_idx[RECOVER_MAX_T], sel_item[RECOVER_MAX_T];
+  int good = 0, distinct = 0;
+  for (size_t j = 0; j < m && good < t; ++j) {
+    const size_t item = r * m + j;
+    if (status[item] != ST_OK) continue;
+    ++good;
+    const uint32_t id = idx[item];
+    bool dup = false;
+    for (int q = 0; q < distinct; ++q) dup = dup || sel_idx[q] == id;
+    if (!dup) {
+      sel_idx[distinct] = id;
+      sel_item[distinct] = (uint32_t)item;
+      ++distinct;
+    }
+  }
+  uint8_t* out = out96 + r * 96;
+  if (distinct < t) {
+    for (int k = 0; k < 96; ++k) out[k] = 0;
+    ok[r] = 0;
+    return;
+  }
+  uint32_t xs[RECOVER_MAX_T];
+  for (int j = 0; j < t; ++j) xs[j] = sel_idx[j] + 1;
+  uint32_t* L = lam + r * (size_t)RECOVER_MAX_T * 8;
+  for (int j = 0; j < t; ++j) fr_lagrange_at_zero(xs, t, j, L + j * 8);
+  g2j acc = g2_infinity();
+  for (int b = 254; b >= 0; --b) {
+    acc = g2_dbl(acc);
+    for (int j = 0; j < t; ++j) {
+      if ((L[j * 8 + (b >> 5)] >> (b & 31)) & 1u) acc = g2_add_affine(acc, ld_g2a(sig_pts, n_items, sel_item[j]));
+    }
+  }
+  const bool inf = g2_is_inf(acc);
+  g2_compress(out, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(acc), inf);
+  ok[r] = 1;
+}
+
+}  // namespace dgpu

@@ -135,6 +135,30 @@ int dgpu_hash_to_g2(dgpu_ctx *ctx, size_t n, const uint8_t *msg32, uint8_t *out9
  * client/test/result/mock/result.go:88). */
 int dgpu_derive_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, uint8_t *pk_out, size_t pk_len);
 
+/* Threshold group public polynomial share.PubPoly (kyber (R); key/keys.go
+ * DistPublic.Coefficients, chain/beacon/node.go:117-125 uses it through
+ * key.Scheme.VerifyPartial): t compressed G1 commitments C_0..C_{t-1}
+ * (48 bytes each), group size n (share indices 0..n-1 get a precomputed
+ * PubPoly.Eval table; larger indices are evaluated on the fly).
+ * 1 <= t <= 32, t <= n <= 65536.  Rejects undecodable commitments. */
+int dgpu_set_group(dgpu_ctx *ctx, int t, int n, const uint8_t *commits48);
+
+/* Batch form of key.Scheme.Recover (kyber tbls.Recover + share.RecoverCommit
+ * (R)) as the aggregator calls it (chain/beacon/chain.go:158-168), n_rounds
+ * rounds at once.  Round r signs msgs32 + 32 r (its DigestMessage) and offers
+ * m partial slots: partial j is partials + (r m + j) partial_stride, length
+ * partial_len[r m + j] (0 = empty slot); a partial is BE16(share index) ||
+ * 96-byte G2 signature (tbls.Sign).  Per round, exactly like the reference:
+ * partials are walked in order, those with a readable index that pass
+ * VerifyPartial (decode + subgroup + pairing against PubPoly.Eval(index))
+ * are kept until t are kept; duplicates of an index count once; fewer than t
+ * distinct -> the reference's error (bit 0 in ok_bits, zero signature);
+ * otherwise out_sigs96 + 96 r = the Lagrange-interpolated signature.
+ * partial_valid (optional, n_rounds*m bytes): 1 iff the partial verified. */
+int dgpu_recover_batch(dgpu_ctx *ctx, size_t n_rounds, const uint8_t *msgs32, size_t m, const uint8_t *partials,
+                       size_t partial_stride, const uint32_t *partial_len, uint8_t *out_sigs96, uint8_t *ok_bits,
+                       uint8_t *partial_valid);
+
 /* Synthetic chain generator (test/bench data tool; mirrors the reference's
  * fixture generator client/test/result/mock/result.go:86-130).  Builds
  * n_seg independent segments of seg_len rounds each, signed with the 32-byte

@@ -99,9 +99,74 @@ def group_keys():
     dump("group_toml_keys.json", {"source": "deploy/latest/group.toml", "keys": out})
 
 
+def recover_cases(name, seed, t, n):
+    """Threshold recovery (kyber tbls.Recover (R), restated in
+    oracle/drand_ref.recover) over a catalog of partial sets."""
+    import random
+    import struct
+    rng = random.Random(seed)
+    co = D.share_poly(seed, t)
+    commits = D.pub_poly_commits(co)
+    cpts = [B.g1_decompress(c) for c in commits]
+    sig_of = lambda i, m: D.partial_sign(i, D.poly_eval(co, i + 1), m)  # noqa: E731
+    cases = []
+
+    def add(kind, msg, partials):
+        valid = []
+        for s in partials:
+            if len(s) < 2:
+                valid.append(False)
+                continue
+            idx = struct.unpack(">H", s[:2])[0]
+            valid.append(B.verify_g2(D.pub_poly_eval(cpts, idx), msg, s[2:]))
+        known = {s: v for s, v in zip(partials, valid)}
+        rec = D.recover(cpts, msg, partials, t, n, verify=lambda i, s: known[struct.pack(">H", i) + s])
+        cases.append({"kind": kind, "msg": msg.hex(), "partials": [x.hex() for x in partials], "valid": valid,
+                      "recovered": rec.hex() if rec else None})
+        print(kind, sum(valid), "valid", "ok" if rec else "fail", flush=True)
+
+    def msg(k):
+        return hashlib.sha256(b"drand-mi355x/recover/" + bytes([seed, k])).digest()
+
+    m = msg(0)
+    idx = rng.sample(range(n), t)
+    add("exact_t", m, [sig_of(i, m) for i in idx])
+    m = msg(1)
+    idx = rng.sample(range(n), t + 3)
+    ps = [sig_of(i, m) for i in idx]
+    ps[1] = sig_of(idx[1], msg(9))                      # signature of another message
+    b = bytearray(ps[3]); b[10] ^= 0x04; ps[3] = bytes(b)  # bit flip in x
+    ps[4] = struct.pack(">H", idx[5]) + ps[4][2:]          # valid sig under the wrong index
+    add("three_bad_enough", m, ps)
+    m = msg(2)
+    idx = rng.sample(range(n), t)
+    ps = [sig_of(i, m) for i in idx]
+    ps[t // 2] = sig_of(idx[t // 2], msg(8))
+    add("one_bad_short", m, ps)
+    m = msg(3)
+    idx = rng.sample(range(n), t + 1)
+    ps = [sig_of(i, m) for i in idx]
+    ps.insert(1, ps[0])                                    # duplicate index among the first t good
+    add("duplicate_index", m, ps)
+    m = msg(4)
+    idx = rng.sample(range(n), t)
+    ps = [b"", b"\x00"] + [sig_of(i, m) for i in idx] + [sig_of(n + 7, m)]
+    add("short_partials_and_extra", m, ps)
+    m = msg(5)
+    idx = rng.sample(range(n), t - 1)
+    ps = [sig_of(i, m) for i in idx] + [sig_of(n + 3, m)]  # a share index beyond n (Eval(i) is defined for any i)
+    add("index_beyond_n", m, ps)
+    dump(name, {"source": "kyber tbls.Recover (R) via oracle/drand_ref.recover", "seed": seed, "t": t, "n": n,
+                "commits": [c.hex() for c in commits], "group_sig_of": "sk = a_0 = drand_ref.share_poly(seed)[0]",
+                "cases": cases})
+
+
 if __name__ == "__main__":
     kat()
     h2g2()
     chain("chain_chained_s1.json", D.SCHEME_CHAINED, 1, 24)
     chain("chain_unchained_s1.json", D.SCHEME_UNCHAINED, 1, 12)
     group_keys()
+    if "--recover" in sys.argv or not os.path.exists(os.path.join(HERE, "recover_t17_n32.json")):
+        recover_cases("recover_t3_n8.json", 3, 3, 8)
+        recover_cases("recover_t17_n32.json", 5, 17, 32)

@@ -232,9 +232,9 @@ void host_run_op(HostGroup& G, int op) {
   for (uint32_t sb = s0; sb < s0 + ns; ++sb) {
     const uint32_t off = ENG_SUB_TAB[sb][0], nt = ENG_SUB_TAB[sb][1];
     fp outs[ENG_LANES];
-    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_compute(G.s, G.c, ENG_WORDS + off + k * (4 + nt), nt);
+    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_compute(G.s, G.c, ENG_WORDS + off + k * eng_rec_words(nt), nt);
     for (int k = 0; k < ENG_LANES; ++k) {
-      const uint32_t* rec = ENG_WORDS + off + k * (4 + nt);
+      const uint32_t* rec = ENG_WORDS + off + k * eng_rec_words(nt);
       if (eng_dst(rec) != 0xFF) G.set(eng_dst(rec), outs[k]);
       const uint32_t e = eng_exp(rec);
       if (e != 0xFF) {
@@ -303,6 +303,8 @@ extern "C" int hs_eng_pairing(const uint8_t* pk48, const uint8_t* msg32, const u
     G.set(p * ENG_LINE_PAIR_SLOTS + 4, fp_one());
     G.set(p * ENG_LINE_PAIR_SLOTS + 5, fp_zero());
   }
+  G.set(ENG_L_NXP0, fp_neg(pk.x));
+  G.set(ENG_L_YP0, pk.y);
   G.step = 0;
   host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
   for (int k = 0; k < 12; ++k) G.set(ENG_M_F + k, k == 0 ? fp_one() : fp_zero());

@@ -378,8 +378,11 @@ def op_cyclo_sqr(name, R, TMP):
 
 
 # ---------------------------------------------------------------- k_lines: T steps for two pairs
-# per pair p (slot base 24 p): X 0,1  Y 2,3  Z 4,5  xQ 6,7  yQ 8,9  temporaries 10..23
+# per pair p (slot base 24 p): X 0,1  Y 2,3  Z 4,5  xQ 6,7  yQ 8,9  temporaries 10..23;
+# pair 0's G1 point (-x, y) per item at 48, 49 (the group key, or a share's key
+# PubPoly.Eval(i) in threshold recovery); pair 1's (-g1) is a block constant.
 LINE_PAIR_SLOTS = 24
+L_NXP0, L_YP0 = 48, 49
 
 
 def _pb(p, off):
@@ -398,7 +401,7 @@ def lines_dbl_op():
         X, Y, Z = fp2(_pb(p, 0)), fp2(_pb(p, 2)), fp2(_pb(p, 4))
         X2, XY, YZ = fp2(_pb(p, 10)), fp2(_pb(p, 12)), fp2(_pb(p, 14))
         W, U, V = fp2(_pb(p, 16)), fp2(_pb(p, 18)), fp2(_pb(p, 20))
-        nxp, yp = (C_NXP0, C_YP0) if p == 0 else (C_NXP1, C_YP1)
+        nxp, yp = (L_NXP0, L_YP0) if p == 0 else (C_NXP1, C_YP1)
         # S1: X2 = X^2, XY = X Y, YZ = Y Z
         fp2_out(S1, X2, *sqr_terms(X))
         fp2_out(S1, XY, *mul_terms(X, Y))
@@ -446,7 +449,7 @@ def lines_add_op():
         TH, LA, C, D = fp2(_pb(p, 10)), fp2(_pb(p, 12)), fp2(_pb(p, 14)), fp2(_pb(p, 16))
         E, F, G = fp2(_pb(p, 18)), fp2(_pb(p, 20)), fp2(_pb(p, 22))
         H, GH = C, D
-        nxp, yp = (C_NXP0, C_YP0) if p == 0 else (C_NXP1, C_YP1)
+        nxp, yp = (L_NXP0, L_YP0) if p == 0 else (C_NXP1, C_YP1)
         # S1: theta = Y - yQ Z, lam = X - xQ Z
         a, b = mul_terms(yQ, Z)
         S1.append(Rec(dst=TH[0], cm=-1, terms=a, post=[(Y[0], 1)]))
@@ -656,11 +659,12 @@ def encode(ops):
         for sub in op.subs:
             nt = max([len(r.terms) for r in sub] + [0])
             assert nt <= MAX_TERMS, (op.name, nt)
+            ntp = (nt + 3) & ~3   # records are 16-byte aligned: header + terms padded to 4 words
             sub_tab.append((len(words), nt))
             for k in range(LANES):
                 r = sub[k] if k < len(sub) else None
                 if r is None:
-                    words += [0xFFFF, 0, 0, 0] + [0] * nt
+                    words += [0xFFFF, 0, 0, 0] + [0] * ntp
                     continue
                 assert len(r.post) <= 3 and -16 < r.cm < 16
                 dst = 0xFF if r.dst is None else r.dst
@@ -675,6 +679,8 @@ def encode(ops):
                         words.append((a & 0xFF) | ((b & 0xFF) << 8) | ((sg < 0) << 16) | ((cf == 2) << 17) | (1 << 31))
                     else:
                         words.append(0)
+                words += [0] * (ntp - nt)
+    assert len(words) % 4 == 0
     return op_tab, sub_tab, words
 
 
@@ -723,7 +729,7 @@ def emit(path):
         f"constexpr int ENG_NCONST = {N_CONST};",
         f"constexpr int ENG_C_ONE = {C_ONE}, ENG_C_NXP0 = {C_NXP0}, ENG_C_YP0 = {C_YP0}, ENG_C_NXP1 = {C_NXP1}, ENG_C_YP1 = {C_YP1};",
         f"constexpr int ENG_C_G1 = {C_G1}, ENG_C_G2 = {C_G2};",
-        f"constexpr int ENG_LINE_PAIR_SLOTS = {LINE_PAIR_SLOTS};",
+        f"constexpr int ENG_LINE_PAIR_SLOTS = {LINE_PAIR_SLOTS}, ENG_L_NXP0 = {L_NXP0}, ENG_L_YP0 = {L_YP0};",
         f"constexpr int ENG_M_F = {M_F}, ENG_M_L1 = {M_L1}, ENG_M_L2 = {M_L2}, ENG_EXP_N1 = {EXP_N1};",
         f"constexpr int ENG_E_F = {E_F}, ENG_E_N1I = {E_N1I}, ENG_E_R = {E_R}, ENG_E_A = {E_A};",
         "",
@@ -749,7 +755,7 @@ def emit(path):
     lines.append(f"ENG_TABLE_QUAL uint32_t ENG_SUB_TAB[{len(sub_tab)}][2] = {{")
     lines.append("  " + ", ".join(f"{{{a}, {b}}}" for a, b in sub_tab))
     lines.append("};")
-    lines.append(f"ENG_TABLE_QUAL uint32_t ENG_WORDS[{len(words)}] = {{")
+    lines.append(f"alignas(16) ENG_TABLE_QUAL uint32_t ENG_WORDS[{len(words)}] = {{")
     for i in range(0, len(words), 12):
         lines.append("  " + ", ".join(f"0x{w:08x}u" for w in words[i:i + 12]) + ",")
     lines.append("};")

@@ -52,6 +52,8 @@ SYMBOLS = [
     ("dgpu_derive_pubkey", _c.c_int, [_P, _c.c_int, _P, _P, _c.c_size_t]),
     ("dgpu_make_chain", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _P, _P]),
     ("dgpu_set_group", _c.c_int, [_P, _c.c_int, _c.c_int, _P]),
+    ("dgpu_recover_batch_device", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P, _P]),
+    ("dgpu_make_partials", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _c.c_size_t, _P]),
     ("dgpu_recover_batch", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P]),
 ]
 

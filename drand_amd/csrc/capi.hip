@@ -77,29 +77,36 @@ struct dgpu_ctx {
   // scratch
   DevBuf h_pts, sig_pts, status;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
-  DevBuf rlc_tree, rlc_idx, rlc_fail;
+  DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st;
   // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
   DevBuf eng_consts, eng_lines, eng_f, eng_n1, eng_pre;
   bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
   int grp_t = 0, grp_n = 0;
-  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok;
+  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok, rec_pts, rec_vpk,
+      rec_st;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
-  // optional per-stage HIP-event timing of the last verify call
+  // optional per-stage HIP-event timing of the last verify call (event pool;
+  // durations are summed per stage name: chunked stages repeat)
   bool profile = false;
-  hipEvent_t ev[DGPU_MAX_STAGES + 1] = {};
-  const char* stage_name[DGPU_MAX_STAGES] = {};
+  std::vector<hipEvent_t> ev;
+  std::vector<const char*> stage_name;
   int n_ev = 0;
 };
 
 // Stage markers: mark(c, s, name) records an event that *starts* stage `name`
 // (and ends the previous one); mark(c, s, nullptr) closes the last stage.
 static void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
-  if (!c->profile || c->n_ev > DGPU_MAX_STAGES) return;
-  if (!c->ev[c->n_ev]) hipEventCreate(&c->ev[c->n_ev]);
+  if (!c->profile || c->n_ev >= 1024) return;
+  if ((size_t)c->n_ev == c->ev.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    c->ev.push_back(e);
+    c->stage_name.push_back(nullptr);
+  }
   hipEventRecord(c->ev[c->n_ev], s);
-  if (c->n_ev < DGPU_MAX_STAGES) c->stage_name[c->n_ev] = name;
+  c->stage_name[c->n_ev] = name;
   c->n_ev++;
 }
 
@@ -174,10 +181,9 @@ void dgpu_close(dgpu_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
-  for (int i = 0; i <= DGPU_MAX_STAGES; ++i)
-    if (c->ev[i]) hipEventDestroy(c->ev[i]);
+  for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
-                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -211,6 +217,10 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
   c->key_scheme = scheme;
   return DGPU_OK;
 }
+
+static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
+                              hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
+                              const uint32_t* pk_items = nullptr);
 
 // RLC batch verification with exact per-round verdicts (mode DGPU_MODE_RLC).
 // 1. R_i = pre-cofactor H(m_i) (Jacobian), sig_i decoded (+ subgroup), status.
@@ -282,8 +292,25 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
     d_idx = (uint32_t*)c->rlc_idx.p;
     d_fail = (uint8_t*)c->rlc_fail.p;
     HIP_TRY(hipMemcpyAsync(d_idx, cand.data(), m * 4, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_rlc_check, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], c->pk, d_fail);
-    HIP_TRY(hipGetLastError());
+    if (c->legacy_pairing) {
+      hipLaunchKernelGGL(k_rlc_check, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], c->pk, d_fail);
+      HIP_TRY(hipGetLastError());
+    } else {
+      // node checks on the pairing engine: e(pk, h_eff P) e(-g1, S) == 1
+      if ((rc = c->rlc_h.ensure(m * G2A_WORDS * 4)) || (rc = c->rlc_s.ensure(m * G2A_WORDS * 4)) ||
+          (rc = c->rlc_st.ensure(m)))
+        return rc;
+      uint32_t* ch = (uint32_t*)c->rlc_h.p;
+      uint32_t* cs = (uint32_t*)c->rlc_s.p;
+      uint8_t* cst = (uint8_t*)c->rlc_st.p;
+      mark(c, s, "rlc_prep");
+      hipLaunchKernelGGL(k_rlc_prep, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], ch, cs, cst);
+      HIP_TRY(hipGetLastError());
+      if ((rc = eng_pairing_locked(c, m, ch, cs, cst, s))) return rc;
+      mark(c, s, "rlc_bisection");
+      hipLaunchKernelGGL(k_rlc_fail, dim3(grid_for(m, B)), dim3(B), 0, s, m, cst, d_fail);
+      HIP_TRY(hipGetLastError());
+    }
     if (l == 0) {
       hipLaunchKernelGGL(k_rlc_mark, dim3(grid_for(m, B)), dim3(B), 0, s, m, d_idx, d_fail, st);
       HIP_TRY(hipGetLastError());
@@ -310,8 +337,7 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
 // (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
 // final exponentiation.  Decode verdicts in `st` stay final.
 static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
-                              hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
-                              const uint32_t* pk_items = nullptr) {
+                              hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items) {
   if (!h_stride) h_stride = n;
   const size_t cap = std::min<size_t>(n, ENG_CHUNK);
   int rc;
@@ -325,14 +351,18 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
   for (size_t r0 = 0; r0 < n; r0 += cap) {
     const size_t cnt = std::min(cap, n - r0);
     const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
+    mark(c, s, "eng_lines");
     hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg, pk_items,
                        consts, lines);
     HIP_TRY(hipGetLastError());
+    mark(c, s, "eng_miller");
     hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
     HIP_TRY(hipGetLastError());
     const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
+    mark(c, s, "eng_inv");
     hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, lines, st);
     HIP_TRY(hipGetLastError());
+    mark(c, s, "eng_fe");
     hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
     HIP_TRY(hipGetLastError());
   }
@@ -373,8 +403,8 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
     mark(c, s, "decode_g2");
     hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
     HIP_TRY(hipGetLastError());
-    mark(c, s, "pairing_check");
     if (c->legacy_pairing) {
+      mark(c, s, "pairing_check");
       hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
       HIP_TRY(hipGetLastError());
     } else if ((rc = eng_pairing_locked(c, n, h, sg, st, s))) {
@@ -455,12 +485,25 @@ int dgpu_stage_times(dgpu_ctx* c, float* ms_out, int max_stages, const char** na
   if (!c || !ms_out) return set_err(DGPU_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  int n = c->n_ev > 0 ? c->n_ev - 1 : 0;
-  if (n > max_stages) n = max_stages;
-  for (int i = 0; i < n; ++i) {
+  std::vector<const char*> names;
+  std::vector<float> sums;
+  for (int i = 0; i + 1 < c->n_ev; ++i) {
+    if (!c->stage_name[i]) continue;
     HIP_TRY(hipEventSynchronize(c->ev[i + 1]));
-    HIP_TRY(hipEventElapsedTime(&ms_out[i], c->ev[i], c->ev[i + 1]));
-    if (names_out) names_out[i] = c->stage_name[i] ? c->stage_name[i] : "?";
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+    size_t k = 0;
+    while (k < names.size() && strcmp(names[k], c->stage_name[i]) != 0) ++k;
+    if (k == names.size()) {
+      names.push_back(c->stage_name[i]);
+      sums.push_back(0.f);
+    }
+    sums[k] += ms;
+  }
+  int n = (int)std::min<size_t>(names.size(), (size_t)std::max(max_stages, 0));
+  for (int i = 0; i < n; ++i) {
+    ms_out[i] = sums[i];
+    if (names_out) names_out[i] = names[i];
   }
   return n;
 }
@@ -613,6 +656,79 @@ int dgpu_set_group(dgpu_ctx* c, int t, int n, const uint8_t* commits48) {
   return DGPU_OK;
 }
 
+}  // extern "C"
+
+// Recovery over device buffers (the body of both recover entry points).
+// d_ok: one byte per round (1 = recovered and VerifyRecovered passed);
+// d_status (optional): ST_* of every partial item.
+static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msgs, size_t m,
+                                 const uint8_t* d_parts, size_t stride, const uint32_t* d_plen, uint8_t* d_out,
+                                 uint8_t* d_ok, uint8_t* d_status, hipStream_t s) {
+  if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
+  const size_t items = n_rounds * m;
+  if (items > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "batch too large (%zu items)", items);
+  int rc;
+  if ((rc = c->rec_hidx.ensure(items * 4))) return rc;
+  if ((rc = c->rec_pk.ensure(items * 2 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->rec_idx.ensure(items * 4))) return rc;
+  if ((rc = c->rec_lam.ensure(n_rounds * RECOVER_MAX_T * 8 * 4))) return rc;
+  if ((rc = c->rec_pts.ensure(n_rounds * G2A_WORDS * 4))) return rc;
+  if ((rc = c->rec_vpk.ensure(n_rounds * 2 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->rec_st.ensure(n_rounds))) return rc;
+  if ((rc = c->h_pts.ensure(n_rounds * G2A_WORDS * 4))) return rc;
+  if ((rc = c->sig_pts.ensure(items * G2A_WORDS * 4))) return rc;
+  if ((rc = c->status.ensure(items))) return rc;
+  uint32_t* h = (uint32_t*)c->h_pts.p;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  uint32_t* hidx = (uint32_t*)c->rec_hidx.p;
+  c->n_ev = 0;
+  mark(c, s, "recover_hash");
+  hipLaunchKernelGGL(k_hash_to_g2_msgs_pts, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds, d_msgs, h);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_decode");
+  hipLaunchKernelGGL(k_round_of_item, dim3(grid_for(items, 256)), dim3(256), 0, s, items, m, hidx);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_decode_partials, dim3(grid_for(items, 256)), dim3(256), 0, s, items, d_parts, stride, d_plen,
+                     c->grp_n, c->grp_t, (const uint32_t*)c->grp_table.p, (const uint32_t*)c->grp_commits.p, sg,
+                     (uint32_t*)c->rec_pk.p, (uint32_t*)c->rec_idx.p, st);
+  HIP_TRY(hipGetLastError());
+  // VerifyPartial of every partial: e(Eval(i), H(msg)) e(-g1, sig) == 1 on the engine
+  if ((rc = eng_pairing_locked(c, items, h, sg, st, s, n_rounds, hidx, (const uint32_t*)c->rec_pk.p))) return rc;
+  uint32_t* rpts = (uint32_t*)c->rec_pts.p;
+  uint32_t* rpk = (uint32_t*)c->rec_vpk.p;
+  uint8_t* rst = (uint8_t*)c->rec_st.p;
+  mark(c, s, "recover_msm");
+  hipLaunchKernelGGL(k_recover_rounds, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, m, c->grp_t,
+                     (const uint32_t*)c->rec_idx.p, (const uint8_t*)st, (const uint32_t*)sg, items,
+                     (uint32_t*)c->rec_lam.p, d_out, d_ok, (const uint32_t*)c->grp_commits.p, rpts, rpk, rst);
+  HIP_TRY(hipGetLastError());
+  // VerifyRecovered: e(C_0, H(msg)) e(-g1, sig) == 1
+  if ((rc = eng_pairing_locked(c, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;
+  mark(c, s, "recover_verdict");
+  hipLaunchKernelGGL(k_recover_verdict, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds, rst, d_out, d_ok);
+  HIP_TRY(hipGetLastError());
+  if (d_status) HIP_TRY(hipMemcpyAsync(d_status, st, items, hipMemcpyDeviceToDevice, s));
+  mark(c, s);
+  return DGPU_OK;
+}
+
+extern "C" {
+
+int dgpu_recover_batch_device(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msgs32, size_t m,
+                              const uint8_t* d_partials, size_t partial_stride, const uint32_t* d_partial_len,
+                              uint8_t* d_out_sigs96, uint8_t* d_ok, uint8_t* d_status, void* stream) {
+  if (!c || !d_msgs32 || !d_partials || !d_partial_len || !d_out_sigs96 || !d_ok)
+    return set_err(DGPU_EINVAL, "null argument");
+  if (n_rounds == 0) return DGPU_OK;
+  if (m == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return recover_device_locked(c, n_rounds, d_msgs32, m, d_partials, partial_stride, d_partial_len, d_out_sigs96,
+                               d_ok, d_status, s);
+}
+
 int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size_t m, const uint8_t* partials,
                        size_t partial_stride, const uint32_t* partial_len, uint8_t* out_sigs96, uint8_t* ok_bits,
                        uint8_t* partial_valid) {
@@ -630,50 +746,69 @@ int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size
   if ((rc = c->rec_msgs.ensure(n_rounds * 32))) return rc;
   if ((rc = c->rec_parts.ensure(items * partial_stride))) return rc;
   if ((rc = c->rec_plen.ensure(items * 4))) return rc;
-  if ((rc = c->rec_hidx.ensure(items * 4))) return rc;
-  if ((rc = c->rec_pk.ensure(items * 2 * FP_LIMBS * 4))) return rc;
-  if ((rc = c->rec_idx.ensure(items * 4))) return rc;
-  if ((rc = c->rec_lam.ensure(n_rounds * RECOVER_MAX_T * 8 * 4))) return rc;
   if ((rc = c->rec_out.ensure(n_rounds * 96))) return rc;
   if ((rc = c->rec_ok.ensure(n_rounds))) return rc;
-  if ((rc = c->h_pts.ensure(n_rounds * G2A_WORDS * 4))) return rc;
-  if ((rc = c->sig_pts.ensure(items * G2A_WORDS * 4))) return rc;
-  if ((rc = c->status.ensure(items))) return rc;
-  std::vector<uint32_t> hidx(items);
-  for (size_t i = 0; i < items; ++i) hidx[i] = (uint32_t)(i / m);
+  if ((rc = c->out_reason.ensure(items))) return rc;
   HIP_TRY(hipMemcpyAsync(c->rec_msgs.p, msgs32, n_rounds * 32, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(c->rec_parts.p, partials, items * partial_stride, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(c->rec_plen.p, partial_len, items * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->rec_hidx.p, hidx.data(), items * 4, hipMemcpyHostToDevice, s));
-  uint32_t* h = (uint32_t*)c->h_pts.p;
-  uint32_t* sg = (uint32_t*)c->sig_pts.p;
-  uint8_t* st = (uint8_t*)c->status.p;
-  hipLaunchKernelGGL(k_hash_to_g2_msgs_pts, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds,
-                     (const uint8_t*)c->rec_msgs.p, h);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_decode_partials, dim3(grid_for(items, 256)), dim3(256), 0, s, items,
-                     (const uint8_t*)c->rec_parts.p, partial_stride, (const uint32_t*)c->rec_plen.p, c->grp_n, c->grp_t,
-                     (const uint32_t*)c->grp_table.p, (const uint32_t*)c->grp_commits.p, sg, (uint32_t*)c->rec_pk.p,
-                     (uint32_t*)c->rec_idx.p, st);
-  HIP_TRY(hipGetLastError());
-  // VerifyPartial of every partial: e(Eval(i), H(msg)) e(-g1, sig) == 1 on the engine
-  if ((rc = eng_pairing_locked(c, items, h, sg, st, s, n_rounds, (const uint32_t*)c->rec_hidx.p,
-                               (const uint32_t*)c->rec_pk.p)))
+  if ((rc = recover_device_locked(c, n_rounds, (const uint8_t*)c->rec_msgs.p, m, (const uint8_t*)c->rec_parts.p,
+                                  partial_stride, (const uint32_t*)c->rec_plen.p, (uint8_t*)c->rec_out.p,
+                                  (uint8_t*)c->rec_ok.p, (uint8_t*)c->out_reason.p, s)))
     return rc;
-  hipLaunchKernelGGL(k_recover_rounds, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, m, c->grp_t,
-                     (const uint32_t*)c->rec_idx.p, (const uint8_t*)st, (const uint32_t*)sg, items,
-                     (uint32_t*)c->rec_lam.p, (uint8_t*)c->rec_out.p, (uint8_t*)c->rec_ok.p);
-  HIP_TRY(hipGetLastError());
   std::vector<uint8_t> okv(n_rounds), stv(partial_valid ? items : 0);
   HIP_TRY(hipMemcpyAsync(out_sigs96, c->rec_out.p, n_rounds * 96, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(okv.data(), c->rec_ok.p, n_rounds, hipMemcpyDeviceToHost, s));
-  if (partial_valid) HIP_TRY(hipMemcpyAsync(stv.data(), st, items, hipMemcpyDeviceToHost, s));
+  if (partial_valid) HIP_TRY(hipMemcpyAsync(stv.data(), c->out_reason.p, items, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   memset(ok_bits, 0, (n_rounds + 7) / 8);
   for (size_t r = 0; r < n_rounds; ++r)
     if (okv[r]) ok_bits[r >> 3] |= (uint8_t)(1u << (r & 7));
   if (partial_valid)
     for (size_t i = 0; i < items; ++i) partial_valid[i] = stv[i] == ST_OK;
+  return DGPU_OK;
+}
+
+int dgpu_make_partials(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size_t m, const uint32_t* sign_idx,
+                       const uint32_t* label, const uint8_t* shares_be32, size_t n_shares, uint8_t* out98) {
+  if (!c || !msgs32 || !sign_idx || !label || !shares_be32 || !out98) return set_err(DGPU_EINVAL, "null argument");
+  if (n_rounds == 0 || m == 0) return DGPU_OK;
+  const size_t items = n_rounds * m;
+  for (size_t i = 0; i < items; ++i)
+    if (sign_idx[i] >= n_shares || label[i] > 0xFFFF) return set_err(DGPU_EINVAL, "bad share index at item %zu", i);
+  std::vector<scalar256> sh(n_shares);
+  for (size_t j = 0; j < n_shares; ++j) sh[j] = scalar_from_be32(shares_be32 + 32 * j);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  DevBuf d_msgs, d_h, d_si, d_lb, d_sh, d_out;
+  auto cleanup = [&]() { d_msgs.release(); d_h.release(); d_si.release(); d_lb.release(); d_sh.release(); d_out.release(); };
+  if ((rc = d_msgs.ensure(n_rounds * 32)) || (rc = d_h.ensure(n_rounds * G2A_WORDS * 4)) ||
+      (rc = d_si.ensure(items * 4)) || (rc = d_lb.ensure(items * 4)) || (rc = d_sh.ensure(n_shares * sizeof(scalar256))) ||
+      (rc = d_out.ensure(items * 98))) {
+    cleanup();
+    return rc;
+  }
+  hipError_t e = hipMemcpyAsync(d_msgs.p, msgs32, n_rounds * 32, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_si.p, sign_idx, items * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_lb.p, label, items * 4, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_sh.p, sh.data(), n_shares * sizeof(scalar256), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_hash_to_g2_msgs_pts, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds,
+                       (const uint8_t*)d_msgs.p, (uint32_t*)d_h.p);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_sign_partials, dim3(grid_for(items, 64)), dim3(64), 0, s, items, m, n_rounds,
+                       (const uint32_t*)d_h.p, (const uint32_t*)d_si.p, (const uint32_t*)d_lb.p,
+                       (const scalar256*)d_sh.p, (uint8_t*)d_out.p);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out98, d_out.p, items * 98, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  cleanup();
+  if (e != hipSuccess) return set_err(DGPU_EDEVICE, "make_partials: %s", hipGetErrorString(e));
   return DGPU_OK;
 }
 

@@ -293,6 +293,35 @@ __global__ void __launch_bounds__(256) k_rlc_check(size_t n_cand, const uint32_t
   fail[c] = ok ? 0 : 1;
 }
 
+// Candidate nodes for the pairing engine: h[c] = affine h_eff * P, sg[c] =
+// affine S, st[c] = ST_OK when both are finite (the engine then decides),
+// RLC_TRIVIAL when both are infinity (passes), ST_PAIRING when exactly one is
+// (e(Q, .) of a non-trivial prime-order point alone is never 1).
+constexpr uint8_t RLC_TRIVIAL = 0x80;
+__global__ void __launch_bounds__(64) k_rlc_prep(size_t n_cand, const uint32_t* __restrict__ idx, size_t n_level,
+                                                 const uint32_t* __restrict__ p_lvl,
+                                                 const uint32_t* __restrict__ s_lvl, uint32_t* __restrict__ h_out,
+                                                 uint32_t* __restrict__ s_out, uint8_t* __restrict__ st) {
+  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;
+  size_t j = idx[c];
+  g2j P = g2_clear_cofactor(ld_g2j(p_lvl, n_level, j));
+  g2j S = ld_g2j(s_lvl, n_level, j);
+  bool pi = g2_is_inf(P), si = g2_is_inf(S);
+  const g2a zero{fp2_zero(), fp2_zero()};
+  st_g2a(h_out, n_cand, c, pi ? zero : g2_to_affine(P));
+  st_g2a(s_out, n_cand, c, si ? zero : g2_to_affine(S));
+  st[c] = (pi && si) ? RLC_TRIVIAL : (pi || si) ? (uint8_t)ST_PAIRING : (uint8_t)ST_OK;
+}
+
+// Engine verdicts of the candidates -> fail flags.
+__global__ void __launch_bounds__(256) k_rlc_fail(size_t n_cand, const uint8_t* __restrict__ st,
+                                                  uint8_t* __restrict__ fail) {
+  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;
+  fail[c] = (st[c] == ST_OK || st[c] == RLC_TRIVIAL) ? 0 : 1;
+}
+
 // Mark the rounds of failing leaves.
 __global__ void k_rlc_mark(size_t n_cand, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ fail,
                            uint8_t* __restrict__ status) {

@@ -9,7 +9,8 @@
 // (xyCommit); fewer than t distinct -> failure; otherwise Lagrange at 0 over
 // Fr (x_i = index + 1) and the G2 multi-scalar multiplication
 // sum_j lambda_j sig_j (Straus: one shared doubling chain, mixed additions),
-// compressed to 96 bytes.
+// compressed to 96 bytes; then VerifyRecovered (chain.go:165) of every
+// recovered signature under C_0 on the engine.
 #pragma once
 #include "fr.cuh"
 #include "kernels.cuh"
@@ -60,8 +61,8 @@ __global__ void k_pubpoly_table(int n, int t, const uint32_t* __restrict__ commi
 
 // Partials -> engine items.  Item i = partial i (round i / m, slot i % m):
 // index (BE16 of the first two bytes; 0xFFFFFFFF if fewer than 2), the
-// signature decoded (96 bytes after the index; other lengths are a decode
-// error), the share key PubPoly.Eval(index) (table for index < n, else
+// signature decoded (96 bytes after the index; any other length, including
+// one above the stride, is a decode error; at most 98 bytes are read), the share key PubPoly.Eval(index) (table for index < n, else
 // evaluated here), status ST_* (ST_OK -> still to be pairing-checked).
 __global__ void __launch_bounds__(256) k_decode_partials(size_t n_items, const uint8_t* __restrict__ partials,
                                                           size_t stride, const uint32_t* __restrict__ plen, int n_group,
@@ -101,6 +102,12 @@ __global__ void __launch_bounds__(256) k_decode_partials(size_t n_items, const u
   status[i] = st;
 }
 
+// Round of every partial item (engine h_idx): item / m.
+__global__ void __launch_bounds__(256) k_round_of_item(size_t n_items, size_t m, uint32_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_items) out[i] = (uint32_t)(i / m);
+}
+
 // Affine hash points H(msg) of raw 32-byte messages (SoA, stride n).
 __global__ void __launch_bounds__(256) k_hash_to_g2_msgs_pts(size_t n, const uint8_t* __restrict__ msgs,
                                                               uint32_t* __restrict__ h_out) {
@@ -114,6 +121,27 @@ __global__ void __launch_bounds__(256) k_hash_to_g2_msgs_pts(size_t n, const uin
   st_g2a(h_out, n, i, g2_to_affine(hash_to_g2(msg)));
 }
 
+// Synthetic partials (test/bench data tool, tbls.Sign (R)): item i of round
+// i / m is BE16(label[i]) || compress(share[sign_idx[i]] * H(msg of round)).
+// A label different from the signing share makes an invalid partial.
+__global__ void __launch_bounds__(64) k_sign_partials(size_t n_items, size_t m, size_t n_rounds,
+                                                      const uint32_t* __restrict__ h_pts,
+                                                      const uint32_t* __restrict__ sign_idx,
+                                                      const uint32_t* __restrict__ label,
+                                                      const scalar256* __restrict__ shares,
+                                                      uint8_t* __restrict__ out98) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_items) return;
+  const g2a h = ld_g2a(h_pts, n_rounds, i / m);
+  const scalar256 k = shares[sign_idx[i]];
+  const g2j sg = g2_mul_words(g2_from_affine(h), k.w, 8);
+  const bool inf = g2_is_inf(sg);
+  uint8_t* o = out98 + i * 98;
+  o[0] = (uint8_t)(label[i] >> 8);
+  o[1] = (uint8_t)label[i];
+  g2_compress(o + 2, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(sg), inf);
+}
+
 // One thread per round: selection (first t good in input order, dedup by
 // index), Lagrange coefficients (scratch: [round][j][8 words]), Straus MSM,
 // compression.  ok[r] = 1 iff recovery succeeded (else out96 is zeroed).
@@ -122,9 +150,14 @@ __global__ void __launch_bounds__(64) k_recover_rounds(size_t n_rounds, size_t m
                                                        const uint8_t* __restrict__ status,
                                                        const uint32_t* __restrict__ sig_pts, size_t n_items,
                                                        uint32_t* __restrict__ lam, uint8_t* __restrict__ out96,
-                                                       uint8_t* __restrict__ ok) {
+                                                       uint8_t* __restrict__ ok, const uint32_t* __restrict__ commits,
+                                                       uint32_t* __restrict__ rec_pts, uint32_t* __restrict__ rec_pk,
+                                                       uint8_t* __restrict__ rec_st) {
   const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rounds) return;
+  // VerifyRecovered operands: key = PubPoly.Commit() = C_0, signature below
+  st_fp(rec_pk, n_rounds, r, fp_neg(ld_fp(commits, t, 0)));
+  st_fp(rec_pk + FP_LIMBS * n_rounds, n_rounds, r, ld_fp(commits + FP_LIMBS * t, t, 0));
   uint32_t sel_idx[RECOVER_MAX_T], sel_item[RECOVER_MAX_T];
   int good = 0, distinct = 0;
   for (size_t j = 0; j < m && good < t; ++j) {
@@ -144,6 +177,8 @@ __global__ void __launch_bounds__(64) k_recover_rounds(size_t n_rounds, size_t m
   if (distinct < t) {
     for (int k = 0; k < 96; ++k) out[k] = 0;
     ok[r] = 0;
+    st_g2a(rec_pts, n_rounds, r, g2a{fp2_zero(), fp2_zero()});
+    rec_st[r] = ST_DECODE;
     return;
   }
   uint32_t xs[RECOVER_MAX_T];
@@ -158,8 +193,21 @@ __global__ void __launch_bounds__(64) k_recover_rounds(size_t n_rounds, size_t m
     }
   }
   const bool inf = g2_is_inf(acc);
-  g2_compress(out, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(acc), inf);
+  const g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(acc);
+  g2_compress(out, a, inf);
+  st_g2a(rec_pts, n_rounds, r, a);
+  rec_st[r] = inf ? (uint8_t)ST_INFINITY : (uint8_t)ST_OK;
   ok[r] = 1;
+}
+
+// VerifyRecovered verdicts (chain/beacon/chain.go:165): a recovered signature
+// that does not verify under C_0 is dropped like a failed recovery.
+__global__ void __launch_bounds__(256) k_recover_verdict(size_t n_rounds, const uint8_t* __restrict__ rec_st,
+                                                         uint8_t* __restrict__ out96, uint8_t* __restrict__ ok) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rounds || !ok[r] || rec_st[r] == ST_OK) return;
+  ok[r] = 0;
+  for (int k = 0; k < 96; ++k) out96[r * 96 + k] = 0;
 }
 
 }  // namespace dgpu

@@ -152,3 +152,99 @@ def corrupt(chain, seed, rate=1e-3, kinds=ALL_CORRUPTIONS):
         elif kind == CORRUPT_TRUNCATED:
             chain.sig_len[i] = 48 if (i & 1) else 0
     return chosen
+
+
+# ---------------------------------------------------------------- threshold groups
+class Group:
+    """A t-of-n threshold group: polynomial coefficients a_0..a_{t-1} over Fr
+    (a_0 = derive_secret(seed), the group secret), the public commitments
+    C_j = a_j * g1 (48-byte compressed) and the shares s_i = f(i + 1)."""
+
+    def __init__(self, seed, t, n, coeffs, commits):
+        self.seed, self.t, self.n = seed, t, n
+        self.coeffs = coeffs
+        self.commits = commits
+        self.shares = [poly_eval(coeffs, i + 1) for i in range(n)]
+
+
+def share_coeffs(seed, t):
+    """a_0 = derive_secret(seed); a_j = OS2IP(SHA-256("drand-mi355x/poly/" ||
+    LE64(seed) || LE64(j))) mod r."""
+    out = [derive_secret(seed)]
+    for j in range(1, t):
+        d = hashlib.sha256(b"drand-mi355x/poly/" + struct.pack("<QQ", seed, j)).digest()
+        out.append(int.from_bytes(d, "big") % R_ORDER)
+    return out
+
+
+def poly_eval(coeffs, x):
+    acc = 0
+    for c in reversed(coeffs):
+        acc = (acc * x + c) % R_ORDER
+    return acc
+
+
+def make_group(seed, t, n, device=0):
+    """Commitments derived on the GPU (dgpu_derive_pubkey per coefficient)."""
+    ctx = get_context(device)
+    coeffs = share_coeffs(seed, t)
+    commits = []
+    for a in coeffs:
+        pk = np.zeros(48, dtype=np.uint8)
+        skb = np.frombuffer(a.to_bytes(32, "big"), dtype=np.uint8).copy()
+        _lib.check(ctx.lib.dgpu_derive_pubkey(ctx.handle, _lib.SCHEME_CHAINED, _lib.ptr(skb), _lib.ptr(pk), 48))
+        commits.append(bytes(pk))
+    return Group(seed, t, n, coeffs, commits)
+
+
+def sign_partials(group, msgs, sign_idx, labels=None, device=0):
+    """tbls.Sign of every (round, slot): msgs (n_rounds, 32) uint8, sign_idx
+    (n_rounds, m) share indices; labels (default = sign_idx) the BE16 index
+    written in front (a label that differs from the signer makes an invalid
+    partial).  Returns (n_rounds, m, 98) uint8.  Runs on the GPU
+    (dgpu_make_partials)."""
+    ctx = get_context(device)
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+    sign_idx = np.ascontiguousarray(sign_idx, dtype=np.uint32)
+    labels = sign_idx if labels is None else np.ascontiguousarray(labels, dtype=np.uint32)
+    nr, m = sign_idx.shape
+    shares = np.frombuffer(b"".join(s.to_bytes(32, "big") for s in group.shares), dtype=np.uint8).copy()
+    out = np.zeros((nr, m, 98), dtype=np.uint8)
+    _lib.check(ctx.lib.dgpu_make_partials(ctx.handle, nr, _lib.ptr(msgs), m, _lib.ptr(sign_idx), _lib.ptr(labels),
+                                          _lib.ptr(shares), len(group.shares), _lib.ptr(out)))
+    return out
+
+
+def group_signatures(group, msgs, device=0):
+    """sk * H(msg) for every message (the expected recovered signatures),
+    through dgpu_make_partials with the group secret as the only share."""
+    ctx = get_context(device)
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+    nr = msgs.shape[0]
+    zeros = np.zeros(nr, dtype=np.uint32)
+    sk = np.frombuffer(group.coeffs[0].to_bytes(32, "big"), dtype=np.uint8).copy()
+    out = np.zeros((nr, 98), dtype=np.uint8)
+    _lib.check(ctx.lib.dgpu_make_partials(ctx.handle, nr, _lib.ptr(msgs), 1, _lib.ptr(zeros), _lib.ptr(zeros),
+                                          _lib.ptr(sk), 1, _lib.ptr(out)))
+    return out[:, 2:].copy()
+
+
+def make_recovery_batch(group, n_rounds, seed, bad_rate=0.1, first_round=1, device=0):
+    """configs[4] workload: per round the DigestMessage of an unchained round
+    (SHA-256(BE64 round)) and t partials from distinct random signers; in a
+    `bad_rate` fraction of rounds one partial carries a wrong index (fails
+    VerifyPartial), so that round cannot be recovered (t - 1 good).
+    Returns (msgs (n, 32), partials (n, t, 98), expect_ok (n,) bool)."""
+    rng = np.random.default_rng(seed)
+    msgs = np.zeros((n_rounds, 32), dtype=np.uint8)
+    for r in range(n_rounds):
+        msgs[r] = np.frombuffer(hashlib.sha256(struct.pack(">Q", first_round + r)).digest(), dtype=np.uint8)
+    t, n = group.t, group.n
+    sign_idx = np.argsort(rng.random((n_rounds, n)), axis=1)[:, :t].astype(np.uint32)
+    labels = sign_idx.copy()
+    bad = rng.random(n_rounds) < bad_rate
+    rows = np.nonzero(bad)[0]
+    cols = rng.integers(0, t, size=len(rows))
+    labels[rows, cols] = (labels[rows, cols] + 1 + rng.integers(0, n - 1, size=len(rows))) % n
+    parts = sign_partials(group, msgs, sign_idx, labels, device=device)
+    return msgs, parts, ~bad

@@ -117,7 +117,9 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
  * stage durations (ms) and names of the last call (per-round mode:
  * hash_to_g2, decode_g2, pairing_check, pack_verdicts; RLC mode:
  * rlc_hash_to_g2_raw, decode_g2, rlc_leaves_tree, rlc_bisection,
- * pack_verdicts) and returns the number of stages written. */
+ * pack_verdicts; the pairing-engine kernels report as eng_lines,
+ * eng_miller, eng_inv and eng_fe, summed over chunks) and returns the
+ * number of stages written. */
 #define DGPU_MAX_STAGES 8
 int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
@@ -153,11 +155,31 @@ int dgpu_set_group(dgpu_ctx *ctx, int t, int n, const uint8_t *commits48);
  * VerifyPartial (decode + subgroup + pairing against PubPoly.Eval(index))
  * are kept until t are kept; duplicates of an index count once; fewer than t
  * distinct -> the reference's error (bit 0 in ok_bits, zero signature);
- * otherwise out_sigs96 + 96 r = the Lagrange-interpolated signature.
+ * otherwise out_sigs96 + 96 r = the Lagrange-interpolated signature, kept
+ * only if it passes VerifyRecovered under C_0 (chain.go:165), as the
+ * aggregator does before appending the beacon.
  * partial_valid (optional, n_rounds*m bytes): 1 iff the partial verified. */
 int dgpu_recover_batch(dgpu_ctx *ctx, size_t n_rounds, const uint8_t *msgs32, size_t m, const uint8_t *partials,
                        size_t partial_stride, const uint32_t *partial_len, uint8_t *out_sigs96, uint8_t *ok_bits,
                        uint8_t *partial_valid);
+
+/* dgpu_recover_batch over device buffers already resident in HBM, enqueued on
+ * `stream` (hipStream_t; NULL = the context's stream) without host
+ * synchronisation.  d_ok: n_rounds bytes (1 = recovered); d_status
+ * (optional): n_rounds*m bytes, DGPU_REASON_* of every partial (0 = verified).
+ * A partial_len above partial_stride reads as an invalid partial. */
+int dgpu_recover_batch_device(dgpu_ctx *ctx, size_t n_rounds, const uint8_t *d_msgs32, size_t m,
+                              const uint8_t *d_partials, size_t partial_stride, const uint32_t *d_partial_len,
+                              uint8_t *d_out_sigs96, uint8_t *d_ok, uint8_t *d_status, void *stream);
+
+/* Synthetic threshold partials (test/bench data tool; tbls.Sign (R),
+ * chain/beacon/node_test.go:56-106 builds the same shape): for item i of
+ * round i / m, out98 + 98 i = BE16(label[i]) || compress(share[sign_idx[i]] *
+ * H(msgs32 + 32 (i / m))), shares given as 32-byte big-endian scalars
+ * (n_shares of them).  A label different from the signing share's index
+ * yields an invalid partial. */
+int dgpu_make_partials(dgpu_ctx *ctx, size_t n_rounds, const uint8_t *msgs32, size_t m, const uint32_t *sign_idx,
+                       const uint32_t *label, const uint8_t *shares_be32, size_t n_shares, uint8_t *out98);
 
 /* Synthetic chain generator (test/bench data tool; mirrors the reference's
  * fixture generator client/test/result/mock/result.go:86-130).  Builds

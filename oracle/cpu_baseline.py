@@ -68,3 +68,62 @@ def _run_py(chain, seconds, cores, why):
     return {"value": sample / wall, "unit": "rounds/s", "cores": cores, "kind": "port",
             "impl": f"oracle/bls12381.py (pure Python; C build unavailable: {why})",
             "sample": f"{sample} uniformly sampled rounds of the bench chain", "wall_s": wall}
+
+
+# ---------------------------------------------------------------- configs[4]: threshold recovery
+_REC = {}
+
+
+def _rec_init(commits, t, n):
+    from oracle import bls12381 as B
+    from oracle import c_ref
+    from oracle import drand_ref as D
+    c_ref.load(build=False)
+    pts = [B.g1_decompress(c) for c in commits]
+    _REC.update(t=t, n=n, pts=pts, c0=commits[0],
+                evals=[B.g1_compress(D.pub_poly_eval(pts, i)) for i in range(n)])
+
+
+def _rec_round(args):
+    """Recover (kyber tbls.Recover restated in oracle/drand_ref.recover) with
+    VerifyPartial on the C restatement, then VerifyRecovered."""
+    from oracle import bls12381 as B
+    from oracle import c_ref
+    from oracle import drand_ref as D
+    msg, parts = args
+    L = c_ref.load(build=False)
+
+    def verify(i, sig):
+        pk = _REC["evals"][i] if i < _REC["n"] else B.g1_compress(D.pub_poly_eval(_REC["pts"], i))
+        return L.ref_verify_msg(pk, msg, sig, len(sig)) == 0
+
+    sig = D.recover(_REC["pts"], msg, parts, _REC["t"], _REC["n"], verify=verify)
+    if sig is not None and L.ref_verify_msg(_REC["c0"], msg, sig, len(sig)) != 0:
+        sig = None
+    return sig
+
+
+def run_recover(commits, t, n, msgs, parts, expect_sigs, seconds, cores):
+    """Bounded sample of the bench's recovery batch on `cores` processes:
+    C restatement pairings (t VerifyPartial + 1 VerifyRecovered per round),
+    Lagrange + G2 MSM in the Python oracle.  Checks against the expected
+    recovered signatures (None = failure)."""
+    from concurrent.futures import ProcessPoolExecutor
+    nr = len(msgs)
+    _rec_init(commits, t, n)
+    job = lambda i: (bytes(msgs[i]), [bytes(p) for p in parts[i]])  # noqa: E731
+    t0 = time.perf_counter()
+    _rec_round(job(0))
+    per = time.perf_counter() - t0
+    sample = int(max(cores, min(nr, seconds * cores / max(per, 1e-6))))
+    idx = sorted(np.random.default_rng(12345).choice(nr, size=sample, replace=False).tolist())
+    t0 = time.perf_counter()
+    with ProcessPoolExecutor(max_workers=cores, initializer=_rec_init, initargs=(commits, t, n)) as ex:
+        got = list(ex.map(_rec_round, [job(i) for i in idx], chunksize=max(1, sample // (4 * cores))))
+    wall = time.perf_counter() - t0
+    mism = sum(1 for i, g in zip(idx, got) if g != expect_sigs[i])
+    return {"value": sample / wall, "unit": "rounds/s", "cores": cores, "kind": "port",
+            "impl": "oracle/drand_ref.recover (Python: selection, Lagrange, G2 MSM) + oracle/c pairings "
+                    "(VerifyPartial, VerifyRecovered)",
+            "sample": f"{sample} uniformly sampled rounds of the bench batch", "wall_s": wall,
+            "single_core_ms_per_round": per * 1e3, "sample_mismatches": mism}

@@ -82,3 +82,75 @@ def test_gpu_recover_many_rounds_property():
         expect.append(B.sign_g2(co[0], m) if k >= t else None)
     sigs, _ = grp.recover_batch(msgs, parts)
     assert sigs == expect
+
+
+def test_synth_group_matches_oracle_poly():
+    """The bench's synthetic group (drand_amd.synth) uses the oracle's
+    coefficient derivation, so fixtures and bench batches share one group."""
+    from drand_amd import synth
+    assert synth.share_coeffs(5, 4) == D.share_poly(5, 4)
+    co = D.share_poly(5, 4)
+    assert [synth.poly_eval(co, x) for x in (1, 7, 33)] == [D.poly_eval(co, x) for x in (1, 7, 33)]
+
+
+@pytest.mark.gpu
+def test_gpu_synthetic_partials_match_oracle():
+    """dgpu_make_partials (bench data tool) == tbls.Sign restated in the oracle;
+    group_signatures == bls.Sign with the group secret; commitments derived on
+    the GPU == the oracle's."""
+    import hashlib
+    import numpy as np
+    from drand_amd import synth
+    grp = synth.make_group(9, 3, 5)
+    co = D.share_poly(9, 3)
+    assert grp.commits == D.pub_poly_commits(co)
+    msgs = np.stack([np.frombuffer(hashlib.sha256(bytes([k])).digest(), dtype=np.uint8) for k in range(2)])
+    idx = np.array([[0, 4, 2], [3, 1, 0]], dtype=np.uint32)
+    lab = idx.copy()
+    lab[1, 2] = 2
+    parts = synth.sign_partials(grp, msgs, idx, lab)
+    for r in range(2):
+        for j in range(3):
+            sig = B.sign_g2(D.poly_eval(co, int(idx[r, j]) + 1), bytes(msgs[r]))
+            assert bytes(parts[r, j]) == struct.pack(">H", int(lab[r, j])) + sig
+    gs = synth.group_signatures(grp, msgs)
+    assert [bytes(g) for g in gs] == [B.sign_g2(co[0], bytes(m)) for m in msgs]
+
+
+@pytest.mark.gpu
+def test_gpu_recover_device_entry_point_bench_batch():
+    """The bench's configs[4] workload at small size through
+    dgpu_recover_batch_device: recovered == group signature on rounds with t
+    good partials, failure (zeros) on rounds with one invalid partial."""
+    import ctypes
+    import numpy as np
+    import torch
+    from drand_amd import _lib, synth
+    from drand_amd.chain import get_context
+    grp = synth.make_group(4, 5, 8)
+    msgs, parts, expect_ok = synth.make_recovery_batch(grp, 96, seed=1, bad_rate=0.25)
+    assert 0 < int((~expect_ok).sum()) < 96
+    expect = synth.group_signatures(grp, msgs)
+    ctx = get_context(0)
+    cb = np.frombuffer(b"".join(grp.commits), dtype=np.uint8).copy()
+    _lib.check(ctx.lib.dgpu_set_group(ctx.handle, grp.t, grp.n, _lib.ptr(cb)))
+    from drand_amd.threshold import ThresholdGroup
+    ThresholdGroup._active = None  # group replaced behind ThresholdGroup's cache
+    n, m = parts.shape[:2]
+    dev = torch.device("cuda", 0)
+    d_msgs = torch.from_numpy(msgs).to(dev)
+    d_parts = torch.from_numpy(parts.reshape(n * m, 98).copy()).to(dev)
+    d_plen = torch.full((n * m,), 98, dtype=torch.int32, device=dev)
+    d_out = torch.zeros((n, 96), dtype=torch.uint8, device=dev)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_st = torch.full((n * m,), 0xFF, dtype=torch.uint8, device=dev)
+    _lib.check(ctx.lib.dgpu_recover_batch_device(ctx.handle, n, d_msgs.data_ptr(), m, d_parts.data_ptr(), 98,
+                                                 d_plen.data_ptr(), d_out.data_ptr(), d_ok.data_ptr(),
+                                                 d_st.data_ptr(), ctypes.c_void_p(0)))
+    torch.cuda.synchronize()
+    ok = d_ok.cpu().numpy().astype(bool)
+    out = d_out.cpu().numpy()
+    st = d_st.cpu().numpy().reshape(n, m)
+    assert (ok == expect_ok).all()
+    assert (out[ok] == expect[ok]).all() and not out[~ok].any()
+    assert ((st != 0).sum(axis=1) == (~expect_ok).astype(int)).all()

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Exact arithmetic work of the pairing engine's kernel programs, per item
+(one two-pair pairing check), from the generated tables (tools/gen_engine.py):
+
+  product terms  -- one 14 x 14-limb column product each (196 v_mad_u64_u32)
+  reductions     -- one Montgomery reduction per output with a product part (196)
+
+summed over the 12 lanes of a group (idle lanes and SIMT padding are not
+counted: this is the algorithm's work, not the schedule's).  Writes
+profiles/engine_work.json, which bench.py uses for roofline.achieved.
+
+    python tools/engine_work.py
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import gen_engine as G  # noqa: E402
+
+MADS_PER_PRODUCT = 14 * 14
+
+
+def program_work(ops, prog):
+    by = {op.name: op for op in ops}
+    terms = redc = outputs = sub_ops = simt_terms = 0
+    for ins in prog:
+        if ins[0] != "run":
+            continue
+        for sub in by[ins[1]].subs:
+            sub_ops += 1
+            nt = max([len(r.terms) for r in sub] + [0])
+            simt_terms += nt + (1 if nt else 0)
+            for r in sub:
+                terms += len(r.terms)
+                outputs += 1
+                redc += 1 if r.terms else 0
+    return {"product_terms": terms, "reductions": redc, "outputs": outputs, "sub_ops": sub_ops,
+            "mads": (terms + redc) * MADS_PER_PRODUCT,
+            "simt_lane_mads": 12 * simt_terms * MADS_PER_PRODUCT}
+
+
+def main():
+    ops = G.build_ops()
+    kern = {
+        "k_eng_lines": program_work(ops, G.prog_lines()),
+        "k_eng_miller": program_work(ops, G.prog_miller()),
+        "k_eng_fe": program_work(ops, G.prog_fe()),
+        # Montgomery's trick: 3 Fp multiplications per item (392 mads each), one
+        # exponentiation per 64 items (~475 multiplications) amortized
+        "k_eng_inv": {"mads": 3 * 392 + 475 * 392 // 64},
+    }
+    out = {
+        "unit": "per item (one two-pair pairing check); mads = 32x32->64 v_mad_u64_u32 products the algorithm performs",
+        "kernels": kern,
+        "pairing_total_mads": sum(k["mads"] for k in kern.values()),
+    }
+    path = os.path.join(os.path.dirname(HERE), "profiles", "engine_work.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,18 +1,28 @@
 #!/bin/bash
-# Round-record session: tests, default bench (+cpu baseline), rlc bench,
-# rocprofv3 kernel-trace stats of the default bench, FETCH/WRITE PMC passes.
+# Full GPU pass: parity suite, the three bench modes (per-round with the CPU
+# baseline, RLC, threshold recovery with its CPU baseline), rocprofv3 kernel
+# stats of the per-round and recovery benches.  Stops at the first failure.
 export TMPDIR=/tmp
 TAG=${TAG:-full}
-D=gpurun_out/$TAG
-mkdir -p $D
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > $D/pytest.log 2>&1
-rc=$?; tail -2 $D/pytest.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 900 python bench.py > $D/bench.json 2> $D/bench.err || exit $?
-cat $D/bench.json
-timeout -k 10 600 python bench.py --mode rlc --no-cpu-baseline > $D/bench_rlc.json 2> $D/bench_rlc.err || exit $?
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o bench -- python3 bench.py --no-cpu-baseline > $D/prof.log 2>&1 || exit $?
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv --pmc $c -d $D/pmc_$c -o p -- python3 tools/prof_verify.py --rounds 131072 --iters 1 > $D/pmc_$c.log 2>&1 || exit $?
-done
-python3 tools/traffic_summary.py $D 131072 $D/traffic.json
+O=gpurun_out/$TAG
+mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+step pytest
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log
+[ $rc -ne 0 ] && exit $rc
+step bench-per-round
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
+cat $O/bench.json
+step bench-rlc
+timeout -k 10 600 python bench.py --mode rlc --no-cpu-baseline > $O/bench_rlc.json 2> $O/bench_rlc.err || exit $?
+cat $O/bench_rlc.json
+step bench-recover
+timeout -k 10 600 python bench.py --mode recover > $O/bench_recover.json 2> $O/bench_recover.err || exit $?
+cat $O/bench_recover.json
+[ -n "$NO_PROF" ] && exit 0
+step prof-per-round
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 2 > $O/prof.out 2>&1 || exit $?
+step prof-recover
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof_recover -o bench -- python3 bench.py --mode recover --no-cpu-baseline --steps 2 > $O/prof_recover.out 2>&1 || exit $?
+find $O/prof $O/prof_recover -name "*kernel_stats*" -exec head -14 {} \;

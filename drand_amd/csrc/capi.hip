@@ -75,7 +75,7 @@ struct dgpu_ctx {
   int key_scheme = -1;
   g1_key pk{};
   // scratch
-  DevBuf h_pts, sig_pts, status;
+  DevBuf h_pts, sig_pts, status, h_z, h_pre;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
   DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st;
   // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
@@ -183,7 +183,7 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
-                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -340,9 +340,10 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
                               hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items) {
   if (!h_stride) h_stride = n;
   const size_t cap = std::min<size_t>(n, ENG_CHUNK);
+  const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
   int rc;
-  if ((rc = c->eng_lines.ensure(cap * (size_t)ENG_LINE_STEPS * 12 * FP_LIMBS * 4))) return rc;
-  if ((rc = c->eng_f.ensure(cap * 24 * FP_LIMBS * 4))) return rc;
+  if ((rc = c->eng_lines.ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
+  if ((rc = c->eng_f.ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
   if ((rc = c->eng_n1.ensure(cap * FP_LIMBS * 4))) return rc;
   const uint32_t* consts = (const uint32_t*)c->eng_consts.p;
   uint32_t* lines = (uint32_t*)c->eng_lines.p;
@@ -397,8 +398,13 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
     if (rc) return rc;
   } else {
     mark(c, s, "hash_to_g2");
+    if ((rc = c->h_z.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
     hipLaunchKernelGGL(k_hash_to_g2_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
-                       d_prev_len, chained ? 1 : 0, h);
+                       d_prev_len, chained ? 1 : 0, h, (uint32_t*)c->h_z.p);
+    HIP_TRY(hipGetLastError());
+    mark(c, s, "h_affine");
+    hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
+                       (const uint32_t*)c->h_z.p, (uint32_t*)c->h_pre.p);
     HIP_TRY(hipGetLastError());
     mark(c, s, "decode_g2");
     hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);

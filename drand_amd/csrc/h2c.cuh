@@ -211,47 +211,52 @@ DG_FN void hash_to_field_g2(fp2& u0, fp2& u1, const uint32_t msg[8]) {
 }
 
 // ================================================================ SSWU + 3-isogeny
-// Simplified SWU on E2': y^2 = x^3 + A'x + B' (RFC 9380 section 6.6.2).
-DG_NOINL g2a map_to_curve_sswu_g2(const fp2& u) {
-  fp2 u2 = fp2_sqr(u);
-  fp2 zu2 = fp2_mul(C_SSWU_Z, u2);
-  fp2 den = fp2_add(fp2_sqr(zu2), zu2);
-  bool den0 = fp2_is_zero(den);
-  fp2 tv1 = fp2_inv(den);
-  fp2 x1 = fp2_mul(C_SSWU_MINUS_B_OVER_A, fp2_add(fp2_one(), tv1));
-  x1 = fp2_cmov(x1, C_SSWU_B_OVER_ZA, den0);
-  fp2 gx1 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x1), C_SSWU_A), x1), C_SSWU_B);
-  fp2 x2 = fp2_mul(zu2, x1);
-  fp2 gx2 = fp2_add(fp2_mul(fp2_add(fp2_sqr(x2), C_SSWU_A), x2), C_SSWU_B);
-  bool e1 = fp2_is_square(gx1);
-  fp2 x = fp2_cmov(x2, x1, e1);
-  fp2 gx = fp2_cmov(gx2, gx1, e1);
-  fp2 y;
-  fp2_sqrt(y, gx);  // gx is a square by construction
+// Simplified SWU on E2': y^2 = x^3 + A'x + B' (RFC 9380 section 6.6.2) fused
+// with the 3-isogeny to E2, inversion-free: x1 = N/D, gx1 = U/D^3 and
+// gx2 = (Z u^2)^3 gx1, so one norm-method square root of w = U D (or of
+// (Z u^2)^3 U D) -- two Fp exponentiations in all, the square test of gx1
+// included -- gives y = sqrt(w)/D^2 = fp2_sqrt_scaled(w, g, norm(D))
+// conj(D)^2.  The isogeny is evaluated on x = N/D homogeneously.  Model and
+// derivation: tools/sswu_model.py (tests/test_sswu_model.py).
+DG_NOINL g2j map_to_curve_sswu_iso3(const fp2& u) {
+  const fp2 zu2 = fp2_mul(C_SSWU_Z, fp2_sqr(u));
+  const fp2 den = fp2_add(fp2_sqr(zu2), zu2);
+  const bool den0 = fp2_is_zero(den);
+  fp2 N = fp2_cmov(fp2_mul(C_SSWU_MINUS_B_OVER_A, fp2_add(den, fp2_one())), C_SSWU_B_OVER_ZA, den0);
+  const fp2 D = fp2_cmov(den, fp2_one(), den0);
+  const fp2 D2 = fp2_sqr(D);
+  const fp2 D3 = fp2_mul(D2, D);
+  fp2 w = fp2_mul(fp2_add(fp2_mul(N, fp2_add(fp2_sqr(N), fp2_mul(C_SSWU_A, D2))), fp2_mul(C_SSWU_B, D3)), D);
+  const fp alpha = fp2_norm(w);
+  fp g = fp_sqrt_cand(alpha);
+  if (!fp_eq(fp_sqr(g), alpha)) {  // gx1 not square: x2 = Z u^2 x1, gx2 = (Z u^2)^3 gx1
+    const fp nu = fp2_norm(u);
+    g = fp_mul(fp_mul(C_SQRT_M125, fp_mul(fp_sqr(nu), nu)), g);
+    w = fp2_mul(fp2_mul(fp2_sqr(zu2), zu2), w);
+    N = fp2_mul(zu2, N);
+  }
+  fp2 y = fp2_mul(fp2_sqrt_scaled(w, g, fp2_norm(D)), fp2_sqr(fp2_conj(D)));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
-  return g2a{x, y};
-}
-
-// 3-isogeny E2' -> E2 evaluated projectively (no inversion): with
-// x = xn/xd and y = y' yn/yd, choose Z = xd*yd so that
-// X = xn xd yd^2, Y = y' yn xd^3 yd^2.
-DG_NOINL g2j iso3_map(const g2a& p) {
-  const fp2& x = p.x;
-  fp2 x2 = fp2_sqr(x);
-  fp2 x3 = fp2_mul(x2, x);
-  fp2 xn = fp2_add(fp2_add(fp2_mul(C_ISO3_XNUM_3, x3), fp2_mul(C_ISO3_XNUM_2, x2)),
-                   fp2_add(fp2_mul(C_ISO3_XNUM_1, x), C_ISO3_XNUM_0));
-  fp2 xd = fp2_add(fp2_add(x2, fp2_mul(C_ISO3_XDEN_1, x)), C_ISO3_XDEN_0);
-  fp2 yn = fp2_add(fp2_add(fp2_mul(C_ISO3_YNUM_3, x3), fp2_mul(C_ISO3_YNUM_2, x2)),
-                   fp2_add(fp2_mul(C_ISO3_YNUM_1, x), C_ISO3_YNUM_0));
-  fp2 yd = fp2_add(fp2_add(x3, fp2_mul(C_ISO3_YDEN_2, x2)), fp2_add(fp2_mul(C_ISO3_YDEN_1, x), C_ISO3_YDEN_0));
-  fp2 yd2 = fp2_sqr(yd);
-  fp2 xdyd2 = fp2_mul(xd, yd2);
+  // 3-isogeny on x = N/D, numerators homogenized to degree 3 (x denominator 2)
+  const fp2 N2 = fp2_sqr(N);
+  const fp2 N3 = fp2_mul(N2, N);
+  const fp2 N2D = fp2_mul(N2, D);
+  const fp2 ND2 = fp2_mul(N, D2);
+  const fp2 xn = fp2_add(fp2_add(fp2_mul(C_ISO3_XNUM_3, N3), fp2_mul(C_ISO3_XNUM_2, N2D)),
+                         fp2_add(fp2_mul(C_ISO3_XNUM_1, ND2), fp2_mul(C_ISO3_XNUM_0, D3)));
+  const fp2 xd = fp2_add(fp2_add(N2, fp2_mul(C_ISO3_XDEN_1, fp2_mul(N, D))), fp2_mul(C_ISO3_XDEN_0, D2));
+  const fp2 yn = fp2_add(fp2_add(fp2_mul(C_ISO3_YNUM_3, N3), fp2_mul(C_ISO3_YNUM_2, N2D)),
+                         fp2_add(fp2_mul(C_ISO3_YNUM_1, ND2), fp2_mul(C_ISO3_YNUM_0, D3)));
+  const fp2 yd = fp2_add(fp2_add(N3, fp2_mul(C_ISO3_YDEN_2, N2D)),
+                         fp2_add(fp2_mul(C_ISO3_YDEN_1, ND2), fp2_mul(C_ISO3_YDEN_0, D3)));
+  // x_E2 = xn / (xd D), y_E2 = y yn / yd; Jacobian with Z = xd D yd
+  const fp2 xdd = fp2_mul(xd, D);
+  const fp2 t = fp2_mul(xdd, fp2_sqr(yd));
   g2j r;
-  r.z = fp2_mul(xd, yd);
-  r.x = fp2_mul(xn, xdyd2);
-  r.y = fp2_mul(fp2_mul(p.y, yn), fp2_mul(fp2_sqr(xd), xdyd2));
-  // an exceptional input (xd or yd = 0) maps to the identity (RFC 9380 section 6.6.3)
+  r.z = fp2_mul(xdd, yd);
+  r.x = fp2_mul(xn, t);
+  r.y = fp2_mul(fp2_mul(y, yn), fp2_mul(fp2_sqr(xdd), t));
+  // an exceptional input (xd or yd = 0) gives Z = 0: the identity (RFC 9380 section 6.6.3)
   return r;
 }
 
@@ -259,8 +264,8 @@ DG_NOINL g2j iso3_map(const g2a& p) {
 DG_NOINL g2j hash_to_g2(const uint32_t msg[8]) {
   fp2 u0, u1;
   hash_to_field_g2(u0, u1, msg);
-  g2j q0 = iso3_map(map_to_curve_sswu_g2(u0));
-  g2j q1 = iso3_map(map_to_curve_sswu_g2(u1));
+  g2j q0 = map_to_curve_sswu_iso3(u0);
+  g2j q1 = map_to_curve_sswu_iso3(u1);
   return g2_clear_cofactor(g2_add(q0, q1));
 }
 

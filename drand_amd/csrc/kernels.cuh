@@ -50,19 +50,58 @@ struct g1_key {  // public key prepared for line evaluation: (-x, y), Montgomery
 };
 
 // ---------------------------------------------------------------- kernels
-// H(m) for m = DigestMessage(round, prev) (chain/verify.go:24-32).
-// chained != 0: prev bytes are hashed (any length up to prev_stride).
+// H(m) for m = DigestMessage(round, prev) (chain/verify.go:24-32), Jacobian:
+// X, Y into h_out (the affine slots, finished in place by k_g2_batch_affine),
+// Z into z_out.  chained != 0: prev bytes are hashed (any length up to prev_stride).
 __global__ void __launch_bounds__(256) k_hash_to_g2_beacons(size_t n, const uint64_t* __restrict__ rounds,
                                                              const uint8_t* __restrict__ prev, size_t prev_stride,
                                                              const uint32_t* __restrict__ prev_len, int chained,
-                                                             uint32_t* __restrict__ h_out) {
+                                                             uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t msg[8];
   uint32_t plen = chained ? prev_len[i] : 0u;
   drand_digest(msg, chained ? prev + i * prev_stride : nullptr, plen, rounds[i]);
   g2j h = hash_to_g2(msg);
-  st_g2a(h_out, n, i, g2_to_affine(h));
+  st_g2a(h_out, n, i, g2a{h.x, h.y});
+  st_fp(z_out, n, i, h.z.c0);
+  st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
+}
+
+// Jacobian -> affine for n G2 points in place (X, Y in pts; Z in z) with one
+// Fp inversion per thread: thread t takes points t, t + T, ... (T threads in
+// the grid) and inverts the norms N(Z_i) by Montgomery's trick (prefix
+// products in `pre`); 1/Z = conj(Z) / N(Z).  Z = 0 (the identity) gives (0, 0)
+// like g2_to_affine.
+__global__ void __launch_bounds__(256) k_g2_batch_affine(size_t n, uint32_t* __restrict__ pts,
+                                                         const uint32_t* __restrict__ z, uint32_t* __restrict__ pre) {
+  const size_t T = (size_t)gridDim.x * blockDim.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  auto ldz = [&](size_t i) { return fp2{ld_fp(z, n, i), ld_fp(z + FP_WORDS * n, n, i)}; };
+  fp acc = fp_one();
+  size_t last = t;
+  for (size_t i = t; i < n; i += T) {
+    const fp nz = fp2_norm(ldz(i));
+    acc = fp_mul(acc, fp_cmov(nz, fp_one(), fp_is_zero(nz)));
+    st_fp(pre, n, i, acc);
+    last = i;
+  }
+  fp inv = fp_inv(acc);
+  for (size_t i = last;; i -= T) {
+    const fp2 zi = ldz(i);
+    const fp nz = fp2_norm(zi);
+    const bool inf = fp_is_zero(nz);
+    const fp ninv = i >= t + T ? fp_mul(inv, ld_fp(pre, n, i - T)) : inv;  // 1 / N(Z_i)
+    const fp2 zinv = fp2_mul_fp(fp2_conj(zi), ninv);
+    const fp2 zinv2 = fp2_sqr(zinv);
+    g2a a = ld_g2a(pts, n, i);
+    a.x = fp2_mul(a.x, zinv2);
+    a.y = fp2_mul(a.y, fp2_mul(zinv2, zinv));
+    st_g2a(pts, n, i, inf ? g2a{fp2_zero(), fp2_zero()} : a);
+    if (i < t + T) break;
+    if (!inf) inv = fp_mul(inv, nz);
+  }
 }
 
 // H(m) for raw 32-byte messages (parity/debug: dgpu_hash_to_g2)
@@ -228,7 +267,7 @@ __global__ void __launch_bounds__(256) k_hash_to_g2_raw(size_t n, const uint64_t
   drand_digest(msg, chained ? prev + i * prev_stride : nullptr, chained ? prev_len[i] : 0u, rounds[i]);
   fp2 u0, u1;
   hash_to_field_g2(u0, u1, msg);
-  g2j q = g2_add(iso3_map(map_to_curve_sswu_g2(u0)), iso3_map(map_to_curve_sswu_g2(u1)));
+  g2j q = g2_add(map_to_curve_sswu_iso3(u0), map_to_curve_sswu_iso3(u1));
   st_g2j(r_out, n, i, q);
 }
 

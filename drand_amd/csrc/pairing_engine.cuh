@@ -12,9 +12,9 @@
 // kilic Engine AddPair/AddPairInv/Check (R).  The conjugation of the Miller
 // value (x < 0) is skipped: FE(conj f) = FE(f)^-1, equal to 1 iff FE(f) is.
 //
-// HBM layouts (chunk-local round index i, chunk capacity cap):
-//   lines  [step 0..67][export 0..11][limb][i]     (export 6p + e: pair p, l0.re .. l3.im)
-//   fbuf   [component 0..23][limb][i]              (f, later t and t2 of the FE)
+// HBM layouts (chunk-local round index i = 5 b + g, block b, chunk capacity cap):
+//   lines  [b][step 0..67][limb][g][export 0..11]  (export 6p + e: pair p, l0.re .. l3.im)
+//   fbuf   [b][plane 0..1][limb][g][component 0..11] (f, later t and t2 of the FE)
 //   n1     [limb][i]
 #pragma once
 #include "engine.cuh"
@@ -64,10 +64,29 @@ __device__ __forceinline__ fp ld_soa(const uint32_t* base, size_t stride, size_t
   return a;
 }
 
-// HBM side of a kernel program (chunk-local SoA buffers, stride cnt).
+// Wave-blocked layout of the line and f buffers: block b (rounds 5b..5b+4)
+// owns planes [b][plane][limb][60] with word g*12 + e (group g, export e), so
+// every limb access of a wave is one contiguous 240-byte segment (a
+// round-fastest SoA would scatter the 60 lanes over 12 planes, 20 bytes each).
+constexpr int ENG_WAVE_WORDS = ENG_GROUPS_PER_WAVE * 12;
+__device__ __forceinline__ size_t eng_blk_off(int planes, int plane, int g, int e) {
+  return ((size_t)blockIdx.x * planes + plane) * FP_LIMBS * ENG_WAVE_WORDS + g * 12 + e;
+}
+__device__ __forceinline__ void st_blk(uint32_t* base, size_t off, const fp& a) {
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) base[off + l * ENG_WAVE_WORDS] = a.l[l];
+}
+__device__ __forceinline__ fp ld_blk(const uint32_t* base, size_t off) {
+  fp a;
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) a.l[l] = base[off + l * ENG_WAVE_WORDS];
+  return a;
+}
+
+// HBM side of a kernel program (chunk-local buffers).
 struct eng_io {
-  uint32_t* lines;   // [step][12][limb][cnt]
-  uint32_t* fbuf;    // [24][limb][cnt]
+  uint32_t* lines;   // blocked, ENG_LINE_STEPS planes of 12 exports per round
+  uint32_t* fbuf;    // blocked, 2 planes of 12 components (f / t, then t2)
   uint32_t* n1;      // [limb][cnt]
   size_t cnt;
 };
@@ -78,7 +97,7 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
   int step = 0;
   auto sink = [&](uint32_t e, const fp& v) {
     if (!L.valid) return;
-    if (e < 12) st_soa(io.lines + ((size_t)(step * 12 + e) * FP_LIMBS) * io.cnt, io.cnt, L.i, v);
+    if (e < 12) st_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, (int)e), v);
     else st_soa(io.n1, io.cnt, L.i, v);
   };
 #pragma unroll 1
@@ -90,12 +109,12 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     } else if (opc == ENG_OPC_STEP) {
       ++step;
     } else if (opc == ENG_OPC_LDLINE) {
-      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_soa(io.lines + ((size_t)(step * 12 + L.k) * FP_LIMBS) * io.cnt, io.cnt, L.i));
+      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, L.k)));
       ++step;
     } else if (opc == ENG_OPC_LD12) {
-      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_soa(io.fbuf + (size_t)(b + L.k) * FP_LIMBS * io.cnt, io.cnt, L.i));
+      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k)));
     } else if (opc == ENG_OPC_ST12) {
-      if (L.valid) st_soa(io.fbuf + (size_t)(b + L.k) * FP_LIMBS * io.cnt, io.cnt, L.i, eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
+      if (L.valid) st_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
     }
     asm volatile("" ::: "memory");
   }
@@ -166,7 +185,7 @@ __global__ void __launch_bounds__(ENG_BLOCK) k_eng_miller(size_t cnt, const uint
   eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
   asm volatile("" ::: "memory");
   eng_exec(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
-  if (L.valid) st_soa(fbuf + (size_t)L.k * FP_LIMBS * cnt, cnt, L.i, eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
+  if (L.valid) st_blk(fbuf, eng_blk_off(2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 
 // ---------------------------------------------------------------- k_eng_inv
@@ -210,7 +229,7 @@ __global__ void __launch_bounds__(ENG_BLOCK) k_eng_fe(size_t cnt, size_t r0, con
   eng_load_consts(c, consts);
   const eng_lane L = eng_lane_id(cnt);
   uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_FE) * ENG_SLOT_WORDS;
-  eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_soa(fbuf + (size_t)L.k * FP_LIMBS * cnt, cnt, L.i));
+  eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(2, 0, L.g, L.k)));
   if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
   asm volatile("" ::: "memory");
   eng_exec(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});

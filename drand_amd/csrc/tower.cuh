@@ -74,33 +74,33 @@ DG_NOINL fp2 fp2_inv(const fp2& a) {
 // square test in Fp2: a is a square iff its norm is a square in Fp
 DG_FN bool fp2_is_square(const fp2& a) { return fp_is_square(fp2_norm(a)); }
 
-// Square root in Fp2 (p = 3 mod 4) by the norm method.  Returns false if a is
+// sqrt(w) / m^2 for w in Fp2 whose norm is g^2 (g a square root of the norm),
+// m in Fp nonzero: one exponentiation, no inversion.  With d = (w0 + g) / 2
+// (or (w0 - g) / 2 when that is 0, i.e. w1 = 0) and t = (d m^4)^((p-3)/4):
+// d square -> d t + (w1 t / 2) u, else (w1 t / 2) - d t u.
+// Derivation and model: tools/sswu_model.py (sqrt_scaled).
+DG_NOINL fp2 fp2_sqrt_scaled(const fp2& w, const fp& g, const fp& m) {
+  fp d = fp_half(fp_add(w.c0, g));
+  d = fp_cmov(d, fp_half(fp_sub(w.c0, g)), fp_is_zero(d));
+  const fp m2 = fp_sqr(m);
+  const fp dm4 = fp_mul(d, fp_sqr(m2));
+  const fp t = fp_pow(dm4, EXP_P_MINUS_3_DIV_4, EXP_P_MINUS_3_DIV_4_BITS);
+  const bool sq = fp_eq(fp_mul(dm4, fp_sqr(t)), fp_one());
+  const fp dt = fp_mul(d, t);
+  const fp wt = fp_half(fp_mul(w.c1, t));
+  return sq ? fp2{dt, wt} : fp2{wt, fp_neg(dt)};
+}
+
+// Square root in Fp2 (p = 3 mod 4) by the norm method in two exponentiations
+// (the square test of the norm and fp2_sqrt_scaled).  Returns false if a is
 // not a square.  Which of the two roots is returned does not matter: every
 // caller fixes the sign afterwards (RFC 9380 sgn0 / ZCash sign bit).
 DG_NOINL bool fp2_sqrt(fp2& out, const fp2& a) {
-  if (fp_is_zero(a.c1)) {
-    fp s = fp_sqrt_cand(a.c0);
-    if (fp_eq(fp_sqr(s), a.c0)) {
-      out = fp2{s, fp_zero()};
-      return true;
-    }
-    fp na = fp_neg(a.c0);
-    s = fp_sqrt_cand(na);
-    out = fp2{fp_zero(), s};
-    return fp_eq(fp_sqr(s), na);
-  }
-  fp alpha = fp2_norm(a);
-  fp g = fp_sqrt_cand(alpha);
+  const fp alpha = fp2_norm(a);
+  const fp g = fp_sqrt_cand(alpha);
   if (!fp_eq(fp_sqr(g), alpha)) return false;
-  fp d = fp_half(fp_add(a.c0, g));
-  fp x0 = fp_sqrt_cand(d);
-  if (!fp_eq(fp_sqr(x0), d)) {
-    d = fp_half(fp_sub(a.c0, g));
-    x0 = fp_sqrt_cand(d);
-  }
-  fp x1 = fp_mul(a.c1, fp_inv(fp_dbl(x0)));
-  out = fp2{x0, x1};
-  return fp2_eq(fp2_sqr(out), a);
+  out = fp2_sqrt_scaled(a, g, fp_one());
+  return true;
 }
 
 // canonical (non-Montgomery) components

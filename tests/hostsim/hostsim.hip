@@ -100,10 +100,10 @@ void hs_hash_to_field(const uint8_t* msg32, uint8_t* out192) {
   fp_to_be(u0.c0, out192); fp_to_be(u0.c1, out192 + 48); fp_to_be(u1.c0, out192 + 96); fp_to_be(u1.c1, out192 + 144);
 }
 
-// SSWU of u (96 bytes) -> affine x, y on E2' (4 x 48)
+// iso3(SSWU(u)) of u (96 bytes) -> affine x, y on E2 (4 x 48)
 void hs_sswu(const uint8_t* u96, uint8_t* out192) {
   fp2 u{fp_from_be(u96), fp_from_be(u96 + 48)};
-  g2a q = map_to_curve_sswu_g2(u);
+  g2a q = g2_to_affine(map_to_curve_sswu_iso3(u));
   fp_to_be(q.x.c0, out192); fp_to_be(q.x.c1, out192 + 48); fp_to_be(q.y.c0, out192 + 96); fp_to_be(q.y.c1, out192 + 144);
 }
 
@@ -190,7 +190,7 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
     msg_words(msgs32 + 32 * i, m);
     fp2 u0, u1;
     hash_to_field_g2(u0, u1, m);
-    g2j R = g2_add(iso3_map(map_to_curve_sswu_g2(u0)), iso3_map(map_to_curve_sswu_g2(u1)));
+    g2j R = g2_add(map_to_curve_sswu_iso3(u0), map_to_curve_sswu_iso3(u1));
     g2a s;
     if (g2_decompress(&s, sigs96 + 96 * i, true) != DEC_OK) return -2;
     uint64_t z = seed + 0x9E3779B97F4A7C15ull * (rounds[i] + 1);

@@ -78,7 +78,7 @@ def test_expand_hash_to_field_sswu(hostsim):
     for uu in u:
         o = buf(192)
         hostsim.hs_sswu(be(uu[0]) + be(uu[1]), o)
-        q = B.map_to_curve_sswu_g2(uu)
+        q = B.iso_map_g2(B.map_to_curve_sswu_g2(uu))
         assert [ib(o.raw[i * 48:(i + 1) * 48]) for i in range(4)] == [q[0][0], q[0][1], q[1][0], q[1][1]]
 
 

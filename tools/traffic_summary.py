@@ -1,11 +1,16 @@
 """Per-round HBM traffic of each verify kernel from separate rocprofv3 PMC
-passes (FETCH_SIZE, WRITE_SIZE; tools/gpu/full.sh), written to
+passes (FETCH_SIZE, WRITE_SIZE; tools/gpu/traffic.sh), written to
 profiles/<tag>_traffic.json for bench.py's roofline.traffic.
 
-FETCH_SIZE/WRITE_SIZE are taken as reported (bytes).  MI355X_MICROARCH.md:
-FETCH_SIZE reads 1/2 of the bytes only for 16-B-per-lane streaming loads;
-these kernels use 4-B-per-lane coalesced accesses (uncalibrated width), so no
-correction factor is applied; treat the figure as indicative."""
+MI355X_MICROARCH.md: FETCH_SIZE reads 1/2 of the bytes for 16-B-per-lane
+streaming loads and other access widths are uncalibrated.  The engine's own
+line buffer gives an exact calibration for its 4-B-per-lane SoA accesses:
+k_eng_lines stores exactly 68 x 12 x 14 x 4 = 45,696 B per round and
+k_eng_miller loads exactly those bytes (inputs/constants of either kernel are
+< 1% of that), so write_cal = 45,696 / WRITE_SIZE(k_eng_lines) and
+fetch_cal = 45,696 / FETCH_SIZE(k_eng_miller); the corrected per-round bytes
+(raw x cal) are what bench.py reports.  The line buffer (6 GB per chunk) far
+exceeds the 256 MiB Infinity Cache, so these bytes do reach HBM."""
 import csv
 import glob
 import json
@@ -13,21 +18,29 @@ import os
 import sys
 from collections import defaultdict
 
+LINE_BYTES_PER_ROUND = 68 * 12 * 14 * 4
+
 
 def main(d, rounds, out):
     tot = defaultdict(lambda: defaultdict(float))
-    for f in glob.glob(os.path.join(d, "*", "p_counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 tot[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]] += float(r["Counter_Value"])
-    res = {}
-    for k, v in tot.items():
-        if "FETCH_SIZE" in v or "WRITE_SIZE" in v:
-            res[k] = {"fetch_bytes_per_round": v.get("FETCH_SIZE", 0) / rounds,
-                      "write_bytes_per_round": v.get("WRITE_SIZE", 0) / rounds}
+    raw = {k: {"fetch": v.get("FETCH_SIZE", 0) / rounds, "write": v.get("WRITE_SIZE", 0) / rounds}
+           for k, v in tot.items() if "FETCH_SIZE" in v or "WRITE_SIZE" in v}
+    wl = raw.get("dgpu::k_eng_lines", {}).get("write")
+    fm = raw.get("dgpu::k_eng_miller", {}).get("fetch")
+    write_cal = LINE_BYTES_PER_ROUND / wl if wl else 1.0
+    fetch_cal = LINE_BYTES_PER_ROUND / fm if fm else 1.0
+    res = {k: {"fetch_bytes_per_round": v["fetch"] * fetch_cal, "write_bytes_per_round": v["write"] * write_cal,
+               "raw_fetch_size_per_round": v["fetch"], "raw_write_size_per_round": v["write"]}
+           for k, v in raw.items()}
+    doc = {"rounds": rounds, "fetch_cal": fetch_cal, "write_cal": write_cal, "kernels": res,
+           "note": __doc__.split("\n\n")[1]}
     with open(out, "w") as f:
-        json.dump({"rounds": rounds, "kernels": res, "note": __doc__.split("\n\n")[1]}, f, indent=1)
-    print(json.dumps(res, indent=1))
+        json.dump(doc, f, indent=1)
+    print(json.dumps({k: v for k, v in doc.items() if k != "note"}, indent=1))
 
 
 if __name__ == "__main__":

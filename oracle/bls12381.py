@@ -710,3 +710,80 @@ def verify_g2(pk_point, msg, sig_bytes, dst=DST_G2):
         return False
     hm = hash_to_g2(msg, dst)
     return pairing_check([(pk_point, hm), (g1_neg(G1_GEN), sig)])
+
+
+# ---------------------------------------------------------------- hash to G1 (RFC 9380 section 8.8.1)
+# Suite BLS12381G1_XMD:SHA-256_SSWU_RO_: expand_message_xmd (128 bytes), two
+# Fp elements, simplified SWU on E1' (Z = 11), the 11-isogeny E1' -> E1
+# (constants derived in tools/derive_iso11.py, pinned there by RFC 9380's
+# published k_(1,0) and test vector J.9.1), h_eff = 1 - x.
+from .iso11_consts import (ISO11_XDEN, ISO11_XNUM, ISO11_YDEN, ISO11_YNUM,  # noqa: E402
+                           SSWU1_A, SSWU1_B, SSWU1_Z)
+
+DST_G1 = b"BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_"
+
+
+def map_to_curve_sswu_g1(u):
+    A, Bc, Z = SSWU1_A, SSWU1_B, SSWU1_Z
+    u %= P
+    zu2 = Z * u * u % P
+    den = (zu2 * zu2 + zu2) % P
+    if den == 0:
+        x1 = Bc * fp_inv(Z * A) % P
+    else:
+        x1 = (-Bc) * fp_inv(A) * (1 + fp_inv(den)) % P
+    gx1 = (x1 * x1 * x1 + A * x1 + Bc) % P
+    x2 = zu2 * x1 % P
+    gx2 = (x2 * x2 * x2 + A * x2 + Bc) % P
+    if fp_is_square(gx1):
+        x, y = x1, fp_sqrt(gx1)
+    else:
+        x, y = x2, fp_sqrt(gx2)
+    if fp_sgn0(u) != fp_sgn0(y):
+        y = (-y) % P
+    return (x, y)
+
+
+def _fp_poly(coeffs, x):
+    acc = 0
+    for c in reversed(coeffs):
+        acc = (acc * x + c) % P
+    return acc
+
+
+def iso_map_g1(pt):
+    x, y = pt
+    xd, yd = _fp_poly(ISO11_XDEN, x), _fp_poly(ISO11_YDEN, x)
+    if xd == 0 or yd == 0:
+        return None
+    return (_fp_poly(ISO11_XNUM, x) * fp_inv(xd) % P, y * _fp_poly(ISO11_YNUM, x) * fp_inv(yd) % P)
+
+
+def clear_cofactor_g1(pt):
+    return g1_mul(pt, H_EFF_G1)
+
+
+def hash_to_g1(msg, dst=DST_G1):
+    u0, u1 = hash_to_field_fp(msg, 2, dst)
+    return clear_cofactor_g1(g1_add(iso_map_g1(map_to_curve_sswu_g1(u0)), iso_map_g1(map_to_curve_sswu_g1(u1))))
+
+
+# ---------------------------------------------------------------- BLS with signatures on G1 (kyber NewSchemeOnG1 (R))
+def sk_to_pk_g2(sk):
+    return g2_compress(g2_mul(G2_GEN, sk % R))
+
+
+def sign_g1(sk, msg, dst=DST_G1):
+    return g1_compress(g1_mul(hash_to_g1(msg, dst), sk % R))
+
+
+def verify_g1(pk_point_g2, msg, sig_bytes, dst=DST_G1):
+    """bls.Verify on G1 (R): HM = Hash(msg) in G1; sig = G1 UnmarshalBinary
+    (error -> invalid); e(HM, pk) * e(-sig, g2) == 1."""
+    try:
+        sig = g1_decompress(sig_bytes)
+    except DecodeError:
+        return False
+    if sig is None:
+        return False
+    return pairing_check([(hash_to_g1(msg, dst), pk_point_g2), (g1_neg(sig), G2_GEN)])

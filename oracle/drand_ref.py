@@ -14,7 +14,14 @@ from . import bls12381 as B
 SCHEME_CHAINED = "pedersen-bls-chained"
 SCHEME_UNCHAINED = "pedersen-bls-unchained"
 SCHEME_UNCHAINED_G1 = "bls-unchained-on-g1"
-DECOUPLE_PREV_SIG = {SCHEME_CHAINED: False, SCHEME_UNCHAINED: True, SCHEME_UNCHAINED_G1: True}
+SCHEME_G1_RFC9380 = "bls-unchained-g1-rfc9380"
+DECOUPLE_PREV_SIG = {SCHEME_CHAINED: False, SCHEME_UNCHAINED: True, SCHEME_UNCHAINED_G1: True,
+                     SCHEME_G1_RFC9380: True}
+# Signatures on G1 (public key on G2): the hash-to-G1 domain separation tag.
+# bls-unchained-on-g1 hashes to G1 under the G2 suite's DST (upstream drand's
+# historical choice (R); the scheme is absent from this snapshot, SURVEY.md
+# section 8c: unpinned); bls-unchained-g1-rfc9380 uses the RFC 9380 G1 DST.
+SIG_ON_G1_DST = {SCHEME_UNCHAINED_G1: B.DST_G2, SCHEME_G1_RFC9380: B.DST_G1}
 
 
 def round_to_bytes(r):
@@ -40,9 +47,9 @@ def randomness_from_signature(sig):
 def verify_beacon(scheme_id, pk_point, round_, prev_sig, sig):
     """chain/verify.go:38-45 -> key.Scheme.VerifyRecovered (kyber tbls ->
     bls.Verify (R)).  Returns True iff the reference would return nil."""
-    if scheme_id == SCHEME_UNCHAINED_G1:
-        raise NotImplementedError("bls-unchained-on-g1 oracle not built yet")
     msg = digest_message(scheme_id, round_, prev_sig)
+    if scheme_id in SIG_ON_G1_DST:  # pk_point on G2, sig on G1
+        return B.verify_g1(pk_point, msg, sig, SIG_ON_G1_DST[scheme_id])
     return B.verify_g2(pk_point, msg, sig)
 
 
@@ -53,14 +60,19 @@ REASON_OK, REASON_DECODE, REASON_SUBGROUP, REASON_PAIRING, REASON_INFINITY = 0, 
 def verify_reason(scheme_id, pk_point, round_, prev_sig, sig):
     """Like verify_beacon, but says why: the kyber error class (R)."""
     msg = digest_message(scheme_id, round_, prev_sig)
+    on_g1 = scheme_id in SIG_ON_G1_DST
     try:
-        s = B.g2_decompress(sig)
+        s = B.g1_decompress(sig) if on_g1 else B.g2_decompress(sig)
     except B.DecodeError as e:
         return REASON_SUBGROUP if "subgroup" in str(e) else REASON_DECODE
     if s is None:
         return REASON_INFINITY
-    hm = B.hash_to_g2(msg)
-    ok = B.pairing_check([(pk_point, hm), (B.g1_neg(B.G1_GEN), s)])
+    if on_g1:
+        hm = B.hash_to_g1(msg, SIG_ON_G1_DST[scheme_id])
+        ok = B.pairing_check([(hm, pk_point), (B.g1_neg(s), B.G2_GEN)])
+    else:
+        hm = B.hash_to_g2(msg)
+        ok = B.pairing_check([(pk_point, hm), (B.g1_neg(B.G1_GEN), s)])
     return REASON_OK if ok else REASON_PAIRING
 
 
@@ -82,13 +94,14 @@ def make_chain(seed, n, scheme_id=SCHEME_CHAINED, start_round=1, prev=None):
     (pk_bytes, [(round, prev_sig, sig)]).  For unchained schemes the stored
     PreviousSig is nil (chain/beacon/store.go:82-83)."""
     sk = derive_secret(seed)
-    pk = B.sk_to_pk(sk)
+    on_g1 = scheme_id in SIG_ON_G1_DST
+    pk = B.sk_to_pk_g2(sk) if on_g1 else B.sk_to_pk(sk)
     prev = derive_genesis(seed) if prev is None else prev
     out = []
     for i in range(n):
         rnd = start_round + i
         msg = digest_message(scheme_id, rnd, prev)
-        sig = B.sign_g2(sk, msg)
+        sig = B.sign_g1(sk, msg, SIG_ON_G1_DST[scheme_id]) if on_g1 else B.sign_g2(sk, msg)
         stored_prev = prev if not DECOUPLE_PREV_SIG[scheme_id] else b""
         out.append((rnd, stored_prev, sig))
         prev = sig

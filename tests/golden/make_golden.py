@@ -48,10 +48,38 @@ def h2g2():
     dump("hash_to_g2.json", {"dst": B.DST_G2.decode(), "cases": out})
 
 
+def h2g1():
+    """RFC 9380 J.9.1 vector (pins the suite) and drand digests under both
+    DSTs the on-G1 schemes use."""
+    tv_dst = b"QUUX-V01-CS02-with-BLS12381G1_XMD:SHA-256_SSWU_RO_"
+    out = [{"msg": "", "dst": tv_dst.decode(), "h": B.g1_compress(B.hash_to_g1(b"", tv_dst)).hex(),
+            "source": "RFC 9380 J.9.1"}]
+    for scheme, dst in sorted(D.SIG_ON_G1_DST.items()):
+        for r in (1, 2, 1969, 184348345343):
+            m = D.digest_message(scheme, r, b"")
+            out.append({"msg": m.hex(), "dst": dst.decode(), "h": B.g1_compress(B.hash_to_g1(m, dst)).hex()})
+        for i in range(16):
+            m = hashlib.sha256(b"drand-mi355x/h2g1/" + bytes([i])).digest()
+            out.append({"msg": m.hex(), "dst": dst.decode(), "h": B.g1_compress(B.hash_to_g1(m, dst)).hex()})
+    dump("hash_to_g1.json", {"cases": out})
+
+
+def non_subgroup_g1(seed):
+    """A compressed point on E1 outside G1 (decodes, fails the subgroup test)."""
+    x = seed
+    while True:
+        x += 1
+        y = B.fp_sqrt(x ** 3 + 4)
+        if y is not None and not B.g1_in_subgroup((x, y)):
+            return B.g1_compress((x, y))
+
+
 def chain(name, scheme, seed, n):
     pk, ch = D.make_chain(seed, n, scheme)
     rounds = [{"round": r, "prev": p.hex(), "sig": s.hex(), "valid": True} for r, p, s in ch]
-    pkp = B.g1_decompress(pk)
+    on_g1 = scheme in D.SIG_ON_G1_DST
+    pkp = B.g2_decompress(pk) if on_g1 else B.g1_decompress(pk)
+    L = 48 if on_g1 else 96
     # corruption catalog (SURVEY.md 8(d)) on copies, with the oracle's verdicts
     cases = []
 
@@ -69,13 +97,16 @@ def chain(name, scheme, seed, n):
         add("prev_altered", r, bytes([p[0] ^ 1]) + p[1:], s)
         add("prev_truncated", r, p[:95], s)
         add("prev_nil", r, b"", s)
-    add("infinity", r, p, bytes([0xC0]) + bytes(95))
+    add("infinity", r, p, bytes([0xC0]) + bytes(L - 1))
     add("empty_sig", r, p, b"")
-    add("truncated_sig", r, p, s[:48])
+    add("truncated_sig", r, p, s[:L // 2])
     add("wrong_round", r - 1, p, s)  # test/mock/grpcserver.go:150-155
     add("compression_flag_clear", r, p, bytes([s[0] & 0x7F]) + s[1:])
-    add("infinity_noncanonical", r, p, bytes([0xC0]) + bytes(94) + b"\x01")
-    add("x_ge_p", r, p, bytes([0x80 | 0x1F]) + b"\xff" * 95)
+    add("infinity_noncanonical", r, p, bytes([0xC0]) + bytes(L - 2) + b"\x01")
+    add("x_ge_p", r, p, bytes([0x80 | 0x1F]) + b"\xff" * (L - 1))
+    if on_g1:
+        add("not_in_subgroup", r, p, non_subgroup_g1(seed))
+        add("g2_sized_sig", r, p, s + bytes(48))
     dump(name, {"scheme": scheme, "seed": seed, "pk": pk.hex(), "genesis": D.derive_genesis(seed).hex(),
                 "rounds": rounds, "corrupted": cases})
 
@@ -166,6 +197,9 @@ if __name__ == "__main__":
     h2g2()
     chain("chain_chained_s1.json", D.SCHEME_CHAINED, 1, 24)
     chain("chain_unchained_s1.json", D.SCHEME_UNCHAINED, 1, 12)
+    h2g1()
+    chain("chain_on_g1_s1.json", D.SCHEME_UNCHAINED_G1, 1, 12)
+    chain("chain_g1_rfc9380_s2.json", D.SCHEME_G1_RFC9380, 2, 8)
     group_keys()
     if "--recover" in sys.argv or not os.path.exists(os.path.join(HERE, "recover_t17_n32.json")):
         recover_cases("recover_t3_n8.json", 3, 3, 8)

@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--n", type=int, default=32)
     ap.add_argument("--bad-rate", type=float, default=0.1, help="recover: fraction of rounds with one invalid partial")
     ap.add_argument("--rlc-seed", type=int, default=3)
+    ap.add_argument("--scheme", default="pedersen-bls-chained",
+                    choices=["pedersen-bls-chained", "pedersen-bls-unchained", "bls-unchained-on-g1",
+                             "bls-unchained-g1-rfc9380"],
+                    help="per-round/rlc modes: the chain's scheme (configs[3]: unchained and on-g1)")
     return ap.parse_args()
 
 
@@ -74,7 +78,8 @@ def legacy_stage_ops():
 
 # stage name (dgpu_stage_times) -> kernel symbol / op_counts.json stages
 STAGE_KERNEL = {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
-                "hash_to_g2": "k_hash_to_g2_beacons", "decode_g2": "k_decode_g2_sigs"}
+                "eng_lines_fixed": "k_eng_lines_fixed", "hash_to_g2": "k_hash_to_g2_beacons",
+                "decode_g2": "k_decode_g2_sigs", "hash_to_g1": "k_hash_to_g1_beacons", "decode_g1": "k_decode_g1_sigs"}
 STAGE_OPS = {"hash_to_g2": ["hash_to_g2"], "decode_g2": ["decode_g2"]}
 
 
@@ -261,7 +266,11 @@ def main():
 
     n = args.rounds or 1_000_000
     t_gen = time.time()
-    chain = make_chain(args.seed, n, _lib.SCHEME_CHAINED, seg_len=args.seg_len, device=local,
+    code = _lib.scheme_from_name(args.scheme) if hasattr(_lib, "scheme_from_name") else {
+        "pedersen-bls-chained": _lib.SCHEME_CHAINED, "pedersen-bls-unchained": _lib.SCHEME_UNCHAINED,
+        "bls-unchained-on-g1": _lib.SCHEME_UNCHAINED_G1, "bls-unchained-g1-rfc9380": _lib.SCHEME_G1_RFC9380}[args.scheme]
+    on_g1 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
+    chain = make_chain(args.seed, n, code, seg_len=args.seg_len, device=local,
                        start_round=rank * n + 1)
     bad = corrupt(chain, args.seed + rank, rate=args.corrupt_rate)
     t_gen = time.time() - t_gen
@@ -275,13 +284,13 @@ def main():
     d_bits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
     ctx = get_context(local)
     lib = ctx.lib
-    _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, chain.pk, 48))
+    _lib.check(lib.dgpu_set_pubkey(ctx.handle, code, chain.pk, len(chain.pk)))
     stream = torch.cuda.current_stream(dev)
     mode = _lib.MODE_RLC if args.mode == "rlc" else _lib.MODE_PER_ROUND
 
     def step():
         _lib.check(lib.dgpu_verify_batch_device(
-            ctx.handle, _lib.SCHEME_CHAINED, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96, d_sig_len.data_ptr(),
+            ctx.handle, code, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96, d_sig_len.data_ptr(),
             d_prev.data_ptr(), 96, d_prev_len.data_ptr(), mode, args.rlc_seed, d_bits.data_ptr(), None,
             ctypes.c_void_p(stream.cuda_stream)))
 
@@ -338,7 +347,8 @@ def main():
             except Exception as e:  # reported, never fatal
                 cpu = {"error": repr(e)}
         out = {
-            "metric": "verified beacon rounds/sec, chained BLS12-381 chain",
+            "metric": "verified beacon rounds/sec, chained BLS12-381 chain" if code == _lib.SCHEME_CHAINED
+                      else f"verified beacon rounds/sec, {args.scheme} chain",
             "value": value,
             "unit": "rounds/s",
             "n_gpus": world,
@@ -350,9 +360,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u32 (14x28-bit limb Fp, int32 VALU)",
             "data": "synthetic chained chain generated on GPU (seeded), 0.1% corrupted",
-            "config": {"workload": ("configs[1]: chained G2 chain, per-round pairing verify" if args.mode == "per-round"
+            "config": {"workload": (f"configs[3]: {args.scheme} chain, per-round pairing verify" if code != _lib.SCHEME_CHAINED
+                                    else "configs[1]: chained G2 chain, per-round pairing verify" if args.mode == "per-round"
                                     else "configs[2]: chained G2 chain, RLC batch verify + bisection, 0.1% corrupted"),
-                       "rounds_per_gpu": n, "seg_len": args.seg_len, "scheme": "pedersen-bls-chained",
+                       "rounds_per_gpu": n, "seg_len": args.seg_len, "scheme": args.scheme,
                        "mode": args.mode, "parallelism": f"shard{world}"},
             "stage_ms": stage_ms,
             "verdict_mismatches": mismatches,

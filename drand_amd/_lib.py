@@ -21,6 +21,7 @@ DGPU_ENOKEY = -5
 SCHEME_CHAINED = 0
 SCHEME_UNCHAINED = 1
 SCHEME_UNCHAINED_G1 = 2
+SCHEME_G1_RFC9380 = 3
 
 MODE_PER_ROUND = 0
 MODE_RLC = 1
@@ -49,6 +50,7 @@ SYMBOLS = [
     ("dgpu_stage_times", _c.c_int, [_P, _c.POINTER(_c.c_float), _c.c_int, _c.POINTER(_c.c_char_p)]),
     ("dgpu_digest_batch", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P]),
     ("dgpu_hash_to_g2", _c.c_int, [_P, _c.c_size_t, _P, _P]),
+    ("dgpu_hash_to_g1", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P]),
     ("dgpu_derive_pubkey", _c.c_int, [_P, _c.c_int, _P, _P, _c.c_size_t]),
     ("dgpu_make_chain", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _P, _P]),
     ("dgpu_set_group", _c.c_int, [_P, _c.c_int, _c.c_int, _P]),

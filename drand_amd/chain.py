@@ -186,3 +186,15 @@ def hash_to_g2(msgs, device=0):
     out = np.zeros(n * 96, dtype=np.uint8)
     _lib.check(ctx.lib.dgpu_hash_to_g2(ctx.handle, n, _lib.ptr(m), _lib.ptr(out)))
     return [bytes(out[i * 96:(i + 1) * 96]) for i in range(n)]
+
+
+def hash_to_g1(msgs, scheme_code_=None, device=0):
+    """Hash to G1 (RFC 9380 G1 suite) of 32-byte messages under a G1-signature
+    scheme's DST -> 48-byte compressed points (parity surface)."""
+    ctx = get_context(device)
+    n = len(msgs)
+    m = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    out = np.zeros(n * 48, dtype=np.uint8)
+    code = _lib.SCHEME_UNCHAINED_G1 if scheme_code_ is None else scheme_code_
+    _lib.check(ctx.lib.dgpu_hash_to_g1(ctx.handle, code, n, _lib.ptr(m), _lib.ptr(out)))
+    return [bytes(out[i * 48:(i + 1) * 48]) for i in range(n)]

@@ -15,6 +15,7 @@
 #include "kernels.cuh"
 #include "pairing_engine.cuh"
 #include "recover.cuh"
+#include "g1sig.cuh"
 
 using namespace dgpu;
 
@@ -62,6 +63,10 @@ struct DevBuf {
 
 inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
+// signatures on G1 / public key on G2 (bls-unchained-on-g1, bls-unchained-g1-rfc9380)
+inline bool sig_on_g1(int scheme) { return scheme == DGPU_SCHEME_UNCHAINED_G1 || scheme == DGPU_SCHEME_G1_RFC9380; }
+inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && scheme <= DGPU_SCHEME_G1_RFC9380; }
+
 // rounds per pairing-engine chunk: the line buffer takes 45.7 KB per round (6 GB at 128Ki)
 constexpr size_t ENG_CHUNK = 131072;
 
@@ -74,6 +79,8 @@ struct dgpu_ctx {
   bool have_key = false;
   int key_scheme = -1;
   g1_key pk{};
+  // on-G1 schemes: the G2 public key and the fixed-Q line table (k_eng_lines_fixed)
+  DevBuf g1_table, g1_aux;
   // scratch
   DevBuf h_pts, sig_pts, status, h_z, h_pre;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
@@ -112,25 +119,27 @@ static void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
 
 // Engine block constants (slot order of tools/gen_engine.py: ONE, the two
 // pairing points (-x, y) -- the group key (zero until dgpu_set_pubkey) and
-// -g1 --, gamma1_1..5, gamma2_1..5).
-static int upload_eng_consts(dgpu_ctx* c) {
+// -g1 --, gamma1_1..5, gamma2_1..5).  unit_points: both points (1, 1), for
+// the on-G1 fixed-line table (written to `dst` instead of the context's block).
+static int upload_eng_consts(dgpu_ctx* c, bool unit_points = false, DevBuf* dst = nullptr) {
   eng_const_block cb;
   const fp2 g1c[5] = {C_FROB1_1, C_FROB1_2, C_FROB1_3, C_FROB1_4, C_FROB1_5};
   const fp2 g2c[5] = {C_FROB2_1, C_FROB2_2, C_FROB2_3, C_FROB2_4, C_FROB2_5};
   auto put = [&](int slot, const fp& v) { memcpy(cb.w + (slot - 64) * ENG_SLOT_WORDS, v.l, FP_LIMBS * 4); };
   put(ENG_C_ONE, fp_one());
-  put(ENG_C_NXP0, c->pk.neg_x);
-  put(ENG_C_YP0, c->pk.y);
-  put(ENG_C_NXP1, fp_neg(C_G1_X));
-  put(ENG_C_YP1, C_G1_NEG_Y);
+  put(ENG_C_NXP0, unit_points ? fp_one() : c->pk.neg_x);
+  put(ENG_C_YP0, unit_points ? fp_one() : c->pk.y);
+  put(ENG_C_NXP1, unit_points ? fp_one() : fp_neg(C_G1_X));
+  put(ENG_C_YP1, unit_points ? fp_one() : C_G1_NEG_Y);
   for (int k = 0; k < 5; ++k) {
     put(ENG_C_G1 + 2 * k, g1c[k].c0);
     put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
     put(ENG_C_G2 + k, g2c[k].c0);
   }
   int rc;
-  if ((rc = c->eng_consts.ensure(sizeof cb))) return rc;
-  HIP_TRY(hipMemcpy(c->eng_consts.p, &cb, sizeof cb, hipMemcpyHostToDevice));
+  DevBuf* b = dst ? dst : &c->eng_consts;
+  if ((rc = b->ensure(sizeof cb))) return rc;
+  HIP_TRY(hipMemcpy(b->p, &cb, sizeof cb, hipMemcpyHostToDevice));
   return DGPU_OK;
 }
 
@@ -144,6 +153,7 @@ int dgpu_scheme_from_name(const char* name) {
   if (name[0] == 0 || !strcmp(name, "pedersen-bls-chained")) return DGPU_SCHEME_CHAINED;
   if (!strcmp(name, "pedersen-bls-unchained")) return DGPU_SCHEME_UNCHAINED;
   if (!strcmp(name, "bls-unchained-on-g1")) return DGPU_SCHEME_UNCHAINED_G1;
+  if (!strcmp(name, "bls-unchained-g1-rfc9380")) return DGPU_SCHEME_G1_RFC9380;
   return set_err(DGPU_EINVAL, "scheme [%s] is not valid", name);
 }
 
@@ -183,17 +193,24 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
-                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
   delete c;
 }
 
+static int set_pubkey_g2_locked(dgpu_ctx* c, int scheme, const uint8_t* pk);
+
 int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
   if (!c || !pk) return set_err(DGPU_EINVAL, "null argument");
-  if (scheme == DGPU_SCHEME_UNCHAINED_G1) return set_err(DGPU_EUNSUPPORTED, "bls-unchained-on-g1 not built yet");
-  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (sig_on_g1(scheme)) {
+    if (len != 96) return set_err(DGPU_EINVAL, "public key must be 96 bytes (compressed G2), got %zu", len);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    return set_pubkey_g2_locked(c, scheme, pk);
+  }
   if (len != 48) return set_err(DGPU_EINVAL, "public key must be 48 bytes (compressed G1), got %zu", len);
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
@@ -220,7 +237,7 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
 
 static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
                               hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
-                              const uint32_t* pk_items = nullptr);
+                              const uint32_t* pk_items = nullptr, const uint32_t* fixed_table = nullptr);
 
 // RLC batch verification with exact per-round verdicts (mode DGPU_MODE_RLC).
 // 1. R_i = pre-cofactor H(m_i) (Jacobian), sig_i decoded (+ subgroup), status.
@@ -337,7 +354,8 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
 // (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
 // final exponentiation.  Decode verdicts in `st` stay final.
 static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
-                              hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items) {
+                              hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
+                              const uint32_t* fixed_table) {
   if (!h_stride) h_stride = n;
   const size_t cap = std::min<size_t>(n, ENG_CHUNK);
   const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
@@ -352,9 +370,15 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
   for (size_t r0 = 0; r0 < n; r0 += cap) {
     const size_t cnt = std::min(cap, n - r0);
     const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
-    mark(c, s, "eng_lines");
-    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg, pk_items,
-                       consts, lines);
+    if (fixed_table) {  // on-G1: h and sg are affine G1 points, the G2 arguments fixed
+      mark(c, s, "eng_lines_fixed");
+      hipLaunchKernelGGL(k_eng_lines_fixed, dim3(blocks, ENG_LINE_STEPS), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, sg,
+                         fixed_table, lines);
+    } else {
+      mark(c, s, "eng_lines");
+      hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
+                         pk_items, consts, lines);
+    }
     HIP_TRY(hipGetLastError());
     mark(c, s, "eng_miller");
     hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
@@ -370,17 +394,106 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
   return DGPU_OK;
 }
 
+// On-G1 schemes: decode the G2 public key (subgroup-checked) and compute the
+// fixed-Q line table: the LINES program for (pk, g2) at P = (1, 1).
+static int set_pubkey_g2_locked(dgpu_ctx* c, int scheme, const uint8_t* pk) {
+  int rc;
+  const size_t tbl_words = (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS;
+  if ((rc = c->g1_table.ensure(tbl_words * 4)) || (rc = c->g1_aux.ensure(4096)) || (rc = c->misc.ensure(256))) return rc;
+  DevBuf unit;
+  if ((rc = upload_eng_consts(c, true, &unit))) return rc;
+  uint8_t* aux = (uint8_t*)c->g1_aux.p;
+  uint32_t* d_pk = (uint32_t*)aux;                       // affine G2, stride 1 (224 B)
+  uint32_t* d_g2 = (uint32_t*)(aux + 1024);              // generator, stride 1
+  int* d_rc = (int*)(aux + 2048);
+  uint8_t* d_in = aux + 3072;
+  g2a gen{C_G2_X, C_G2_Y};
+  uint32_t gw[G2A_WORDS];
+  memcpy(gw, gen.x.c0.l, 56);
+  memcpy(gw + 14, gen.x.c1.l, 56);
+  memcpy(gw + 28, gen.y.c0.l, 56);
+  memcpy(gw + 42, gen.y.c1.l, 56);
+  hipStream_t s = c->stream;
+  hipError_t e = hipMemcpyAsync(d_in, pk, 96, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_g2, gw, sizeof gw, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_decode_g2_pk, dim3(1), dim3(64), 0, s, d_in, d_pk, d_rc);
+    e = hipGetLastError();
+  }
+  int drc = -1;
+  if (e == hipSuccess) e = hipMemcpyAsync(&drc, d_rc, sizeof drc, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    unit.release();
+    return set_err(DGPU_EDEVICE, "set_pubkey: %s", hipGetErrorString(e));
+  }
+  if (drc != DEC_OK) {
+    unit.release();
+    return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
+  }
+  hipLaunchKernelGGL(k_eng_lines, dim3(1), dim3(ENG_BLOCK), 0, s, (size_t)1, (size_t)0, (size_t)1,
+                     (const uint32_t*)d_pk, (size_t)1, (const uint32_t*)nullptr, (const uint32_t*)d_g2,
+                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)c->g1_table.p);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  unit.release();
+  if (e != hipSuccess) return set_err(DGPU_EDEVICE, "set_pubkey lines: %s", hipGetErrorString(e));
+  c->have_key = true;
+  c->key_scheme = scheme;
+  return DGPU_OK;
+}
+
+// Signatures on G1: H(m) in G1 (+ batch affine), G1 signature decode, fixed-Q
+// lines, then the engine's Miller / inversion / final-exponentiation kernels.
+static int verify_g1_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
+                            size_t sig_stride, const uint32_t* d_sig_len, uint8_t* d_bits, uint8_t* d_reason,
+                            hipStream_t s) {
+  const unsigned B = 256;
+  int rc;
+  if ((rc = c->h_pts.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->sig_pts.ensure(n * 2 * FP_WORDS * 4)) ||
+      (rc = c->status.ensure(n)) || (rc = c->h_z.ensure(n * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4)))
+    return rc;
+  uint32_t* h = (uint32_t*)c->h_pts.p;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  c->n_ev = 0;
+  mark(c, s, "hash_to_g1");
+  hipLaunchKernelGGL(k_hash_to_g1_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds,
+                     scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, h, (uint32_t*)c->h_z.p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "h_affine");
+  hipLaunchKernelGGL(k_g1_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
+                     (const uint32_t*)c->h_z.p, (uint32_t*)c->h_pre.p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "decode_g1");
+  hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
+  HIP_TRY(hipGetLastError());
+  if ((rc = eng_pairing_locked(c, n, h, sg, st, s, 0, nullptr, nullptr, (const uint32_t*)c->g1_table.p))) return rc;
+  mark(c, s, "pack_verdicts");
+  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);
+  HIP_TRY(hipGetLastError());
+  mark(c, s);
+  if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, n, hipMemcpyDeviceToDevice, s));
+  return DGPU_OK;
+}
+
 static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
                                 size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev,
                                 size_t prev_stride, const uint32_t* d_prev_len, int mode, uint64_t rlc_seed,
                                 uint8_t* d_bits, uint8_t* d_reason, hipStream_t s) {
-  (void)rlc_seed;
-  if (scheme == DGPU_SCHEME_UNCHAINED_G1) return set_err(DGPU_EUNSUPPORTED, "bls-unchained-on-g1 not built yet");
-  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
   if (mode != DGPU_MODE_PER_ROUND && mode != DGPU_MODE_RLC) return set_err(DGPU_EINVAL, "bad mode %d", mode);
   if (!c->have_key) return set_err(DGPU_ENOKEY, "no public key installed (dgpu_set_pubkey)");
+  if (sig_on_g1(scheme) != sig_on_g1(c->key_scheme))
+    return set_err(DGPU_ENOKEY, "installed public key is for scheme %d, whose signatures are on the other group",
+                   c->key_scheme);
   if (n == 0) return DGPU_OK;
   bool chained = scheme == DGPU_SCHEME_CHAINED;
+  if (sig_on_g1(scheme)) {
+    if (mode != DGPU_MODE_PER_ROUND) return set_err(DGPU_EUNSUPPORTED, "RLC mode is built for G2 signatures only");
+    if (!d_rounds || !d_sigs || !d_sig_len || !d_bits || sig_stride < 48) return set_err(DGPU_EINVAL, "bad buffers");
+    return verify_g1_locked(c, scheme, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_bits, d_reason, s);
+  }
   if (!d_rounds || !d_sigs || !d_sig_len || !d_bits || sig_stride < 96) return set_err(DGPU_EINVAL, "bad buffers");
   if (chained && (!d_prev || !d_prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
   int rc;
@@ -565,6 +678,25 @@ int dgpu_hash_to_g2(dgpu_ctx* c, size_t n, const uint8_t* msg32, uint8_t* out96)
   return DGPU_OK;
 }
 
+int dgpu_hash_to_g1(dgpu_ctx* c, int scheme, size_t n, const uint8_t* msg32, uint8_t* out48) {
+  if (!c || !msg32 || !out48) return set_err(DGPU_EINVAL, "null argument");
+  if (!sig_on_g1(scheme)) return set_err(DGPU_EINVAL, "scheme %d does not sign on G1", scheme);
+  if (n == 0) return DGPU_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  int rc;
+  if ((rc = c->in_sigs.ensure(n * 32))) return rc;
+  if ((rc = c->misc.ensure(n * 48))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, msg32, n * 32, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_hash_to_g1_msgs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const uint8_t*)c->in_sigs.p,
+                     scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, (uint8_t*)c->misc.p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out48, c->misc.p, n * 48, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
 static scalar256 scalar_from_be32(const uint8_t* b) {
   scalar256 k;
   for (int w = 0; w < 8; ++w)
@@ -575,15 +707,21 @@ static scalar256 scalar_from_be32(const uint8_t* b) {
 
 int dgpu_derive_pubkey(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, uint8_t* pk_out, size_t pk_len) {
   if (!c || !sk_be32 || !pk_out) return set_err(DGPU_EINVAL, "null argument");
-  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EUNSUPPORTED, "scheme %d", scheme);
-  if (pk_len != 48) return set_err(DGPU_EINVAL, "pk_len must be 48");
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  const size_t want = sig_on_g1(scheme) ? 96 : 48;
+  if (pk_len != want) return set_err(DGPU_EINVAL, "pk_len must be %zu", want);
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  int rc = c->misc.ensure(64);
+  int rc = c->misc.ensure(128);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_derive_pubkey, dim3(1), dim3(64), 0, c->stream, scalar_from_be32(sk_be32), (uint8_t*)c->misc.p);
+  if (sig_on_g1(scheme))
+    hipLaunchKernelGGL(k_derive_pubkey_g2, dim3(1), dim3(64), 0, c->stream, scalar_from_be32(sk_be32),
+                       (uint8_t*)c->misc.p);
+  else
+    hipLaunchKernelGGL(k_derive_pubkey, dim3(1), dim3(64), 0, c->stream, scalar_from_be32(sk_be32),
+                       (uint8_t*)c->misc.p);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(pk_out, c->misc.p, 48, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(pk_out, c->misc.p, want, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return DGPU_OK;
 }
@@ -592,7 +730,7 @@ int dgpu_make_chain(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n_se
                     const uint64_t* first_round, const uint8_t* seed_prev, const uint32_t* seed_prev_len,
                     uint8_t* sigs_out) {
   if (!c || !sk_be32 || !first_round || !sigs_out) return set_err(DGPU_EINVAL, "null argument");
-  if (scheme != DGPU_SCHEME_CHAINED && scheme != DGPU_SCHEME_UNCHAINED) return set_err(DGPU_EUNSUPPORTED, "scheme %d", scheme);
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
   bool chained = scheme == DGPU_SCHEME_CHAINED;
   if (chained && (!seed_prev || !seed_prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs seed_prev");
   if (n_seg == 0 || seg_len == 0) return DGPU_OK;
@@ -618,7 +756,14 @@ int dgpu_make_chain(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n_se
   hipError_t e = hipMemcpyAsync(d_first.p, first_round, n_seg * 8, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(d_prev.p, pv.data(), n_seg * 96, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipMemcpyAsync(d_plen.p, pl.data(), n_seg * 4, hipMemcpyHostToDevice, s);
-  for (size_t j = 0; e == hipSuccess && j < seg_len; ++j) {
+  if (e == hipSuccess) e = hipMemsetAsync(d_sigs.p, 0, n_seg * seg_len * 96, s);
+  for (size_t j = 0; e == hipSuccess && sig_on_g1(scheme) && j < seg_len; ++j) {
+    hipLaunchKernelGGL(k_sign_step_g1, dim3(grid_for(n_seg, 64)), dim3(64), 0, s, n_seg, (const uint64_t*)d_first.p,
+                       (uint64_t)j, scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, sk, (uint8_t*)d_sigs.p + j * 96,
+                       seg_len * 96);
+    e = hipGetLastError();
+  }
+  for (size_t j = 0; e == hipSuccess && !sig_on_g1(scheme) && j < seg_len; ++j) {
     // segment-major output: round j of segment s at (s*seg_len + j)*96
     hipLaunchKernelGGL(k_sign_step, dim3(grid_for(n_seg, 64)), dim3(64), 0, s, n_seg, (const uint64_t*)d_first.p,
                        (uint64_t)j, (uint8_t*)d_prev.p, (uint32_t*)d_plen.p, chained ? 1 : 0, sk,

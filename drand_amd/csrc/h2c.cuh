@@ -119,11 +119,20 @@ constexpr uint32_t DST_G2_PRIME[11] = {0x424c535f, 0x5349475f, 0x424c5331, 0x323
                                                              0x47325f58, 0x4d443a53, 0x48412d32, 0x35365f53,
                                                              0x5357555f, 0x524f5f4e, 0x554c5f2b};
 
-// expand_message_xmd(msg (32 bytes), DST_G2, 256) -> 64 big-endian words
+// DST' word i: the G2 suite's DST, or (G1DST) the G1 suite's
+// "BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_", which differs in word 4 only.
+template <bool G1DST>
+DG_FN uint32_t dst_word(int i) {
+  return (G1DST && i == 4) ? 0x47315f58u : DST_G2_PRIME[i];
+}
+
+// expand_message_xmd(msg (32 bytes), DST, 32 ELL bytes) -> 8 ELL big-endian words
+// (ELL = 8: hash to G2, 256 bytes; ELL = 4: hash to G1, 128 bytes).
 // Message layouts (bytes):
-//  b0: Z_pad(64) || msg(32) || 0x01 0x00 || 0x00 || DST'(44)  = 143 bytes, 3 blocks
-//  bi: x(32) || i(1) || DST'(44)                              =  77 bytes, 2 blocks
-DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) {
+//  b0: Z_pad(64) || msg(32) || I2OSP(32 ELL, 2) || 0x00 || DST'(44)  = 143 bytes, 3 blocks
+//  bi: x(32) || i(1) || DST'(44)                                      =  77 bytes, 2 blocks
+template <bool G1DST, int ELL>
+DG_NOINL void expand_xmd(uint32_t out[8 * ELL], const uint32_t msg[8]) {
   // b0
   sha_state s0;
 #pragma unroll
@@ -132,19 +141,19 @@ DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) {
     uint32_t blk[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) blk[i] = msg[i];
-    // bytes 96..: 0x01 0x00 0x00 DST'[0]
-    blk[8] = 0x01000000u | (DST_G2_PRIME[0] >> 24);
+    // bytes 96..: I2OSP(32 ELL, 2) 0x00 DST'[0]
+    blk[8] = ((uint32_t)(32 * ELL) << 16) | (dst_word<G1DST>(0) >> 24);
 #pragma unroll
-    for (int i = 1; i < 8; ++i) blk[8 + i] = (DST_G2_PRIME[i - 1] << 8) | (DST_G2_PRIME[i] >> 24);
+    for (int i = 1; i < 8; ++i) blk[8 + i] = (dst_word<G1DST>(i - 1) << 8) | (dst_word<G1DST>(i) >> 24);
     sha_compress(s0, blk);
     // remaining DST' bytes: DST'[29..43] (15 bytes), then 0x80, zeros, length 143*8 = 1144
     uint32_t blk2[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) blk2[i] = 0;
-    blk2[0] = (DST_G2_PRIME[7] << 8) | (DST_G2_PRIME[8] >> 24);
-    blk2[1] = (DST_G2_PRIME[8] << 8) | (DST_G2_PRIME[9] >> 24);
-    blk2[2] = (DST_G2_PRIME[9] << 8) | (DST_G2_PRIME[10] >> 24);
-    blk2[3] = (DST_G2_PRIME[10] << 8) | 0x80u;
+    blk2[0] = (dst_word<G1DST>(7) << 8) | (dst_word<G1DST>(8) >> 24);
+    blk2[1] = (dst_word<G1DST>(8) << 8) | (dst_word<G1DST>(9) >> 24);
+    blk2[2] = (dst_word<G1DST>(9) << 8) | (dst_word<G1DST>(10) >> 24);
+    blk2[3] = (dst_word<G1DST>(10) << 8) | 0x80u;
     blk2[15] = 143 * 8;
     sha_compress(s0, blk2);
   }
@@ -154,23 +163,23 @@ DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) {
   uint32_t prev[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) prev[i] = 0;
-  for (int idx = 1; idx <= 8; ++idx) {
+  for (int idx = 1; idx <= ELL; ++idx) {
     sha_state s = sha_init();
     uint32_t blk[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) blk[i] = b0[i] ^ prev[i];
-    blk[8] = ((uint32_t)idx << 24) | (DST_G2_PRIME[0] >> 8);
+    blk[8] = ((uint32_t)idx << 24) | (dst_word<G1DST>(0) >> 8);
 #pragma unroll
-    for (int i = 1; i < 8; ++i) blk[8 + i] = (DST_G2_PRIME[i - 1] << 24) | (DST_G2_PRIME[i] >> 8);
+    for (int i = 1; i < 8; ++i) blk[8 + i] = (dst_word<G1DST>(i - 1) << 24) | (dst_word<G1DST>(i) >> 8);
     sha_compress(s, blk);
     // bytes 64..76: DST'[31..43] (13 bytes), 0x80, zeros, length 77*8 = 616
     uint32_t blk2[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) blk2[i] = 0;
-    blk2[0] = (DST_G2_PRIME[7] << 24) | (DST_G2_PRIME[8] >> 8);
-    blk2[1] = (DST_G2_PRIME[8] << 24) | (DST_G2_PRIME[9] >> 8);
-    blk2[2] = (DST_G2_PRIME[9] << 24) | (DST_G2_PRIME[10] >> 8);
-    blk2[3] = (DST_G2_PRIME[10] << 24) | 0x00800000u;
+    blk2[0] = (dst_word<G1DST>(7) << 24) | (dst_word<G1DST>(8) >> 8);
+    blk2[1] = (dst_word<G1DST>(8) << 24) | (dst_word<G1DST>(9) >> 8);
+    blk2[2] = (dst_word<G1DST>(9) << 24) | (dst_word<G1DST>(10) >> 8);
+    blk2[3] = (dst_word<G1DST>(10) << 24) | 0x00800000u;
     blk2[15] = 77 * 8;
     sha_compress(s, blk2);
 #pragma unroll
@@ -180,6 +189,8 @@ DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) {
     }
   }
 }
+
+DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) { expand_xmd<false, 8>(out, msg); }
 
 // 64 big-endian bytes (as 16 BE words) -> Fp (Montgomery): x = hi * 2^384 + lo
 DG_NOINL fp fp_from_be64_words(const uint32_t* w) {

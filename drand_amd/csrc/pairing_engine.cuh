@@ -241,3 +241,35 @@ __global__ void __launch_bounds__(ENG_BLOCK) k_eng_fe(size_t cnt, size_t r0, con
 }
 
 }  // namespace dgpu
+
+namespace dgpu {
+
+// ---------------------------------------------------------------- k_eng_lines_fixed
+// Signatures on G1: e(H_i, pk) e(-sig_i, g2) with both G2 arguments fixed per
+// key.  `table` holds the LINES program's exports for (pk, g2) evaluated at
+// P = (1, 1) (one item, blocked layout of block 0 / group 0; computed by
+// dgpu_set_pubkey); every export is linear in its pair's -x_P (exports 2, 3)
+// or y_P (4, 5), so item i's lines are the table scaled by P0 = H_i and
+// P1 = -sig_i = (x_s, -y_s).  Grid: (blocks of 5 items) x ENG_LINE_STEPS, one
+// thread per export; points are affine [x, y][limb][n].
+__global__ void __launch_bounds__(64) k_eng_lines_fixed(size_t n, size_t r0, size_t cnt,
+                                                        const uint32_t* __restrict__ h_pts,
+                                                        const uint32_t* __restrict__ s_pts,
+                                                        const uint32_t* __restrict__ table,
+                                                        uint32_t* __restrict__ lines) {
+  const int lane = threadIdx.x;
+  if (lane >= ENG_WAVE_WORDS) return;
+  const int g = lane / 12, e = lane % 12;
+  const size_t i = (size_t)blockIdx.x * ENG_ROUNDS_PER_BLOCK + g;
+  if (i >= cnt) return;
+  const int step = blockIdx.y, pair = e / 6, k = e % 6;
+  fp v = ld_blk(table, (size_t)step * FP_LIMBS * ENG_WAVE_WORDS + e);
+  if (k >= 2) {
+    const uint32_t* pts = pair ? s_pts : h_pts;
+    const fp c = k < 4 ? fp_neg(ld_fp(pts, n, r0 + i)) : ld_fp(pts + FP_WORDS * n, n, r0 + i);
+    v = fp_mul(v, (pair && k >= 4) ? fp_neg(c) : c);
+  }
+  st_blk(lines, (((size_t)blockIdx.x * ENG_LINE_STEPS + step) * FP_LIMBS) * ENG_WAVE_WORDS + lane, v);
+}
+
+}  // namespace dgpu

@@ -1,12 +1,14 @@
 """Scheme registry: mirrors common/scheme/scheme.go (same IDs, same lookup
 and error behaviour), plus the `bls-unchained-on-g1` scheme this build adds
-(absent from the reference snapshot)."""
+(absent from the reference snapshot) and its RFC 9380
+DST variant `bls-unchained-g1-rfc9380`."""
 import os
 from dataclasses import dataclass
 
 DEFAULT_SCHEME_ID = "pedersen-bls-chained"       # scheme.go:9
 UNCHAINED_SCHEME_ID = "pedersen-bls-unchained"   # scheme.go:12
 UNCHAINED_ON_G1_SCHEME_ID = "bls-unchained-on-g1"  # added (G1 signatures, G2 public key)
+G1_RFC9380_SCHEME_ID = "bls-unchained-g1-rfc9380"  # added: as on-g1 with the RFC 9380 G1 DST
 
 
 @dataclass(frozen=True)
@@ -21,6 +23,7 @@ _SCHEMES = [
     Scheme(DEFAULT_SCHEME_ID, False),
     Scheme(UNCHAINED_SCHEME_ID, True),
     Scheme(UNCHAINED_ON_G1_SCHEME_ID, True, sigs_on_g1=True),
+    Scheme(G1_RFC9380_SCHEME_ID, True, sigs_on_g1=True),
 ]
 
 
@@ -63,4 +66,4 @@ def get_scheme_from_env():
 def scheme_code(s):
     from . import _lib
     return {DEFAULT_SCHEME_ID: _lib.SCHEME_CHAINED, UNCHAINED_SCHEME_ID: _lib.SCHEME_UNCHAINED,
-            UNCHAINED_ON_G1_SCHEME_ID: _lib.SCHEME_UNCHAINED_G1}[s.id]
+            UNCHAINED_ON_G1_SCHEME_ID: _lib.SCHEME_UNCHAINED_G1, G1_RFC9380_SCHEME_ID: _lib.SCHEME_G1_RFC9380}[s.id]

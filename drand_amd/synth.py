@@ -67,9 +67,10 @@ def make_chain(seed, n, scheme_code=_lib.SCHEME_CHAINED, seg_len=64, device=0, s
     ctx = get_context(device)
     lib = ctx.lib
     sk = derive_secret(seed).to_bytes(32, "big")
-    pk = np.zeros(48, dtype=np.uint8)
+    on_g1 = scheme_code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
+    pk = np.zeros(96 if on_g1 else 48, dtype=np.uint8)
     skb = np.frombuffer(sk, dtype=np.uint8).copy()
-    _lib.check(lib.dgpu_derive_pubkey(ctx.handle, scheme_code, _lib.ptr(skb), _lib.ptr(pk), 48))
+    _lib.check(lib.dgpu_derive_pubkey(ctx.handle, scheme_code, _lib.ptr(skb), _lib.ptr(pk), pk.size))
     seg_len = max(1, min(seg_len, n))
     n_seg = (n + seg_len - 1) // seg_len
     first = (start_round + np.arange(n_seg, dtype=np.uint64) * seg_len).astype(np.uint64)
@@ -90,7 +91,7 @@ def make_chain(seed, n, scheme_code=_lib.SCHEME_CHAINED, seg_len=64, device=0, s
         starts = np.arange(0, n, seg_len)
         prev[starts] = seeds[: len(starts)]
         prev_len[starts] = 32
-    sig_len = np.full(n, 96, dtype=np.uint32)
+    sig_len = np.full(n, 48 if on_g1 else 96, dtype=np.uint32)
     return Chain(scheme_code, bytes(pk), rounds, out.copy(), sig_len, prev, prev_len, derive_genesis(seed))
 
 
@@ -150,7 +151,7 @@ def corrupt(chain, seed, rate=1e-3, kinds=ALL_CORRUPTIONS):
             chain.sigs[i] = 0
             chain.sigs[i, 0] = 0xC0
         elif kind == CORRUPT_TRUNCATED:
-            chain.sig_len[i] = 48 if (i & 1) else 0
+            chain.sig_len[i] = (chain.sig_len[i] // 2) if (i & 1) else 0
     return chosen
 
 

@@ -43,7 +43,10 @@ extern "C" {
 enum {
   DGPU_SCHEME_CHAINED = 0,      /* "pedersen-bls-chained":   msg = SHA256(prev || BE64(round)) */
   DGPU_SCHEME_UNCHAINED = 1,    /* "pedersen-bls-unchained": msg = SHA256(BE64(round))        */
-  DGPU_SCHEME_UNCHAINED_G1 = 2  /* "bls-unchained-on-g1":    G1 signatures, G2 public key     */
+  DGPU_SCHEME_UNCHAINED_G1 = 2, /* "bls-unchained-on-g1":    G1 signatures (48 B), G2 public key
+                                   (96 B); msg = SHA256(BE64(round)) hashed to G1 under the G2
+                                   suite's DST (upstream drand's choice (R), unpinned here)  */
+  DGPU_SCHEME_G1_RFC9380 = 3    /* "bls-unchained-g1-rfc9380": as above, RFC 9380 G1 DST    */
 };
 
 enum {
@@ -82,21 +85,26 @@ int dgpu_scheme_from_name(const char *name);
 
 /* Decode and install the group public key (chain.Info.PublicKey,
  * chain/convert.go:20-23): 48-byte compressed G1 for the G2-signature
- * schemes.  Rejects malformed or out-of-subgroup keys (DGPU_EINVAL). */
+ * schemes, 96-byte compressed G2 for the G1-signature schemes (which also
+ * precomputes the key's fixed Miller-loop lines).  Rejects malformed or
+ * out-of-subgroup keys (DGPU_EINVAL). */
 int dgpu_set_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t len);
 
 /* Batch form of Verifier.VerifyBeacon (chain/verify.go:38-45) over n beacons
  * given as fixed-stride records (host pointers):
  *   rounds[i]                   Beacon.Round
  *   sigs + i*sig_stride         Beacon.Signature, sig_len[i] bytes (any length
- *                               != 96 is a decode failure, like the reference)
+ *                               != 96 -- != 48 for the G1-signature schemes --
+ *                               is a decode failure, like the reference)
  *   prev + i*prev_stride        Beacon.PreviousSig, prev_len[i] <= prev_stride
  *                               bytes; ignored (may be NULL) for unchained schemes
  * mode: DGPU_MODE_PER_ROUND (one pairing check per round) or DGPU_MODE_RLC
  *       (random linear combination over the batch with coefficients derived
  *       from rlc_seed, exact per-round verdicts by bisection; the verdicts are
  *       identical to per-round mode except with probability <= 2^-64 per
- *       failing check; pass a fresh unpredictable seed for adversarial input).
+ *       failing check; pass a fresh unpredictable seed for adversarial input;
+ *       G2-signature schemes only).  The scheme must sign on the same group as
+ *       the installed key's scheme (else DGPU_ENOKEY).
  * verdict_bits: ceil(n/8) bytes out.  reason: optional n bytes out. */
 int dgpu_verify_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *sigs,
                       size_t sig_stride, const uint32_t *sig_len, const uint8_t *prev, size_t prev_stride,
@@ -114,12 +122,13 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
 
 /* Instrumentation: when enabled, every verify call records one HIP event
  * per kernel stage on the stream it runs on; dgpu_stage_times returns the
- * stage durations (ms) and names of the last call (per-round mode:
- * hash_to_g2, decode_g2, pairing_check, pack_verdicts; RLC mode:
- * rlc_hash_to_g2_raw, decode_g2, rlc_leaves_tree, rlc_bisection,
- * pack_verdicts; the pairing-engine kernels report as eng_lines,
- * eng_miller, eng_inv and eng_fe, summed over chunks) and returns the
- * number of stages written. */
+ * stage durations (ms) and names of the last call, summed per name over
+ * chunks (per-round mode: hash_to_g2, h_affine, decode_g2, eng_lines,
+ * eng_miller, eng_inv, eng_fe, pack_verdicts; G1 signatures: hash_to_g1,
+ * h_affine, decode_g1, eng_lines_fixed, ...; RLC mode: rlc_hash_to_g2_raw,
+ * decode_g2, rlc_leaves_tree, rlc_prep and the engine stages of the node
+ * checks, rlc_bisection; recovery: recover_hash, recover_decode, engine
+ * stages, recover_msm, recover_verdict) and returns the number written. */
 #define DGPU_MAX_STAGES 8
 int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
@@ -132,9 +141,13 @@ int dgpu_digest_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *round
  * compressed to 96 bytes each: the parity surface for hash-to-curve. */
 int dgpu_hash_to_g2(dgpu_ctx *ctx, size_t n, const uint8_t *msg32, uint8_t *out96);
 
-/* pk = sk * g1 (48-byte compressed G1) for a 32-byte big-endian secret:
- * synthetic-chain tool (KeyGroup.Point().Mul(secret, nil),
- * client/test/result/mock/result.go:88). */
+/* Hash-to-G1 of n 32-byte messages (RFC 9380 suite BLS12381G1_XMD:SHA-256_
+ * SSWU_RO_) with the DST of a G1-signature scheme, compressed to 48 bytes. */
+int dgpu_hash_to_g1(dgpu_ctx *ctx, int scheme, size_t n, const uint8_t *msg32, uint8_t *out48);
+
+/* pk = sk * g1 (48-byte compressed G1; 96-byte sk * g2 for the G1-signature
+ * schemes) for a 32-byte big-endian secret: synthetic-chain tool
+ * (KeyGroup.Point().Mul(secret, nil), client/test/result/mock/result.go:88). */
 int dgpu_derive_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, uint8_t *pk_out, size_t pk_len);
 
 /* Threshold group public polynomial share.PubPoly (kyber (R); key/keys.go

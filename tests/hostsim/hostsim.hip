@@ -6,6 +6,8 @@
 #include <cstring>
 #include "../../drand_amd/csrc/h2c.cuh"
 #include "../../drand_amd/csrc/pairing.cuh"
+#define DG_NO_KERNELS
+#include "../../drand_amd/csrc/g1sig.cuh"
 
 using namespace dgpu;
 
@@ -105,6 +107,23 @@ void hs_sswu(const uint8_t* u96, uint8_t* out192) {
   fp2 u{fp_from_be(u96), fp_from_be(u96 + 48)};
   g2a q = g2_to_affine(map_to_curve_sswu_iso3(u));
   fp_to_be(q.x.c0, out192); fp_to_be(q.x.c1, out192 + 48); fp_to_be(q.y.c0, out192 + 96); fp_to_be(q.y.c1, out192 + 144);
+}
+
+// hash to G1 (g1dst: RFC 9380 G1 DST, else the G2 suite's DST), compressed
+void hs_hash_to_g1(const uint8_t* msg32, int g1dst, uint8_t* out48) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  g1j h = hash_to_g1(m, g1dst != 0);
+  bool inf = g1_is_inf(h);
+  g1_compress(out48, inf ? g1a{fp_zero(), fp_zero()} : g1_to_affine(h), inf);
+}
+
+// G1 signature decode (endomorphism membership test); recompressed on success
+int hs_decompress_g1(const uint8_t* in48, uint8_t* recompressed) {
+  g1a p{fp_zero(), fp_zero()};
+  int rc = g1_decompress_sig(&p, in48);
+  if (rc == DEC_OK) g1_compress(recompressed, p, false);
+  return rc;
 }
 
 void hs_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {

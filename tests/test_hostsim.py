@@ -166,3 +166,33 @@ def test_engine_pairing_host_emulation(hostsim):
         w = [exp[0][0], exp[1][0], exp[0][1], exp[1][1], exp[0][2], exp[1][2]]
         got = [ib(out.raw[48 * k:48 * k + 48]) for k in range(12)]
         assert got == [c % P for pair in w for c in pair]
+
+
+def test_hash_to_g1_golden(hostsim):
+    """Kernel hash-to-G1 (inversion-free SSWU + 11-isogeny, both DSTs) vs the
+    oracle's fixture, including drand digests under the legacy and RFC DSTs."""
+    for c in load_golden("hash_to_g1.json")["cases"]:
+        if c["msg"] == "":
+            continue  # the RFC vector's empty message is not a 32-byte digest
+        o = buf(48)
+        hostsim.hs_hash_to_g1(bytes.fromhex(c["msg"]), 1 if "G1" in c["dst"] else 0, o)
+        assert o.raw.hex() == c["h"], c
+
+
+def test_decompress_g1_catalog(hostsim):
+    """G1 signature decode verdicts (incl. the endomorphism subgroup test) on
+    the on-G1 chain fixtures' catalog and valid rounds."""
+    codes = {0: D.REASON_OK, 4: D.REASON_INFINITY, 7: D.REASON_SUBGROUP}
+    for name in ("chain_on_g1_s1.json", "chain_g1_rfc9380_s2.json"):
+        g = load_golden(name)
+        for r in g["rounds"][:4]:
+            o = buf(48)
+            assert hostsim.hs_decompress_g1(bytes.fromhex(r["sig"]), o) == 0
+            assert o.raw.hex() == r["sig"]
+        for c in g["corrupted"]:
+            sig = bytes.fromhex(c["sig"])
+            if len(sig) != 48:
+                continue
+            rc = hostsim.hs_decompress_g1(sig, buf(48))
+            want = c["reason"] if c["reason"] != D.REASON_PAIRING else D.REASON_OK
+            assert codes.get(rc, D.REASON_DECODE) == want, (c["kind"], rc)

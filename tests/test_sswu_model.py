@@ -38,3 +38,9 @@ def test_fp2_sqrt_two_exponentiations():
         assert (r is not None) == B.f2_is_square(a), a
         if r is not None:
             assert B.f2_sqr(r) == (a[0] % P, a[1] % P)
+
+
+def test_sswu_iso11_g1_matches_oracle():
+    rng = random.Random(3)
+    for u in [0, 1, P - 1] + [rng.randrange(P) for _ in range(150)]:
+        assert S.g1_to_affine(S.sswu_iso11_jacobian(u)) == B.iso_map_g1(B.map_to_curve_sswu_g1(u))

@@ -108,3 +108,47 @@ def to_affine(J):
     zi = B.f2_inv(Zj)
     zi2 = B.f2_sqr(zi)
     return (B.f2_mul(X, zi2), B.f2_mul(Y, B.f2_mul(zi2, zi)))
+
+
+# ---------------------------------------------------------------- G1: SSWU on E1' + 11-isogeny, inversion-free
+def sswu_iso11_jacobian(u):
+    """Kernel model (h2c_g1.cuh map_to_curve_sswu_iso11): x1 = N/D, gx1 = U/D^3;
+    t = (U V^3)^((p-3)/4) with V = D^3 gives y1 = U V t, a square root of
+    gx1 when y1^2 V = U, else of -gx1; then sqrt(gx2) = Z u^3 sqrt(-Z) y1
+    (gx2 = Z^3 u^6 gx1, -Z a square).  One exponentiation, no inversion."""
+    from oracle import iso11_consts as I
+    A, Bc, Z = I.SSWU1_A, I.SSWU1_B, I.SSWU1_Z
+    sqrt_mz = pow((-Z) % P, (P + 1) // 4, P)
+    assert sqrt_mz * sqrt_mz % P == (-Z) % P
+    u %= P
+    zu2 = Z * u * u % P
+    den = (zu2 * zu2 + zu2) % P
+    if den == 0:
+        N, D = Bc * pow(Z * A, P - 2, P) % P, 1
+    else:
+        N, D = (-Bc) * pow(A, P - 2, P) * (den + 1) % P, den
+    D3 = pow(D, 3, P)
+    U = (N * (N * N + A * D * D) + Bc * D3) % P
+    t = pow(U * pow(D3, 3, P) % P, (P - 3) // 4, P)
+    y = U * D3 * t % P
+    if y * y * D3 % P != U:
+        y = Z * pow(u, 3, P) * sqrt_mz * y % P
+        N = zu2 * N % P
+    if (u & 1) != (y & 1):
+        y = (-y) % P
+
+    def hom(coeffs, deg):
+        return sum(c * pow(N, i, P) * pow(D, deg - i, P) for i, c in enumerate(coeffs)) % P
+    xn, xd = hom(I.ISO11_XNUM, 11), hom(I.ISO11_XDEN, 10)
+    yn, yd = hom(I.ISO11_YNUM, 15), hom(I.ISO11_YDEN, 15)
+    xdd = xd * D % P
+    T = xdd * yd * yd % P
+    return xn * T % P, y * yn * xdd * xdd % P * T % P, xdd * yd % P
+
+
+def g1_to_affine(J):
+    X, Y, Zj = J
+    if Zj % P == 0:
+        return None
+    zi = pow(Zj, P - 2, P)
+    return (X * zi * zi % P, Y * zi * zi * zi % P)

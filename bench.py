@@ -359,7 +359,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32 (14x28-bit limb Fp, int32 VALU)",
-            "data": "synthetic chained chain generated on GPU (seeded), 0.1% corrupted",
+            "data": f"synthetic {args.scheme} chain generated on GPU (seeded), {args.corrupt_rate:.1%} corrupted",
             "config": {"workload": (f"configs[3]: {args.scheme} chain, per-round pairing verify" if code != _lib.SCHEME_CHAINED
                                     else "configs[1]: chained G2 chain, per-round pairing verify" if args.mode == "per-round"
                                     else "configs[2]: chained G2 chain, RLC batch verify + bisection, 0.1% corrupted"),

@@ -127,3 +127,113 @@ def check_past_beacons(store, verifier, pubkey, up_to, cb=None, window=1 << 16, 
                 return faulty or None
         i = hi
     return faulty or None
+
+
+# ---------------------------------------------------------------- streaming sync
+class SchemeStore:
+    """chain/beacon/store.go:56-95 schemeStore.Put: unchained schemes store
+    PreviousSig as nil; chained ones require PreviousSig to equal the last
+    stored signature or the stored signature of round - 1."""
+
+    def __init__(self, store, decouple_prev_sig):
+        self.store = store
+        self.decouple = decouple_prev_sig
+        try:
+            self._last = store.last()
+        except ErrNoBeaconSaved:
+            self._last = None
+
+    def put(self, b: Beacon):
+        if self.decouple:
+            b = Beacon(b"", b.round, b.signature)
+        elif self._last is None or self._last.signature != b.previous_sig:
+            try:
+                pb = self.store.get(b.round - 1)
+            except ErrNoBeaconSaved as e:
+                raise ValueError(f"invalid previous signature for {b.round} or previous beacon not found "
+                                 f"in database. Err: {e}") from None
+            if pb.signature != b.previous_sig:
+                raise ValueError(f"invalid previous signature for {b.round} or previous beacon not found "
+                                 f"in database. Err: <nil>")
+        self.store.put(b)
+        self._last = b
+
+    def last(self):
+        return self.store.last()
+
+    def get(self, round_):
+        return self.store.get(round_)
+
+
+def try_node(packets, verifier, pubkey, store, up_to, beacon_id=None, window=500, mode=0):
+    """Batch mirror of SyncManager.tryNode's receive loop
+    (chain/beacon/sync_manager.go:370-424).  `packets` yields (Beacon,
+    beacon_id or None) in stream order (the peer's channel; exhaustion = the
+    channel closed).  Up to `window` buffered packets (the peer buffer,
+    MaxSyncBuffer = 500, net/client_grpc.go:220) are verified in one GPU call;
+    then, per packet in order, exactly the reference's rules: a wrong beacon
+    ID -> False; an invalid beacon -> False (earlier ones stay stored);
+    store.put failure -> False; the beacon reaching up_to -> True.  Returns
+    (ok, last_stored_beacon or None)."""
+    it = iter(packets)
+    last = None
+    while True:
+        buf = []
+        for pkt in it:
+            buf.append(pkt)
+            if len(buf) >= window:
+                break
+        if not buf:
+            return False, last  # channel closed
+        # verify only the prefix the loop can reach: up to the first wrong ID
+        stop = next((k for k, (_, bid) in enumerate(buf) if bid is not None and beacon_id is not None
+                     and bid != beacon_id), len(buf))
+        reasons = verifier.verify_reasons([b for b, _ in buf[:stop]], pubkey, mode) if stop else []
+        for k, (b, _) in enumerate(buf):
+            if k == stop:
+                return False, last  # sync_manager.go:378-381
+            if int(reasons[k]) != 0:
+                return False, last  # :394-397
+            try:
+                store.put(b)
+            except Exception:
+                return False, last  # :406-410
+            last = b
+            if last.round == up_to:
+                return True, last  # :417-420
+
+
+def trusted_previous_signature(verifier, pubkey, get_signature, genesis_seed, round_, point_of_trust=None,
+                               window=1 << 14, mode=0):
+    """Batch mirror of verifyingClient.getTrustedPreviousSignature
+    (client/verify.go:118-178): walk from the point of trust (or round 1,
+    whose previous signature is the genesis seed) to round - 1, verifying each
+    fetched beacon with PreviousSig = the previous signature; here the walk's
+    beacons are verified `window` at a time.  `get_signature(r)` fetches round
+    r's signature (raise to signal a fetch error).  Returns (prev_sig,
+    new_point_of_trust) where the point of trust is (round, signature) or the
+    old one; raises VerifyError at the first invalid beacon, as the reference
+    returns "verifying beacon: ..."."""
+    from .chain import VerifyError
+    if round_ == 1:
+        return genesis_seed, point_of_trust
+    if point_of_trust is None or point_of_trust[0] > round_:
+        trust_round, trust_sig = 1, genesis_seed  # slow path: from round 1
+    else:
+        trust_round, trust_sig = point_of_trust
+    initial = trust_round
+    new_pot = point_of_trust
+    while trust_round < round_ - 1:
+        hi = min(round_ - 1, trust_round + window)
+        rounds = list(range(trust_round + 1, hi + 1))
+        sigs = [get_signature(r) for r in rounds]
+        prevs = [trust_sig] + sigs[:-1]
+        beacons = [Beacon(p, r, s) for p, r, s in zip(prevs, rounds, sigs)]
+        reasons = verifier.verify_reasons(beacons, pubkey, mode)
+        for b, rs in zip(beacons, reasons):
+            if int(rs) != 0:
+                raise VerifyError(b.round, int(rs))
+        trust_round, trust_sig = hi, sigs[-1]
+    if trust_round == round_ - 1 and trust_round > initial:
+        new_pot = (trust_round, trust_sig)
+    return trust_sig, new_pot

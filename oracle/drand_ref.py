@@ -235,3 +235,48 @@ def recover(commit_points, msg, partials, t, n, verify=None):
     for i, l in zip(order, lam):
         acc = B.g2_add(acc, B.g2_mul(ys[i], l))
     return B.g2_compress(acc)
+
+
+# ------------------------------------------------------------- streaming sync / client walk (sequential)
+def try_node(packets, verify, put, up_to, beacon_id=None):
+    """chain/beacon/sync_manager.go:370-424 restated: one packet at a time.
+    packets: iterable of (beacon, beacon_id | None); verify(beacon) -> bool;
+    put(beacon) may raise.  Returns (ok, last_stored)."""
+    last = None
+    for b, bid in packets:
+        if bid is not None and beacon_id is not None and bid != beacon_id:  # :378-381
+            return False, last
+        if not verify(b):  # :394-397
+            return False, last
+        try:
+            put(b)  # :399-410
+        except Exception:
+            return False, last
+        last = b
+        if last[0] == up_to:  # :417-420
+            return True, last
+    return False, last  # :372-375 channel closed
+
+
+def trusted_previous_signature(verify, get_signature, genesis_seed, round_, point_of_trust=None):
+    """client/verify.go:118-178 restated: returns (prev_sig, point_of_trust)
+    or raises ValueError("verifying beacon") at the first invalid beacon.
+    verify(round, prev, sig) -> bool."""
+    if round_ == 1:
+        return genesis_seed, point_of_trust
+    if point_of_trust is None or point_of_trust[0] > round_:
+        trust_round, trust_sig = 1, genesis_seed
+    else:
+        trust_round, trust_sig = point_of_trust
+    initial = trust_round
+    nxt = None
+    while trust_round < round_ - 1:
+        trust_round += 1
+        sig = get_signature(trust_round)
+        if not verify(trust_round, trust_sig, sig):
+            raise ValueError(f"verifying beacon {trust_round}")
+        trust_sig = sig
+        nxt = (trust_round, sig)
+    if trust_round == round_ - 1 and trust_round > initial:
+        point_of_trust = nxt
+    return trust_sig, point_of_trust

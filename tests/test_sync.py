@@ -96,3 +96,110 @@ def test_check_past_beacons_gpu_golden():
     exp, _ = D.check_past_beacons(table, 10**9, lambda b: b[2] == bytes.fromhex(
         next(x["sig"] for x in g["rounds"] if x["round"] == b[0])))
     assert got == exp and 5 in got
+
+
+# ---------------------------------------------------------------- tryNode / client walk mirrors
+def _packets(rng, n, start=1):
+    out = []
+    for r in range(start, start + n):
+        sig = (b"BAD" if rng.random() < 0.04 else b"ok") + r.to_bytes(4, "big")
+        bid = "other" if rng.random() < 0.02 else ("main" if rng.random() < 0.5 else None)
+        out.append((Beacon(b"", r, sig), bid))
+    return out
+
+
+@pytest.mark.parametrize("window", [1, 4, 500])
+def test_try_node_matches_oracle(window):
+    from drand_amd.sync import try_node
+    rng = random.Random(7 + window)
+    for trial in range(60):
+        pk = _packets(rng, rng.randint(0, 40))
+        up_to = rng.randint(0, 45)
+        fail_put = rng.choice([None, rng.randint(1, 45)])
+        stored_a, stored_b = [], []
+
+        class Store:
+            def __init__(self, sink):
+                self.sink = sink
+
+            def put(self, b):
+                if b.round == fail_put:
+                    raise ValueError("put failed")
+                self.sink.append(b.round)
+
+        ok, last = try_node(pk, MarkerVerifier(), b"pk", Store(stored_a), up_to, beacon_id="main", window=window)
+
+        def put_ref(b):
+            if b[0] == fail_put:
+                raise ValueError("put failed")
+            stored_b.append(b[0])
+        ok_r, last_r = D.try_node([((b.round, b.previous_sig, b.signature), bid) for b, bid in pk],
+                                  lambda b: not b[2].startswith(b"BAD"), put_ref, up_to, beacon_id="main")
+        assert (ok, stored_a) == (ok_r, stored_b)
+        assert (last.round if last else None) == (last_r[0] if last_r else None)
+
+
+def test_scheme_store_linkage():
+    from drand_amd.sync import SchemeStore
+    st = MemoryStore()
+    st.put(Beacon(b"", 0, b"g"))
+    ss = SchemeStore(st, decouple_prev_sig=False)
+    ss.put(Beacon(b"g", 1, b"s1"))
+    with pytest.raises(ValueError):
+        ss.put(Beacon(b"xx", 2, b"s2"))
+    ss.put(Beacon(b"s1", 2, b"s2"))
+    uns = SchemeStore(MemoryStore(), decouple_prev_sig=True)
+    uns.put(Beacon(b"anything", 5, b"s5"))
+    assert uns.get(5).previous_sig == b""
+
+
+@pytest.mark.parametrize("window", [1, 3, 1 << 14])
+def test_trusted_previous_signature_matches_oracle(window):
+    from drand_amd.chain import VerifyError
+    from drand_amd.sync import trusted_previous_signature
+    rng = random.Random(window)
+    for trial in range(40):
+        n = rng.randint(1, 30)
+        sigs = {r: (b"BAD" if rng.random() < 0.03 else b"ok") + bytes([r]) for r in range(1, n + 2)}
+        pot = rng.choice([None, (rng.randint(1, n), None)])
+        if pot:
+            pot = (pot[0], sigs[pot[0]])
+        target = rng.randint(1, n + 1)
+        try:
+            ref = D.trusted_previous_signature(lambda r, p, s: not s.startswith(b"BAD"), sigs.__getitem__,
+                                               b"seed", target, pot)
+        except ValueError:
+            ref = "error"
+        try:
+            got = trusted_previous_signature(MarkerVerifier(), b"pk", sigs.__getitem__, b"seed", target, pot,
+                                             window=window)
+        except VerifyError:
+            got = "error"
+        assert got == ref
+
+
+@pytest.mark.gpu
+def test_client_walk_and_try_node_gpu_golden():
+    """The batch client walk and tryNode mirrors with the real HIP verifier on
+    the golden chained chain: the walk returns round r-1's signature (and the
+    new point of trust), a corrupted round in the walk raises; tryNode stores
+    up to the first invalid beacon."""
+    from drand_amd.chain import VerifyError, new_verifier
+    from drand_amd.scheme import get_scheme_by_id_with_default
+    from drand_amd.sync import SchemeStore, trusted_previous_signature, try_node
+    g = load_golden("chain_chained_s1.json")
+    v = new_verifier(get_scheme_by_id_with_default(g["scheme"]))
+    pk = bytes.fromhex(g["pk"])
+    sig = {r["round"]: bytes.fromhex(r["sig"]) for r in g["rounds"]}
+    seed = bytes.fromhex(g["genesis"])
+    prev, pot = trusted_previous_signature(v, pk, sig.__getitem__, seed, 20, window=7)
+    assert prev == sig[19] and pot == (19, sig[19])
+    bad = dict(sig)
+    bad[10] = sig[11]
+    with pytest.raises(VerifyError):
+        trusted_previous_signature(v, pk, bad.__getitem__, seed, 20, window=7)
+    st = MemoryStore()
+    st.put(Beacon(b"", 0, seed))
+    packets = [(Beacon(bytes.fromhex(r["prev"]), r["round"], bad[r["round"]]), None) for r in g["rounds"]]
+    ok, last = try_node(packets, v, pk, SchemeStore(st, False), up_to=24, window=5)
+    assert not ok and last.round == 9 and st.len() == 10

@@ -82,7 +82,7 @@ struct dgpu_ctx {
   // on-G1 schemes: the G2 public key and the fixed-Q line table (k_eng_lines_fixed)
   DevBuf g1_table, g1_aux;
   // scratch
-  DevBuf h_pts, sig_pts, status, h_z, h_pre;
+  DevBuf h_pts, sig_pts, status, h_z, h_pre, h_tmp;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
   DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st;
   // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
@@ -193,7 +193,7 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
-                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -511,9 +511,18 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
     if (rc) return rc;
   } else {
     mark(c, s, "hash_to_g2");
-    if ((rc = c->h_z.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
-    hipLaunchKernelGGL(k_hash_to_g2_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
-                       d_prev_len, chained ? 1 : 0, h, (uint32_t*)c->h_z.p);
+    if ((rc = c->h_z.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4)) ||
+        (rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4)))
+      return rc;
+    uint32_t* u = (uint32_t*)c->h_tmp.p;
+    uint32_t* q = u + 4 * FP_WORDS * n;
+    hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride, d_prev_len,
+                       chained ? 1 : 0, u);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
+                       (uint32_t*)c->h_z.p);
     HIP_TRY(hipGetLastError());
     mark(c, s, "h_affine");
     hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,

@@ -229,7 +229,7 @@ DG_FN void hash_to_field_g2(fp2& u0, fp2& u1, const uint32_t msg[8]) {
 // included -- gives y = sqrt(w)/D^2 = fp2_sqrt_scaled(w, g, norm(D))
 // conj(D)^2.  The isogeny is evaluated on x = N/D homogeneously.  Model and
 // derivation: tools/sswu_model.py (tests/test_sswu_model.py).
-DG_NOINL g2j map_to_curve_sswu_iso3(const fp2& u) {
+DG_FN g2j map_to_curve_sswu_iso3_body(const fp2& u) {
   const fp2 zu2 = fp2_mul(C_SSWU_Z, fp2_sqr(u));
   const fp2 den = fp2_add(fp2_sqr(zu2), zu2);
   const bool den0 = fp2_is_zero(den);
@@ -270,6 +270,8 @@ DG_NOINL g2j map_to_curve_sswu_iso3(const fp2& u) {
   // an exceptional input (xd or yd = 0) gives Z = 0: the identity (RFC 9380 section 6.6.3)
   return r;
 }
+
+DG_NOINL g2j map_to_curve_sswu_iso3(const fp2& u) { return map_to_curve_sswu_iso3_body(u); }
 
 // hash_to_curve for G2 from the 32-byte drand digest; returns Jacobian H(m)
 DG_NOINL g2j hash_to_g2(const uint32_t msg[8]) {

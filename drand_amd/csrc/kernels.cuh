@@ -36,6 +36,27 @@ __device__ __forceinline__ g2a ld_g2a(const uint32_t* base, size_t n, size_t i) 
   return p;
 }
 
+constexpr int G2J_WORDS = 6 * FP_WORDS;
+
+__device__ __forceinline__ void st_g2j(uint32_t* base, size_t n, size_t i, const g2j& p) {
+  st_fp(base, n, i, p.x.c0);
+  st_fp(base + FP_WORDS * n, n, i, p.x.c1);
+  st_fp(base + 2 * FP_WORDS * n, n, i, p.y.c0);
+  st_fp(base + 3 * FP_WORDS * n, n, i, p.y.c1);
+  st_fp(base + 4 * FP_WORDS * n, n, i, p.z.c0);
+  st_fp(base + 5 * FP_WORDS * n, n, i, p.z.c1);
+}
+__device__ __forceinline__ g2j ld_g2j(const uint32_t* base, size_t n, size_t i) {
+  g2j p;
+  p.x.c0 = ld_fp(base, n, i);
+  p.x.c1 = ld_fp(base + FP_WORDS * n, n, i);
+  p.y.c0 = ld_fp(base + 2 * FP_WORDS * n, n, i);
+  p.y.c1 = ld_fp(base + 3 * FP_WORDS * n, n, i);
+  p.z.c0 = ld_fp(base + 4 * FP_WORDS * n, n, i);
+  p.z.c1 = ld_fp(base + 5 * FP_WORDS * n, n, i);
+  return p;
+}
+
 // per-round status codes carried between kernels (also the public `reason`)
 enum : uint8_t {
   ST_OK = 0,
@@ -63,6 +84,46 @@ __global__ void __launch_bounds__(256) k_hash_to_g2_beacons(size_t n, const uint
   uint32_t plen = chained ? prev_len[i] : 0u;
   drand_digest(msg, chained ? prev + i * prev_stride : nullptr, plen, rounds[i]);
   g2j h = hash_to_g2(msg);
+  st_g2a(h_out, n, i, g2a{h.x, h.y});
+  st_fp(z_out, n, i, h.z.c0);
+  st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
+}
+
+// The per-round hash to G2 as three launches (the fused kernel needs 512
+// registers per lane -- one wave per SIMD -- and 6 KB of scratch; each stage
+// alone is far lighter, and the SSWU stage has 2n independent items):
+//   k_h2c_field   DigestMessage + expand_message_xmd -> u0, u1 ([4 fp][n])
+//   k_h2c_sswu    SSWU + 3-isogeny of each of the 2n field elements -> Jacobian ([2][6 fp][n])
+//   k_h2c_finish  Q0 + Q1, cofactor clearing -> X, Y (h_out) and Z (z_out)
+__global__ void __launch_bounds__(256) k_h2c_field(size_t n, const uint64_t* __restrict__ rounds,
+                                                    const uint8_t* __restrict__ prev, size_t prev_stride,
+                                                    const uint32_t* __restrict__ prev_len, int chained,
+                                                    uint32_t* __restrict__ u_out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t msg[8];
+  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, chained ? prev_len[i] : 0u, rounds[i]);
+  uint32_t uni[64];
+  expand_xmd_g2(uni, msg);
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) st_fp(u_out + (size_t)k * FP_WORDS * n, n, i, fp_from_be64_words(uni + 16 * k));
+}
+
+__global__ void __launch_bounds__(256, 2) k_h2c_sswu(size_t n, const uint32_t* __restrict__ u,
+                                                   uint32_t* __restrict__ q_out) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const size_t which = j / n, i = j % n;
+  const uint32_t* ub = u + which * 2 * FP_WORDS * n;
+  const fp2 uu{ld_fp(ub, n, i), ld_fp(ub + FP_WORDS * n, n, i)};
+  st_g2j(q_out + which * G2J_WORDS * n, n, i, map_to_curve_sswu_iso3_body(uu));
+}
+
+__global__ void __launch_bounds__(256, 4) k_h2c_finish(size_t n, const uint32_t* __restrict__ q,
+                                                     uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const g2j h = g2_clear_cofactor(g2_add(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i)));
   st_g2a(h_out, n, i, g2a{h.x, h.y});
   st_fp(z_out, n, i, h.z.c0);
   st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
@@ -138,7 +199,7 @@ __global__ void __launch_bounds__(256) k_digest(size_t n, const uint64_t* __rest
 }
 
 // Signature decode (kilic G2.FromCompressed semantics (R)) + G2 membership.
-__global__ void __launch_bounds__(256) k_decode_g2_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
+__global__ void __launch_bounds__(256, 4) k_decode_g2_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
                                                          const uint32_t* __restrict__ sig_len,
                                                          uint32_t* __restrict__ sig_out, uint8_t* __restrict__ status) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -226,27 +287,6 @@ __global__ void k_derive_pubkey(scalar256 sk, uint8_t* __restrict__ out48) {
 // with R_i the pre-cofactor hash point (h_eff applied once per checked node,
 // by linearity) and d_i = e(pk, H_i) e(-g1, sig_i).  Jacobian G2 arrays are
 // SoA [6 Fp][limb][index].
-constexpr int G2J_WORDS = 6 * FP_WORDS;
-
-__device__ __forceinline__ void st_g2j(uint32_t* base, size_t n, size_t i, const g2j& p) {
-  st_fp(base, n, i, p.x.c0);
-  st_fp(base + FP_WORDS * n, n, i, p.x.c1);
-  st_fp(base + 2 * FP_WORDS * n, n, i, p.y.c0);
-  st_fp(base + 3 * FP_WORDS * n, n, i, p.y.c1);
-  st_fp(base + 4 * FP_WORDS * n, n, i, p.z.c0);
-  st_fp(base + 5 * FP_WORDS * n, n, i, p.z.c1);
-}
-__device__ __forceinline__ g2j ld_g2j(const uint32_t* base, size_t n, size_t i) {
-  g2j p;
-  p.x.c0 = ld_fp(base, n, i);
-  p.x.c1 = ld_fp(base + FP_WORDS * n, n, i);
-  p.y.c0 = ld_fp(base + 2 * FP_WORDS * n, n, i);
-  p.y.c1 = ld_fp(base + 3 * FP_WORDS * n, n, i);
-  p.z.c0 = ld_fp(base + 4 * FP_WORDS * n, n, i);
-  p.z.c1 = ld_fp(base + 5 * FP_WORDS * n, n, i);
-  return p;
-}
-
 // SplitMix64-derived nonzero 64-bit coefficient for round `round` under `seed`.
 __device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t round) {
   uint64_t z = seed + 0x9E3779B97F4A7C15ull * (round + 1);

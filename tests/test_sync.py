@@ -192,12 +192,18 @@ def test_client_walk_and_try_node_gpu_golden():
     pk = bytes.fromhex(g["pk"])
     sig = {r["round"]: bytes.fromhex(r["sig"]) for r in g["rounds"]}
     seed = bytes.fromhex(g["genesis"])
-    prev, pot = trusted_previous_signature(v, pk, sig.__getitem__, seed, 20, window=7)
+    prev, pot = trusted_previous_signature(v, pk, sig.__getitem__, seed, 20, point_of_trust=(5, sig[5]), window=7)
     assert prev == sig[19] and pot == (19, sig[19])
     bad = dict(sig)
     bad[10] = sig[11]
     with pytest.raises(VerifyError):
-        trusted_previous_signature(v, pk, bad.__getitem__, seed, 20, window=7)
+        trusted_previous_signature(v, pk, bad.__getitem__, seed, 20, point_of_trust=(5, sig[5]), window=7)
+    # without a point of trust the reference walks from (1, GenesisSeed) and
+    # verifies round 2 against the genesis seed (client/verify.go:129-160), so
+    # a chained walk fails at round 2 -- reproduced, not corrected
+    with pytest.raises(VerifyError) as e:
+        trusted_previous_signature(v, pk, sig.__getitem__, seed, 20, window=7)
+    assert e.value.round == 2
     st = MemoryStore()
     st.put(Beacon(b"", 0, seed))
     packets = [(Beacon(bytes.fromhex(r["prev"]), r["round"], bad[r["round"]]), None) for r in g["rounds"]]

@@ -141,7 +141,7 @@ __device__ __forceinline__ bool eng_eq_canon(const fp& x, const fp& K) {
 //   H_i = h_pts[h_idx ? h_idx[r0 + i] : r0 + i], S_i = sig_pts[r0 + i]
 //   (affine G2 SoA [x.c0, x.c1, y.c0, y.c1][limb][stride]),
 //   P_i = pk_items ? pk_items[r0 + i] ((-x, y) SoA [2][limb][n]) : the block constant key.
-__global__ void __launch_bounds__(ENG_BLOCK) k_eng_lines(size_t n, size_t r0, size_t cnt,
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0, size_t cnt,
                                                          const uint32_t* __restrict__ h_pts, size_t h_stride,
                                                          const uint32_t* __restrict__ h_idx,
                                                          const uint32_t* __restrict__ sig_pts,
@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(ENG_BLOCK) k_eng_lines(size_t n, size_t r0, si
 }
 
 // ---------------------------------------------------------------- k_eng_miller
-__global__ void __launch_bounds__(ENG_BLOCK) k_eng_miller(size_t cnt, const uint32_t* __restrict__ consts,
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller(size_t cnt, const uint32_t* __restrict__ consts,
                                                           uint32_t* __restrict__ lines,
                                                           uint32_t* __restrict__ fbuf, uint32_t* __restrict__ n1) {
   __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS];
@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256) k_eng_inv(size_t cnt, size_t r0, uint32_t
 }
 
 // ---------------------------------------------------------------- k_eng_fe
-__global__ void __launch_bounds__(ENG_BLOCK) k_eng_fe(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
                                                       uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ n1inv,
                                                       uint8_t* __restrict__ status) {
   __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_FE) * ENG_SLOT_WORDS];

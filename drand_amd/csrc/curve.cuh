@@ -32,7 +32,9 @@ DG_FN g2j g2_cmov(const g2j& a, const g2j& b, bool take_b) {
 }
 
 // dbl-2009-l (a = 0): 2M + 5S.  Infinity stays infinity (Z3 = 2YZ).
-DG_NOINL g2j g2_dbl(const g2j& p) {
+// (*_body: the same code force-inlined, for loops that keep the point in
+// registers instead of passing it through the stack to an out-of-line call)
+DG_FN g2j g2_dbl_body(const g2j& p) {
   fp2 A = fp2_sqr(p.x);
   fp2 B = fp2_sqr(p.y);
   fp2 C = fp2_sqr(B);
@@ -48,9 +50,11 @@ DG_NOINL g2j g2_dbl(const g2j& p) {
   return r;
 }
 
+DG_NOINL g2j g2_dbl(const g2j& p) { return g2_dbl_body(p); }
+
 // add-2007-bl with the exceptional cases resolved (P == Q -> dbl,
 // P == -Q -> infinity, either operand infinity -> the other).
-DG_NOINL g2j g2_add(const g2j& p, const g2j& q) {
+DG_FN g2j g2_add_body(const g2j& p, const g2j& q) {
   fp2 z1z1 = fp2_sqr(p.z);
   fp2 z2z2 = fp2_sqr(q.z);
   fp2 u1 = fp2_mul(p.x, z2z2);
@@ -74,6 +78,8 @@ DG_NOINL g2j g2_add(const g2j& p, const g2j& q) {
   return r;
 }
 
+DG_NOINL g2j g2_add(const g2j& p, const g2j& q) { return g2_add_body(p, q); }
+
 // Mixed addition p + q with q affine (madd-2007-bl: 7M + 4S), exceptional
 // cases resolved (p == q -> dbl, p == -q -> infinity, p infinity -> q).
 DG_NOINL g2j g2_add_affine(const g2j& p, const g2a& q) {
@@ -94,6 +100,17 @@ DG_NOINL g2j g2_add_affine(const g2j& p, const g2a& q) {
   r.z = fp2_sub(fp2_sqr(fp2_add(p.z, h)), fp2_add(z1z1, hh));
   if (h0 && !p_inf) r = r0 ? g2_dbl(g2_from_affine(q)) : g2_infinity();
   if (p_inf) r = g2_from_affine(q);
+  return r;
+}
+
+// [|x|] p with the group law inlined (register-resident loop state)
+DG_FN g2j g2_mul_absx_inl(const g2j& p) {
+  g2j r = p;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    r = g2_dbl_body(r);
+    if ((BLS_X_ABS >> i) & 1ull) r = g2_add_body(r, p);
+  }
   return r;
 }
 
@@ -151,6 +168,19 @@ DG_NOINL g2a g2_to_affine(const g2j& p) {
 DG_FN bool g2_on_curve_affine(const g2a& a) {
   fp2 rhs = fp2_add(fp2_mul(fp2_sqr(a.x), a.x), C_B2);
   return fp2_eq(fp2_sqr(a.y), rhs);
+}
+
+// Clear cofactor with the whole computation inlined (k_h2c_finish).
+DG_FN g2j g2_clear_cofactor_inl(const g2j& p) {
+  g2j t1 = g2_neg(g2_mul_absx_inl(p));
+  g2j t2 = g2_psi(p);
+  g2j t3 = g2_psi2(g2_dbl_body(p));
+  t3 = g2_add_body(t3, g2_neg(t2));
+  t2 = g2_add_body(t1, t2);
+  t2 = g2_neg(g2_mul_absx_inl(t2));
+  t3 = g2_add_body(t3, t2);
+  t3 = g2_add_body(t3, g2_neg(t1));
+  return g2_add_body(t3, g2_neg(p));
 }
 
 // Clear cofactor: h_eff * P = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P)

@@ -119,11 +119,11 @@ __global__ void __launch_bounds__(256, 2) k_h2c_sswu(size_t n, const uint32_t* _
   st_g2j(q_out + which * G2J_WORDS * n, n, i, map_to_curve_sswu_iso3_body(uu));
 }
 
-__global__ void __launch_bounds__(256, 4) k_h2c_finish(size_t n, const uint32_t* __restrict__ q,
+__global__ void __launch_bounds__(256, 2) k_h2c_finish(size_t n, const uint32_t* __restrict__ q,
                                                      uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const g2j h = g2_clear_cofactor(g2_add(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i)));
+  const g2j h = g2_clear_cofactor_inl(g2_add_body(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i)));
   st_g2a(h_out, n, i, g2a{h.x, h.y});
   st_fp(z_out, n, i, h.z.c0);
   st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);

@@ -90,7 +90,7 @@ struct dgpu_ctx {
   bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
   int grp_t = 0, grp_n = 0;
-  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok, rec_pts, rec_vpk,
+  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok, rec_pts, rec_vpk, rec_sel, rec_part,
       rec_st;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
@@ -193,7 +193,7 @@ void dgpu_close(dgpu_ctx* c) {
   hipStreamSynchronize(c->stream);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
-                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->rec_sel, &c->rec_part, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
                     &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
     b->release();
   hipStreamDestroy(c->stream);
@@ -858,10 +858,29 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   uint32_t* rpts = (uint32_t*)c->rec_pts.p;
   uint32_t* rpk = (uint32_t*)c->rec_vpk.p;
   uint8_t* rst = (uint8_t*)c->rec_st.p;
+  if ((rc = c->rec_sel.ensure(n_rounds * RECOVER_MAX_T * 2 * 4)) ||
+      (rc = c->rec_part.ensure(n_rounds * 4 * G2J_WORDS * 4)))
+    return rc;
+  uint32_t* sel = (uint32_t*)c->rec_sel.p;
+  uint32_t* xs = sel + n_rounds * RECOVER_MAX_T;
+  uint64_t* dig = (uint64_t*)c->rec_lam.p;
+  uint32_t* part = (uint32_t*)c->rec_part.p;
+  const int t = c->grp_t;
+  mark(c, s, "recover_select");
+  hipLaunchKernelGGL(k_recover_select, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, m, t,
+                     (const uint32_t*)c->rec_idx.p, (const uint8_t*)st, sel, xs, d_out, d_ok,
+                     (const uint32_t*)c->grp_commits.p, rpts, rpk, rst);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_lagrange");
+  hipLaunchKernelGGL(k_recover_lagrange, dim3(grid_for(n_rounds * RECOVER_MAX_T, 256)), dim3(256), 0, s, n_rounds, t,
+                     (const uint8_t*)d_ok, (const uint32_t*)xs, dig);
+  HIP_TRY(hipGetLastError());
   mark(c, s, "recover_msm");
-  hipLaunchKernelGGL(k_recover_rounds, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, m, c->grp_t,
-                     (const uint32_t*)c->rec_idx.p, (const uint8_t*)st, (const uint32_t*)sg, items,
-                     (uint32_t*)c->rec_lam.p, d_out, d_ok, (const uint32_t*)c->grp_commits.p, rpts, rpk, rst);
+  hipLaunchKernelGGL(k_recover_msm, dim3(grid_for(4 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t,
+                     (const uint8_t*)d_ok, (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_recover_finish, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, (const uint8_t*)d_ok,
+                     (const uint32_t*)part, d_out, rpts, rst);
   HIP_TRY(hipGetLastError());
   // VerifyRecovered: e(C_0, H(msg)) e(-g1, sig) == 1
   if ((rc = eng_pairing_locked(c, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;

@@ -82,7 +82,7 @@ DG_NOINL g2j g2_add(const g2j& p, const g2j& q) { return g2_add_body(p, q); }
 
 // Mixed addition p + q with q affine (madd-2007-bl: 7M + 4S), exceptional
 // cases resolved (p == q -> dbl, p == -q -> infinity, p infinity -> q).
-DG_NOINL g2j g2_add_affine(const g2j& p, const g2a& q) {
+DG_FN g2j g2_add_affine_body(const g2j& p, const g2a& q) {
   fp2 z1z1 = fp2_sqr(p.z);
   fp2 u2 = fp2_mul(q.x, z1z1);
   fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
@@ -102,6 +102,8 @@ DG_NOINL g2j g2_add_affine(const g2j& p, const g2a& q) {
   if (p_inf) r = g2_from_affine(q);
   return r;
 }
+
+DG_NOINL g2j g2_add_affine(const g2j& p, const g2a& q) { return g2_add_affine_body(p, q); }
 
 // [|x|] p with the group law inlined (register-resident loop state)
 DG_FN g2j g2_mul_absx_inl(const g2j& p) {
@@ -157,7 +159,7 @@ DG_NOINL bool g2_eq(const g2j& p, const g2j& q) {
 // G2 membership: psi(Q) == [x] Q  (Scott, "A note on group membership tests
 // for G1, G2 and GT on BLS pairing-friendly curves"); same verdict as the
 // reference's [r] Q == O test (R), checked against it in tests.
-DG_FN bool g2_in_subgroup(const g2j& p) { return g2_eq(g2_psi(p), g2_mul_x(p)); }
+DG_FN bool g2_in_subgroup(const g2j& p) { return g2_eq(g2_psi(p), g2_neg(g2_mul_absx_inl(p))); }
 
 DG_NOINL g2a g2_to_affine(const g2j& p) {
   fp2 zi = fp2_inv(p.z);
@@ -256,7 +258,7 @@ DG_FN g1j g1_infinity() { return g1j{fp_one(), fp_one(), fp_zero()}; }
 DG_FN bool g1_is_inf(const g1j& a) { return fp_is_zero(a.z); }
 DG_FN g1j g1_neg(const g1j& a) { return g1j{a.x, fp_neg(a.y), a.z}; }
 
-DG_NOINL g1j g1_dbl(const g1j& p) {
+DG_FN g1j g1_dbl_body(const g1j& p) {
   fp A = fp_sqr(p.x);
   fp B = fp_sqr(p.y);
   fp C = fp_sqr(B);
@@ -270,7 +272,9 @@ DG_NOINL g1j g1_dbl(const g1j& p) {
   return r;
 }
 
-DG_NOINL g1j g1_add(const g1j& p, const g1j& q) {
+DG_NOINL g1j g1_dbl(const g1j& p) { return g1_dbl_body(p); }
+
+DG_FN g1j g1_add_body(const g1j& p, const g1j& q) {
   fp z1z1 = fp_sqr(p.z), z2z2 = fp_sqr(q.z);
   fp u1 = fp_mul(p.x, z2z2), u2 = fp_mul(q.x, z1z1);
   fp s1 = fp_mul(fp_mul(p.y, q.z), z2z2), s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
@@ -290,6 +294,8 @@ DG_NOINL g1j g1_add(const g1j& p, const g1j& q) {
   if (q_inf) r = p;
   return r;
 }
+
+DG_NOINL g1j g1_add(const g1j& p, const g1j& q) { return g1_add_body(p, q); }
 
 // generic scalar multiplication by a little-endian 32-bit-word scalar
 DG_NOINL g1j g1_mul_words(const g1j& p, const uint32_t* k, int nwords) {

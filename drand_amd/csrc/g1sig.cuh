@@ -42,7 +42,7 @@ DG_NOINL fp iso11_hom(const uint32_t (*c)[FP_LIMBS], int deg, const fp& N, const
 // free: x1 = N/D, gx1 = U/V with V = D^3; t = (U V^3)^((p-3)/4) gives
 // y1 = U V t with y1^2 = gx1 (if y1^2 V = U) or -gx1; in the latter case
 // sqrt(gx2) = Z u^3 sqrt(-Z) y1 (gx2 = Z^3 u^6 gx1).  One exponentiation.
-DG_NOINL g1j map_to_curve_sswu_iso11(const fp& u) {
+DG_FN g1j map_to_curve_sswu_iso11_body(const fp& u) {
   const fp zu2 = fp_mul(C_SSWU1_Z, fp_sqr(u));
   const fp den = fp_add(fp_sqr(zu2), zu2);
   const bool den0 = fp_is_zero(den);
@@ -72,12 +72,15 @@ DG_NOINL g1j map_to_curve_sswu_iso11(const fp& u) {
   return r;
 }
 
-// [|x|] p, |x| = 0xd201000000010000
-DG_NOINL g1j g1_mul_absx(const g1j& p) {
+DG_NOINL g1j map_to_curve_sswu_iso11(const fp& u) { return map_to_curve_sswu_iso11_body(u); }
+
+// [|x|] p, |x| = 0xd201000000010000 (group law inlined: register-resident points)
+DG_FN g1j g1_mul_absx(const g1j& p) {
   g1j r = p;
+#pragma unroll 1
   for (int i = 62; i >= 0; --i) {
-    r = g1_dbl(r);
-    if ((BLS_X_ABS >> i) & 1ull) r = g1_add(r, p);
+    r = g1_dbl_body(r);
+    if ((BLS_X_ABS >> i) & 1ull) r = g1_add_body(r, p);
   }
   return r;
 }
@@ -85,7 +88,8 @@ DG_NOINL g1j g1_mul_absx(const g1j& p) {
 // hash_to_curve for G1 of a 32-byte digest; g1dst selects the G1 suite's DST
 // (bls-unchained-g1-rfc9380) over the G2 suite's (bls-unchained-on-g1).
 // Cofactor clearing by h_eff = 1 - x = 1 + |x|.
-DG_NOINL g1j hash_to_g1(const uint32_t msg[8], bool g1dst) {
+template <bool INL>
+DG_FN g1j hash_to_g1_t(const uint32_t msg[8], bool g1dst) {
   uint32_t uni[32];
   if (g1dst)
     expand_xmd<true, 4>(uni, msg);
@@ -93,9 +97,12 @@ DG_NOINL g1j hash_to_g1(const uint32_t msg[8], bool g1dst) {
     expand_xmd<false, 4>(uni, msg);
   const fp u0 = fp_from_be64_words(uni);
   const fp u1 = fp_from_be64_words(uni + 16);
-  const g1j q = g1_add(map_to_curve_sswu_iso11(u0), map_to_curve_sswu_iso11(u1));
-  return g1_add(q, g1_mul_absx(q));
+  const g1j q = INL ? g1_add_body(map_to_curve_sswu_iso11_body(u0), map_to_curve_sswu_iso11_body(u1))
+                   : g1_add(map_to_curve_sswu_iso11(u0), map_to_curve_sswu_iso11(u1));
+  return g1_add_body(q, g1_mul_absx(q));
 }
+
+DG_NOINL g1j hash_to_g1(const uint32_t msg[8], bool g1dst) { return hash_to_g1_t<false>(msg, g1dst); }
 
 // G1 membership of an affine point on E1: (beta x, y) == -[x^2] P (Scott's
 // endomorphism test; same verdict as [r] P == O, tests/test_oracle_g1.py).
@@ -135,13 +142,13 @@ DG_NOINL int g1_decompress_sig(g1a* out, const uint8_t* in) {
 // ---------------------------------------------------------------- kernels
 // H(m) in G1 for m = SHA-256(BE64(round)) (unchained DigestMessage,
 // chain/verify.go:24-32): X, Y into h_out ([x, y][limb][n]), Z into z_out.
-__global__ void __launch_bounds__(256) k_hash_to_g1_beacons(size_t n, const uint64_t* __restrict__ rounds, int g1dst,
+__global__ void __launch_bounds__(256, 2) k_hash_to_g1_beacons(size_t n, const uint64_t* __restrict__ rounds, int g1dst,
                                                              uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t msg[8];
   drand_digest(msg, nullptr, 0u, rounds[i]);
-  const g1j h = hash_to_g1(msg, g1dst != 0);
+  const g1j h = hash_to_g1_t<true>(msg, g1dst != 0);
   st_fp(h_out, n, i, h.x);
   st_fp(h_out + FP_WORDS * n, n, i, h.y);
   st_fp(z_out, n, i, h.z);
@@ -193,7 +200,7 @@ __global__ void __launch_bounds__(256) k_g1_batch_affine(size_t n, uint32_t* __r
 }
 
 // G1 signature decode + membership: affine [x, y][limb][n], status ST_*.
-__global__ void __launch_bounds__(256) k_decode_g1_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
+__global__ void __launch_bounds__(256, 2) k_decode_g1_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
                                                          const uint32_t* __restrict__ sig_len,
                                                          uint32_t* __restrict__ sig_out, uint8_t* __restrict__ status) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -8,7 +8,7 @@
 // all partial "items" of the batch), stop after t good ones; dedup by index
 // (xyCommit); fewer than t distinct -> failure; otherwise Lagrange at 0 over
 // Fr (x_i = index + 1) and the G2 multi-scalar multiplication
-// sum_j lambda_j sig_j (Straus: one shared doubling chain, mixed additions),
+// sum_j lambda_j sig_j (4-way split by the psi endomorphism, Straus, mixed additions),
 // compressed to 96 bytes; then VerifyRecovered (chain.go:165) of every
 // recovered signature under C_0 on the engine.
 #pragma once
@@ -142,23 +142,50 @@ __global__ void __launch_bounds__(64) k_sign_partials(size_t n_items, size_t m, 
   g2_compress(o + 2, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(sg), inf);
 }
 
-// One thread per round: selection (first t good in input order, dedup by
-// index), Lagrange coefficients (scratch: [round][j][8 words]), Straus MSM,
-// compression.  ok[r] = 1 iff recovery succeeded (else out96 is zeroed).
-__global__ void __launch_bounds__(64) k_recover_rounds(size_t n_rounds, size_t m, int t,
+// Recovery after the VerifyPartial pairings, in four launches (one thread per
+// round ran only n_rounds threads, at one wave per SIMD):
+//   k_recover_select    per round: the first t good partials in input order,
+//                       deduplicated by index (sel = items, xs = index + 1);
+//                       failures are final here (zero output, ok = 0)
+//   k_recover_lagrange  per (round, j): the Lagrange coefficient at 0 over Fr
+//                       as base-|x| digits, lambda = d0 + d1|x| + d2|x|^2 + d3|x|^3
+//   k_recover_msm       per (round, i < 4): P_i = sum_j d_{j,i} sig_j (Straus, 64 bits)
+//   k_recover_finish    per round: sum_j lambda_j sig_j = P0 - psi(P1) + psi^2(P2)
+//                       - psi^3(P3) (psi = [x] on G2, x < 0: [|x|] = -psi), compressed
+constexpr uint64_t RECOVER_ABSX_ODD = 0xd20100000001ull;  // |x| = 2^16 RECOVER_ABSX_ODD
+
+// w (little-endian 32-bit words of v < 2^256) <- v / |x|; returns v mod |x|.
+DG_FN uint64_t div_absx(uint32_t w[8]) {
+  const uint32_t low = w[0] & 0xFFFFu;
+  uint32_t q[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  uint64_t rem = 0;
+  for (int k = 14; k >= 0; --k) {  // 16-bit digit k of v >> 16, most significant first
+    const int bit = 16 * k + 16;
+    rem = (rem << 16) | ((w[bit >> 5] >> (bit & 31)) & 0xFFFFu);
+    const uint64_t qd = rem / RECOVER_ABSX_ODD;
+    rem -= qd * RECOVER_ABSX_ODD;
+    q[(16 * k) >> 5] |= (uint32_t)qd << ((16 * k) & 31);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = q[i];
+  return (rem << 16) | low;
+}
+
+__global__ void __launch_bounds__(64) k_recover_select(size_t n_rounds, size_t m, int t,
                                                        const uint32_t* __restrict__ idx,
-                                                       const uint8_t* __restrict__ status,
-                                                       const uint32_t* __restrict__ sig_pts, size_t n_items,
-                                                       uint32_t* __restrict__ lam, uint8_t* __restrict__ out96,
+                                                       const uint8_t* __restrict__ status, uint32_t* __restrict__ sel,
+                                                       uint32_t* __restrict__ xs, uint8_t* __restrict__ out96,
                                                        uint8_t* __restrict__ ok, const uint32_t* __restrict__ commits,
                                                        uint32_t* __restrict__ rec_pts, uint32_t* __restrict__ rec_pk,
                                                        uint8_t* __restrict__ rec_st) {
   const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rounds) return;
-  // VerifyRecovered operands: key = PubPoly.Commit() = C_0, signature below
+  // VerifyRecovered operands: key = PubPoly.Commit() = C_0
   st_fp(rec_pk, n_rounds, r, fp_neg(ld_fp(commits, t, 0)));
   st_fp(rec_pk + FP_LIMBS * n_rounds, n_rounds, r, ld_fp(commits + FP_LIMBS * t, t, 0));
-  uint32_t sel_idx[RECOVER_MAX_T], sel_item[RECOVER_MAX_T];
+  uint32_t sel_idx[RECOVER_MAX_T];
+  uint32_t* sl = sel + r * RECOVER_MAX_T;
+  uint32_t* xr = xs + r * RECOVER_MAX_T;
   int good = 0, distinct = 0;
   for (size_t j = 0; j < m && good < t; ++j) {
     const size_t item = r * m + j;
@@ -169,35 +196,76 @@ __global__ void __launch_bounds__(64) k_recover_rounds(size_t n_rounds, size_t m
     for (int q = 0; q < distinct; ++q) dup = dup || sel_idx[q] == id;
     if (!dup) {
       sel_idx[distinct] = id;
-      sel_item[distinct] = (uint32_t)item;
+      sl[distinct] = (uint32_t)item;
+      xr[distinct] = id + 1;
       ++distinct;
     }
   }
-  uint8_t* out = out96 + r * 96;
   if (distinct < t) {
-    for (int k = 0; k < 96; ++k) out[k] = 0;
+    for (int k = 0; k < 96; ++k) out96[r * 96 + k] = 0;
     ok[r] = 0;
     st_g2a(rec_pts, n_rounds, r, g2a{fp2_zero(), fp2_zero()});
     rec_st[r] = ST_DECODE;
     return;
   }
-  uint32_t xs[RECOVER_MAX_T];
-  for (int j = 0; j < t; ++j) xs[j] = sel_idx[j] + 1;
-  uint32_t* L = lam + r * (size_t)RECOVER_MAX_T * 8;
-  for (int j = 0; j < t; ++j) fr_lagrange_at_zero(xs, t, j, L + j * 8);
+  ok[r] = 1;
+}
+
+__global__ void __launch_bounds__(256) k_recover_lagrange(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
+                                                          const uint32_t* __restrict__ xs,
+                                                          uint64_t* __restrict__ digits) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_rounds * RECOVER_MAX_T) return;
+  const size_t r = g / RECOVER_MAX_T;
+  const int j = (int)(g % RECOVER_MAX_T);
+  if (j >= t || !ok[r]) return;
+  uint32_t w[8];
+  fr_lagrange_at_zero(xs + r * RECOVER_MAX_T, t, j, w);
+  uint64_t* d = digits + g * 4;
+  d[0] = div_absx(w);
+  d[1] = div_absx(w);
+  d[2] = div_absx(w);
+  d[3] = ((uint64_t)w[1] << 32) | w[0];  // the last quotient, < |x| since lambda < r < |x|^4
+}
+
+__global__ void __launch_bounds__(256, 2) k_recover_msm(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
+                                                     const uint32_t* __restrict__ sel,
+                                                     const uint64_t* __restrict__ digits,
+                                                     const uint32_t* __restrict__ sig_pts, size_t n_items,
+                                                     uint32_t* __restrict__ part) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 4 * n_rounds) return;
+  const size_t r = g >> 2;
+  const int i = (int)(g & 3);
+  if (!ok[r]) return;
+  const uint64_t* d = digits + r * RECOVER_MAX_T * 4 + i;
+  const uint32_t* sl = sel + r * RECOVER_MAX_T;
   g2j acc = g2_infinity();
-  for (int b = 254; b >= 0; --b) {
-    acc = g2_dbl(acc);
-    for (int j = 0; j < t; ++j) {
-      if ((L[j * 8 + (b >> 5)] >> (b & 31)) & 1u) acc = g2_add_affine(acc, ld_g2a(sig_pts, n_items, sel_item[j]));
-    }
+  for (int b = 63; b >= 0; --b) {
+    acc = g2_dbl_body(acc);
+    for (int j = 0; j < t; ++j)
+      if ((d[4 * j] >> b) & 1ull) acc = g2_add_affine_body(acc, ld_g2a(sig_pts, n_items, sl[j]));
   }
+  st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
+}
+
+__global__ void __launch_bounds__(64) k_recover_finish(size_t n_rounds, const uint8_t* __restrict__ ok,
+                                                       const uint32_t* __restrict__ part, uint8_t* __restrict__ out96,
+                                                       uint32_t* __restrict__ rec_pts, uint8_t* __restrict__ rec_st) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rounds || !ok[r]) return;
+  const g2j p0 = ld_g2j(part, n_rounds, r);
+  const g2j p1 = ld_g2j(part + G2J_WORDS * n_rounds, n_rounds, r);
+  const g2j p2 = ld_g2j(part + 2 * G2J_WORDS * n_rounds, n_rounds, r);
+  const g2j p3 = ld_g2j(part + 3 * G2J_WORDS * n_rounds, n_rounds, r);
+  g2j acc = g2_add(p0, g2_neg(g2_psi(p1)));
+  acc = g2_add(acc, g2_psi2(p2));
+  acc = g2_add(acc, g2_neg(g2_psi(g2_psi2(p3))));
   const bool inf = g2_is_inf(acc);
   const g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(acc);
-  g2_compress(out, a, inf);
+  g2_compress(out96 + r * 96, a, inf);
   st_g2a(rec_pts, n_rounds, r, a);
   rec_st[r] = inf ? (uint8_t)ST_INFINITY : (uint8_t)ST_OK;
-  ok[r] = 1;
 }
 
 // VerifyRecovered verdicts (chain/beacon/chain.go:165): a recovered signature

@@ -279,10 +279,16 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
   hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
   HIP_TRY(hipGetLastError());
   mark(c, s, "rlc_leaves_tree");
-  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, seed, rpts, sg, st, P[0], S[0]);
+  // R_i to affine in place (X, Y slots; Z follows them in the Jacobian SoA)
+  if ((rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
+  hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, rpts,
+                     (const uint32_t*)(rpts + 4 * FP_WORDS * n), (uint32_t*)c->h_pre.p);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, d_rounds, seed, rpts, sg, st, P[0],
+                     S[0]);
   HIP_TRY(hipGetLastError());
   for (size_t l = 0; l + 1 < sz.size(); ++l) {
-    hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(sz[l + 1], B)), dim3(B), 0, s, sz[l], P[l], S[l], sz[l + 1],
+    hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(2 * sz[l + 1], B)), dim3(B), 0, s, sz[l], P[l], S[l], sz[l + 1],
                        P[l + 1], S[l + 1]);
     HIP_TRY(hipGetLastError());
   }

@@ -136,6 +136,40 @@ DG_NOINL g2j g2_mul_words(const g2j& p, const uint32_t* k, int nwords) {
   return r;
 }
 
+// Non-adjacent form of a 64-bit scalar: k = (3k >> 1) - (k >> 1), and digit j
+// of NAF(k) is bit j of (3k >> 1) minus bit j of (k >> 1).  pos / neg hold the
+// +1 / -1 digits at positions 0..63, top the digit at position 64 (0 or +1).
+DG_FN void naf64(uint64_t k, uint64_t& pos, uint64_t& neg, uint32_t& top) {
+  const uint64_t lo = k + (k << 1);  // 3k = hi:lo
+  const uint64_t hi = (k >> 63) + (lo < k ? 1ull : 0ull);
+  const uint64_t h = (lo >> 1) | (hi << 63);  // (3k >> 1) mod 2^64
+  const uint64_t kk = k >> 1;
+  const uint64_t c = h ^ kk;
+  pos = h & c;
+  neg = kk & c;
+  top = (uint32_t)(hi >> 1);
+}
+
+// [k] q for an affine q and a 64-bit k: MSB-first signed double-and-add over
+// NAF(k) (about 21 mixed additions instead of 32), group law inlined so the
+// accumulator stays in registers (RLC leaves).
+DG_FN g2j g2_mul64_naf_affine(const g2a& q, uint64_t k) {
+  uint64_t pos, neg;
+  uint32_t top;
+  naf64(k, pos, neg, top);
+  const uint64_t any = pos | neg;
+  g2j r = top ? g2_from_affine(q) : g2_infinity();
+#pragma unroll 1
+  for (int i = 63; i >= 0; --i) {
+    r = g2_dbl_body(r);
+    if ((any >> i) & 1ull) {
+      const g2a t{q.x, fp2_cmov(q.y, fp2_neg(q.y), (neg >> i) & 1ull)};
+      r = g2_add_affine_body(r, t);
+    }
+  }
+  return r;
+}
+
 // [x] p with x < 0
 DG_FN g2j g2_mul_x(const g2j& p) { return g2_neg(g2_mul_absx(p)); }
 

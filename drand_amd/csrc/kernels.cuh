@@ -312,39 +312,40 @@ __global__ void __launch_bounds__(256) k_hash_to_g2_raw(size_t n, const uint64_t
 }
 
 // Leaves of the RLC tree: P_i = r_i R_i, S_i = r_i sig_i (infinity for rounds
-// whose decode verdict is already final).
+// whose decode verdict is already final).  R_i is affine here (k_g2_batch_affine
+// ran on the pre-cofactor hash points; (0, 0) marks the identity).  2n threads:
+// j < n computes P_j, j >= n computes S_{j-n}.
 __global__ void __launch_bounds__(256) k_rlc_leaves(size_t n, const uint64_t* __restrict__ rounds, uint64_t seed,
-                                                     const uint32_t* __restrict__ r_pts,
+                                                     const uint32_t* __restrict__ r_aff,
                                                      const uint32_t* __restrict__ sig_pts,
                                                      const uint8_t* __restrict__ status, uint32_t* __restrict__ p_out,
                                                      uint32_t* __restrict__ s_out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  g2j P = g2_infinity(), S = g2_infinity();
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const bool sig = j >= n;
+  const size_t i = sig ? j - n : j;
+  g2j acc = g2_infinity();
   if (status[i] == ST_OK) {
-    uint64_t r = rlc_coeff(seed, rounds[i]);
-    uint32_t k[2] = {(uint32_t)r, (uint32_t)(r >> 32)};
-    P = g2_mul_words(ld_g2j(r_pts, n, i), k, 2);
-    S = g2_mul_words(g2_from_affine(ld_g2a(sig_pts, n, i)), k, 2);
+    const g2a q = ld_g2a(sig ? sig_pts : r_aff, n, i);
+    if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) acc = g2_mul64_naf_affine(q, rlc_coeff(seed, rounds[i]));
   }
-  st_g2j(p_out, n, i, P);
-  st_g2j(s_out, n, i, S);
+  st_g2j(sig ? s_out : p_out, n, i, acc);
 }
 
-// One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied).
+// One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied); 2 n_out
+// threads, the first n_out on the P tree, the rest on the S tree.
 __global__ void __launch_bounds__(256) k_rlc_level(size_t n_in, const uint32_t* __restrict__ p_in,
                                                     const uint32_t* __restrict__ s_in, size_t n_out,
                                                     uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
-  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n_out) return;
-  size_t a = 2 * j, b = 2 * j + 1;
-  g2j P = ld_g2j(p_in, n_in, a), S = ld_g2j(s_in, n_in, a);
-  if (b < n_in) {
-    P = g2_add(P, ld_g2j(p_in, n_in, b));
-    S = g2_add(S, ld_g2j(s_in, n_in, b));
-  }
-  st_g2j(p_out, n_out, j, P);
-  st_g2j(s_out, n_out, j, S);
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * n_out) return;
+  const bool sig = t >= n_out;
+  const size_t j = sig ? t - n_out : t;
+  const uint32_t* in = sig ? s_in : p_in;
+  const size_t a = 2 * j, b = 2 * j + 1;
+  g2j P = ld_g2j(in, n_in, a);
+  if (b < n_in) P = g2_add_body(P, ld_g2j(in, n_in, b));
+  st_g2j(sig ? s_out : p_out, n_out, j, P);
 }
 
 // Check candidate nodes of one level: fail[c] = 1 iff

@@ -217,9 +217,13 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     z ^= z >> 31;
     if (!z) z = 1;
+    // the device's leaf arithmetic (R affine, signed NAF ladder), checked
+    // against plain double-and-add on the Jacobian point
     uint32_t k[2] = {(uint32_t)z, (uint32_t)(z >> 32)};
-    P = g2_add(P, g2_mul_words(R, k, 2));
-    S = g2_add(S, g2_mul_words(g2_from_affine(s), k, 2));
+    g2j rR = g2_mul64_naf_affine(g2_to_affine(R), z);
+    if (!g2_eq(rR, g2_mul_words(R, k, 2))) return -3;
+    P = g2_add(P, rR);
+    S = g2_add(S, g2_mul64_naf_affine(s, z));
   }
   g2a Pa = g2_to_affine(g2_clear_cofactor(P)), Sa = g2_to_affine(S);
   fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);

@@ -170,6 +170,43 @@ DG_FN g2j g2_mul64_naf_affine(const g2a& q, uint64_t k) {
   return r;
 }
 
+// NAF of a 32-bit scalar (digits 0..32) as +1 / -1 masks (see naf64).
+DG_FN void naf32(uint32_t k, uint64_t& pos, uint64_t& neg) {
+  const uint64_t h = (3ull * k) >> 1, kk = (uint64_t)(k >> 1), c = h ^ kk;
+  pos = h & c;
+  neg = kk & c;
+}
+
+// psi of an affine point: (conj(x) cx, conj(y) cy)
+DG_FN g2a g2a_psi(const g2a& q) {
+  return g2a{fp2_mul(fp2_conj(q.x), C_PSI_CX), fp2_mul(fp2_conj(q.y), C_PSI_CY)};
+}
+
+// [a] q + [b] pq for affine q, pq and 32-bit a, b: one shared ladder of at
+// most 33 doublings over NAF(a) and NAF(b) (Straus), mixed additions, group
+// law inlined.  With pq = psi(q) and q in G2 this is [a + b x] q (psi acts as
+// [x] on G2); the RLC leaves draw their coefficients as r = a + b x.
+DG_FN g2j g2_mul2_naf32_affine(const g2a& q, const g2a& pq, uint32_t a, uint32_t b) {
+  uint64_t ap, an, bp, bn;
+  naf32(a, ap, an);
+  naf32(b, bp, bn);
+  const uint64_t am = ap | an, bm = bp | bn;
+  g2j r = g2_infinity();
+#pragma unroll 1
+  for (int i = 63 - __builtin_clzll(am | bm | 1ull); i >= 0; --i) {
+    r = g2_dbl_body(r);
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {
+      if ((((s ? bm : am) >> i) & 1ull) == 0) continue;
+      const fp2 by = fp2_cmov(q.y, pq.y, s != 0);
+      const bool negd = (((s ? bn : an) >> i) & 1ull) != 0;
+      const g2a t{fp2_cmov(q.x, pq.x, s != 0), fp2_cmov(by, fp2_neg(by), negd)};
+      r = g2_add_affine_body(r, t);
+    }
+  }
+  return r;
+}
+
 // [x] p with x < 0
 DG_FN g2j g2_mul_x(const g2j& p) { return g2_neg(g2_mul_absx(p)); }
 

@@ -311,10 +311,14 @@ __global__ void __launch_bounds__(256) k_hash_to_g2_raw(size_t n, const uint64_t
   st_g2j(r_out, n, i, q);
 }
 
-// Leaves of the RLC tree: P_i = r_i R_i, S_i = r_i sig_i (infinity for rounds
-// whose decode verdict is already final).  R_i is affine here (k_g2_batch_affine
-// ran on the pre-cofactor hash points; (0, 0) marks the identity).  2n threads:
-// j < n computes P_j, j >= n computes S_{j-n}.
+// Leaves of the RLC tree: P_i = [a_i] R_i + [b_i] psi(R_i), S_i = [a_i] sig_i +
+// [b_i] psi(sig_i) with (a_i, b_i) the two halves of rlc_coeff (infinity for
+// rounds whose decode verdict is already final).  psi commutes with h_eff and
+// acts as [x] on G2, so h_eff P_i = [r_i] H_i and S_i = [r_i] sig_i with
+// r_i = a_i + b_i x: 2^64 distinct nonzero coefficients mod r (|a_i| < |x|), the
+// same soundness as a uniform 64-bit r_i, at half the doublings.  R_i is affine
+// here (k_g2_batch_affine ran on the pre-cofactor hash points; (0, 0) marks
+// the identity).  2n threads: j < n computes P_j, j >= n computes S_{j-n}.
 __global__ void __launch_bounds__(256) k_rlc_leaves(size_t n, const uint64_t* __restrict__ rounds, uint64_t seed,
                                                      const uint32_t* __restrict__ r_aff,
                                                      const uint32_t* __restrict__ sig_pts,
@@ -327,7 +331,10 @@ __global__ void __launch_bounds__(256) k_rlc_leaves(size_t n, const uint64_t* __
   g2j acc = g2_infinity();
   if (status[i] == ST_OK) {
     const g2a q = ld_g2a(sig ? sig_pts : r_aff, n, i);
-    if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) acc = g2_mul64_naf_affine(q, rlc_coeff(seed, rounds[i]));
+    if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) {
+      const uint64_t z = rlc_coeff(seed, rounds[i]);
+      acc = g2_mul2_naf32_affine(q, g2a_psi(q), (uint32_t)z, (uint32_t)(z >> 32));
+    }
   }
   st_g2j(sig ? s_out : p_out, n, i, acc);
 }

@@ -217,13 +217,16 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     z ^= z >> 31;
     if (!z) z = 1;
-    // the device's leaf arithmetic (R affine, signed NAF ladder), checked
-    // against plain double-and-add on the Jacobian point
-    uint32_t k[2] = {(uint32_t)z, (uint32_t)(z >> 32)};
-    g2j rR = g2_mul64_naf_affine(g2_to_affine(R), z);
-    if (!g2_eq(rR, g2_mul_words(R, k, 2))) return -3;
+    // the device's leaf arithmetic (k_rlc_leaves: R affine, psi split of the
+    // coefficient, joint NAF ladder), checked against plain double-and-add
+    const uint32_t a = (uint32_t)z, b = (uint32_t)(z >> 32);
+    const g2a Ra = g2_to_affine(R);
+    g2j rR = g2_mul2_naf32_affine(Ra, g2a_psi(Ra), a, b);
+    if (!g2_eq(rR, g2_add(g2_mul_words(R, &a, 1), g2_mul_words(g2_psi(R), &b, 1)))) return -3;
+    const uint32_t kw[2] = {a, b};
+    if (!g2_eq(g2_mul64_naf_affine(Ra, z), g2_mul_words(R, kw, 2))) return -4;
     P = g2_add(P, rR);
-    S = g2_add(S, g2_mul64_naf_affine(s, z));
+    S = g2_add(S, g2_mul2_naf32_affine(s, g2a_psi(s), a, b));
   }
   g2a Pa = g2_to_affine(g2_clear_cofactor(P)), Sa = g2_to_affine(S);
   fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);

@@ -136,8 +136,10 @@ def test_pairing_value_matches_generic(hostsim):
 
 
 def test_rlc_collapse_algebra(hostsim):
-    """sum r_i R_i with h_eff applied once == sum r_i H_i: a valid batch passes,
-    one altered round (valid point, wrong message) fails."""
+    """sum r_i R_i with h_eff applied once == sum r_i H_i, with the leaves
+    computed as the device does ([a] R + [b] psi(R), r = a + b x, joint NAF
+    ladder; each leaf checked against plain double-and-add): a valid batch
+    passes, one altered round (valid point, wrong message) fails."""
     g = load_golden("chain_chained_s1.json")
     pk = bytes.fromhex(g["pk"])
     rs = g["rounds"][:5]

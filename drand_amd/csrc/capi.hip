@@ -272,9 +272,19 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
   uint8_t* st = (uint8_t*)c->status.p;
   mark(c, s, "rlc_hash_to_g2_raw");
-  hipLaunchKernelGGL(k_hash_to_g2_raw, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride,
-                     d_prev_len, chained ? 1 : 0, rpts);
-  HIP_TRY(hipGetLastError());
+  {
+    // the per-round hash's field and SSWU stages, then Q0 + Q1 without the cofactor
+    if ((rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4))) return rc;
+    uint32_t* u = (uint32_t*)c->h_tmp.p;
+    uint32_t* q = u + 4 * FP_WORDS * n;
+    hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride, d_prev_len,
+                       chained ? 1 : 0, u);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_h2c_sum, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, rpts);
+    HIP_TRY(hipGetLastError());
+  }
   mark(c, s, "decode_g2");
   hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
   HIP_TRY(hipGetLastError());

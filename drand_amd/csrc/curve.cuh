@@ -186,6 +186,9 @@ DG_FN g2a g2a_psi(const g2a& q) {
 // most 33 doublings over NAF(a) and NAF(b) (Straus), mixed additions, group
 // law inlined.  With pq = psi(q) and q in G2 this is [a + b x] q (psi acts as
 // [x] on G2); the RLC leaves draw their coefficients as r = a + b x.
+// PSI_ON_DEMAND: pq is ignored and psi(q) recomputed at each of its digits
+// (2 Fp2 products each) instead of being held live across the ladder.
+template <bool PSI_ON_DEMAND = false>
 DG_FN g2j g2_mul2_naf32_affine(const g2a& q, const g2a& pq, uint32_t a, uint32_t b) {
   uint64_t ap, an, bp, bn;
   naf32(a, ap, an);
@@ -198,9 +201,14 @@ DG_FN g2j g2_mul2_naf32_affine(const g2a& q, const g2a& pq, uint32_t a, uint32_t
 #pragma unroll 1
     for (int s = 0; s < 2; ++s) {
       if ((((s ? bm : am) >> i) & 1ull) == 0) continue;
-      const fp2 by = fp2_cmov(q.y, pq.y, s != 0);
+      g2a t;
+      if (PSI_ON_DEMAND) {
+        t = s ? g2a_psi(q) : q;
+      } else {
+        t = g2a{fp2_cmov(q.x, pq.x, s != 0), fp2_cmov(q.y, pq.y, s != 0)};
+      }
       const bool negd = (((s ? bn : an) >> i) & 1ull) != 0;
-      const g2a t{fp2_cmov(q.x, pq.x, s != 0), fp2_cmov(by, fp2_neg(by), negd)};
+      t.y = fp2_cmov(t.y, fp2_neg(t.y), negd);
       r = g2_add_affine_body(r, t);
     }
   }

@@ -129,6 +129,15 @@ __global__ void __launch_bounds__(256, 2) k_h2c_finish(size_t n, const uint32_t*
   st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
 }
 
+// RLC mode's pre-cofactor hash point R = Q0 + Q1 (Jacobian, [6 fp][n]) from
+// k_h2c_sswu's output: the cofactor is cleared once per checked tree node.
+__global__ void __launch_bounds__(256, 2) k_h2c_sum(size_t n, const uint32_t* __restrict__ q,
+                                                  uint32_t* __restrict__ r_out) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_g2j(r_out, n, i, g2_add_body(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i)));
+}
+
 // Jacobian -> affine for n G2 points in place (X, Y in pts; Z in z) with one
 // Fp inversion per thread: thread t takes points t, t + T, ... (T threads in
 // the grid) and inverts the norms N(Z_i) by Montgomery's trick (prefix
@@ -296,21 +305,6 @@ __device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t round) {
   return z ? z : 1ull;
 }
 
-// Pre-cofactor hash point R (Jacobian) for m = DigestMessage(round, prev).
-__global__ void __launch_bounds__(256) k_hash_to_g2_raw(size_t n, const uint64_t* __restrict__ rounds,
-                                                         const uint8_t* __restrict__ prev, size_t prev_stride,
-                                                         const uint32_t* __restrict__ prev_len, int chained,
-                                                         uint32_t* __restrict__ r_out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t msg[8];
-  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, chained ? prev_len[i] : 0u, rounds[i]);
-  fp2 u0, u1;
-  hash_to_field_g2(u0, u1, msg);
-  g2j q = g2_add(map_to_curve_sswu_iso3(u0), map_to_curve_sswu_iso3(u1));
-  st_g2j(r_out, n, i, q);
-}
-
 // Leaves of the RLC tree: P_i = [a_i] R_i + [b_i] psi(R_i), S_i = [a_i] sig_i +
 // [b_i] psi(sig_i) with (a_i, b_i) the two halves of rlc_coeff (infinity for
 // rounds whose decode verdict is already final).  psi commutes with h_eff and
@@ -319,11 +313,13 @@ __global__ void __launch_bounds__(256) k_hash_to_g2_raw(size_t n, const uint64_t
 // same soundness as a uniform 64-bit r_i, at half the doublings.  R_i is affine
 // here (k_g2_batch_affine ran on the pre-cofactor hash points; (0, 0) marks
 // the identity).  2n threads: j < n computes P_j, j >= n computes S_{j-n}.
-__global__ void __launch_bounds__(256) k_rlc_leaves(size_t n, const uint64_t* __restrict__ rounds, uint64_t seed,
-                                                     const uint32_t* __restrict__ r_aff,
-                                                     const uint32_t* __restrict__ sig_pts,
-                                                     const uint8_t* __restrict__ status, uint32_t* __restrict__ p_out,
-                                                     uint32_t* __restrict__ s_out) {
+// Two waves per SIMD with psi(q) recomputed at its digits measured fastest
+// (1 or 3 waves, or psi(q) held live: 120 vs 123-157 ms per 1M rounds).
+__global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, const uint64_t* __restrict__ rounds,
+                                                            uint64_t seed, const uint32_t* __restrict__ r_aff,
+                                                            const uint32_t* __restrict__ sig_pts,
+                                                            const uint8_t* __restrict__ status,
+                                                            uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= 2 * n) return;
   const bool sig = j >= n;
@@ -333,7 +329,7 @@ __global__ void __launch_bounds__(256) k_rlc_leaves(size_t n, const uint64_t* __
     const g2a q = ld_g2a(sig ? sig_pts : r_aff, n, i);
     if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) {
       const uint64_t z = rlc_coeff(seed, rounds[i]);
-      acc = g2_mul2_naf32_affine(q, g2a_psi(q), (uint32_t)z, (uint32_t)(z >> 32));
+      acc = g2_mul2_naf32_affine<true>(q, q, (uint32_t)z, (uint32_t)(z >> 32));
     }
   }
   st_g2j(sig ? s_out : p_out, n, i, acc);

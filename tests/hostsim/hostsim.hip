@@ -221,12 +221,13 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
     // coefficient, joint NAF ladder), checked against plain double-and-add
     const uint32_t a = (uint32_t)z, b = (uint32_t)(z >> 32);
     const g2a Ra = g2_to_affine(R);
-    g2j rR = g2_mul2_naf32_affine(Ra, g2a_psi(Ra), a, b);
+    g2j rR = g2_mul2_naf32_affine<true>(Ra, Ra, a, b);
     if (!g2_eq(rR, g2_add(g2_mul_words(R, &a, 1), g2_mul_words(g2_psi(R), &b, 1)))) return -3;
+    if (!g2_eq(rR, g2_mul2_naf32_affine<false>(Ra, g2a_psi(Ra), a, b))) return -5;
     const uint32_t kw[2] = {a, b};
     if (!g2_eq(g2_mul64_naf_affine(Ra, z), g2_mul_words(R, kw, 2))) return -4;
     P = g2_add(P, rR);
-    S = g2_add(S, g2_mul2_naf32_affine(s, g2a_psi(s), a, b));
+    S = g2_add(S, g2_mul2_naf32_affine<true>(s, s, a, b));
   }
   g2a Pa = g2_to_affine(g2_clear_cofactor(P)), Sa = g2_to_affine(S);
   fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);

@@ -70,11 +70,20 @@ inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && s
 // rounds per pairing-engine chunk: the line buffer takes 45.7 KB per round (6 GB at 128Ki)
 constexpr size_t ENG_CHUNK = 131072;
 
+// Per-round G2 path scratch of one "lane" (a stream working on a contiguous
+// slice of the batch).  Two lanes overlap one slice's register-bound hash /
+// decode kernels with the other slice's LDS-bound pairing engine.
+struct lane_bufs {
+  DevBuf *h_pts, *sig_pts, *h_z, *h_pre, *h_tmp, *lines, *f, *n1;
+};
+
 }  // namespace
 
 struct dgpu_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // second lane of the per-round G2 path
+  hipEvent_t lane_ev[2] = {nullptr, nullptr};
   std::mutex mu;
   bool have_key = false;
   int key_scheme = -1;
@@ -87,6 +96,9 @@ struct dgpu_ctx {
   DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st;
   // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
   DevBuf eng_consts, eng_lines, eng_f, eng_n1, eng_pre;
+  // second lane's scratch (same roles as h_pts .. eng_n1)
+  DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1;
+  int lanes = 2;  // DGPU_LANES=1: one stream (A/B)
   bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
   int grp_t = 0, grp_n = 0;
@@ -173,7 +185,12 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->device = device;
   const char* pm = getenv("DGPU_PAIRING");
   c->legacy_pairing = pm && !strcmp(pm, "legacy");
+  const char* lv = getenv("DGPU_LANES");
+  if (lv && !strcmp(lv, "1")) c->lanes = 1;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[1], hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
     return set_err(DGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -191,12 +208,17 @@ void dgpu_close(dgpu_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  if (c->stream2) hipStreamSynchronize(c->stream2);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
+  for (hipEvent_t e : c->lane_ev)
+    if (e) hipEventDestroy(e);
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
                     &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->rec_sel, &c->rec_part, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
-                    &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc})
+                    &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc, &c->l2_h_pts, &c->l2_sig_pts,
+                    &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp, &c->l2_lines, &c->l2_f, &c->l2_n1})
     b->release();
-  hipStreamDestroy(c->stream);
+  if (c->stream2) hipStreamDestroy(c->stream2);
+  if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -237,7 +259,8 @@ int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
 
 static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
                               hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
-                              const uint32_t* pk_items = nullptr, const uint32_t* fixed_table = nullptr);
+                              const uint32_t* pk_items = nullptr, const uint32_t* fixed_table = nullptr,
+                              const lane_bufs* L = nullptr);
 
 // RLC batch verification with exact per-round verdicts (mode DGPU_MODE_RLC).
 // 1. R_i = pre-cofactor H(m_i) (Jacobian), sig_i decoded (+ subgroup), status.
@@ -371,18 +394,21 @@ static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uin
 // final exponentiation.  Decode verdicts in `st` stay final.
 static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
                               hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
-                              const uint32_t* fixed_table) {
+                              const uint32_t* fixed_table, const lane_bufs* L) {
   if (!h_stride) h_stride = n;
   const size_t cap = std::min<size_t>(n, ENG_CHUNK);
   const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
+  DevBuf* b_lines = L ? L->lines : &c->eng_lines;
+  DevBuf* b_f = L ? L->f : &c->eng_f;
+  DevBuf* b_n1 = L ? L->n1 : &c->eng_n1;
   int rc;
-  if ((rc = c->eng_lines.ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
-  if ((rc = c->eng_f.ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
-  if ((rc = c->eng_n1.ensure(cap * FP_LIMBS * 4))) return rc;
+  if ((rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
+  if ((rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
+  if ((rc = b_n1->ensure(cap * FP_LIMBS * 4))) return rc;
   const uint32_t* consts = (const uint32_t*)c->eng_consts.p;
-  uint32_t* lines = (uint32_t*)c->eng_lines.p;
-  uint32_t* f = (uint32_t*)c->eng_f.p;
-  uint32_t* n1 = (uint32_t*)c->eng_n1.p;
+  uint32_t* lines = (uint32_t*)b_lines->p;
+  uint32_t* f = (uint32_t*)b_f->p;
+  uint32_t* n1 = (uint32_t*)b_n1->p;
   for (size_t r0 = 0; r0 < n; r0 += cap) {
     const size_t cnt = std::min(cap, n - r0);
     const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
@@ -493,6 +519,41 @@ static int verify_g1_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d
   return DGPU_OK;
 }
 
+// Per-round G2 path, first half of one lane: hash-to-G2 (field, SSWU, finish),
+// batch affine, signature decode of `n` rounds into the lane's buffers.
+static int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const uint64_t* d_rounds,
+                               const uint8_t* d_sigs, size_t sig_stride, const uint32_t* d_sig_len,
+                               const uint8_t* d_prev, size_t prev_stride, const uint32_t* d_prev_len, bool chained,
+                               uint8_t* st, hipStream_t s) {
+  const unsigned B = 256;
+  int rc;
+  if ((rc = L.h_pts->ensure(n * G2A_WORDS * 4)) || (rc = L.sig_pts->ensure(n * G2A_WORDS * 4)) ||
+      (rc = L.h_z->ensure(n * 2 * FP_WORDS * 4)) || (rc = L.h_pre->ensure(n * FP_WORDS * 4)) ||
+      (rc = L.h_tmp->ensure(n * (4 + 12) * FP_WORDS * 4)))
+    return rc;
+  uint32_t* h = (uint32_t*)L.h_pts->p;
+  uint32_t* sg = (uint32_t*)L.sig_pts->p;
+  uint32_t* u = (uint32_t*)L.h_tmp->p;
+  uint32_t* q = u + 4 * FP_WORDS * n;
+  mark(c, s, "hash_to_g2");
+  hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride, d_prev_len,
+                     chained ? 1 : 0, u);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
+                     (uint32_t*)L.h_z->p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "h_affine");
+  hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
+                     (const uint32_t*)L.h_z->p, (uint32_t*)L.h_pre->p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "decode_g2");
+  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
+  HIP_TRY(hipGetLastError());
+  return DGPU_OK;
+}
+
 static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
                                 size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev,
                                 size_t prev_stride, const uint32_t* d_prev_len, int mode, uint64_t rlc_seed,
@@ -513,45 +574,53 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
   if (!d_rounds || !d_sigs || !d_sig_len || !d_bits || sig_stride < 96) return set_err(DGPU_EINVAL, "bad buffers");
   if (chained && (!d_prev || !d_prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
   int rc;
-  if ((rc = c->h_pts.ensure(n * G2A_WORDS * 4))) return rc;
-  if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
   if ((rc = c->status.ensure(n))) return rc;
-  uint32_t* h = (uint32_t*)c->h_pts.p;
-  uint32_t* sg = (uint32_t*)c->sig_pts.p;
   uint8_t* st = (uint8_t*)c->status.p;
   const unsigned B = 256;
   c->n_ev = 0;
   if (mode == DGPU_MODE_RLC) {
+    if ((rc = c->h_pts.ensure(n * G2A_WORDS * 4))) return rc;
+    if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
     rc = rlc_locked(c, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len, chained, rlc_seed,
                     s);
     if (rc) return rc;
   } else {
-    mark(c, s, "hash_to_g2");
-    if ((rc = c->h_z.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4)) ||
-        (rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4)))
+    const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z, &c->h_pre, &c->h_tmp, &c->eng_lines, &c->eng_f, &c->eng_n1};
+    const lane_bufs L1{&c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp, &c->l2_lines, &c->l2_f,
+                       &c->l2_n1};
+    // Two lanes (streams) on the two halves of the batch once it spans more
+    // than one engine chunk; lane 1 starts when lane 0's hash/decode kernels
+    // are done, so its register-bound hash runs beside lane 0's LDS-bound
+    // engine.  Profiled passes stay on one stream (clean per-kernel times).
+    const bool two = c->lanes > 1 && !c->profile && !c->legacy_pairing && n >= 2 * ENG_CHUNK;
+    const size_t n0 = two ? ((n / 2 + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
+    if ((rc = g2_lane_hash_locked(c, L0, n0, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len,
+                                  chained, st, s)))
       return rc;
-    uint32_t* u = (uint32_t*)c->h_tmp.p;
-    uint32_t* q = u + 4 * FP_WORDS * n;
-    hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride, d_prev_len,
-                       chained ? 1 : 0, u);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
-                       (uint32_t*)c->h_z.p);
-    HIP_TRY(hipGetLastError());
-    mark(c, s, "h_affine");
-    hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
-                       (const uint32_t*)c->h_z.p, (uint32_t*)c->h_pre.p);
-    HIP_TRY(hipGetLastError());
-    mark(c, s, "decode_g2");
-    hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
-    HIP_TRY(hipGetLastError());
-    if (c->legacy_pairing) {
+    if (two) {
+      const size_t n1 = n - n0;
+      hipStream_t s2 = c->stream2;
+      HIP_TRY(hipEventRecord(c->lane_ev[0], s));
+      HIP_TRY(hipStreamWaitEvent(s2, c->lane_ev[0], 0));
+      if ((rc = eng_pairing_locked(c, n0, (const uint32_t*)L0.h_pts->p, (const uint32_t*)L0.sig_pts->p, st, s, 0,
+                                   nullptr, nullptr, nullptr, &L0)))
+        return rc;
+      if ((rc = g2_lane_hash_locked(c, L1, n1, d_rounds + n0, d_sigs + n0 * sig_stride, sig_stride, d_sig_len + n0,
+                                    chained ? d_prev + n0 * prev_stride : nullptr, prev_stride,
+                                    chained ? d_prev_len + n0 : nullptr, chained, st + n0, s2)))
+        return rc;
+      if ((rc = eng_pairing_locked(c, n1, (const uint32_t*)L1.h_pts->p, (const uint32_t*)L1.sig_pts->p, st + n0, s2,
+                                   0, nullptr, nullptr, nullptr, &L1)))
+        return rc;
+      HIP_TRY(hipEventRecord(c->lane_ev[1], s2));
+      HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
+    } else if (c->legacy_pairing) {
       mark(c, s, "pairing_check");
-      hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, h, sg, st, c->pk);
+      hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)c->h_pts.p,
+                         (const uint32_t*)c->sig_pts.p, st, c->pk);
       HIP_TRY(hipGetLastError());
-    } else if ((rc = eng_pairing_locked(c, n, h, sg, st, s))) {
+    } else if ((rc = eng_pairing_locked(c, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
+                                        nullptr, nullptr, nullptr, &L0))) {
       return rc;
     }
   }

@@ -170,3 +170,46 @@ def test_rlc_mode_large_chain(chained):
     expect = np.ones(len(c), dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(per == 0, expect)
+
+
+def test_two_lane_per_round_large_chain():
+    """A batch spanning two engine chunks runs on two lanes (streams, half the
+    batch each, capi.hip verify_device_locked): 2*131072 + 1001 rounds (odd
+    split), 0.1% corrupted -- reasons equal the one-lane context's
+    (DGPU_LANES=1) and the construction."""
+    import os
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 2 * 131072 + 1001
+    c = make_chain(13, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 13, rate=1e-3)
+
+    def run(lanes):
+        old = os.environ.get("DGPU_LANES")
+        os.environ["DGPU_LANES"] = lanes
+        try:
+            ctx = _lib.Context(0)
+        finally:
+            if old is None:
+                del os.environ["DGPU_LANES"]
+            else:
+                os.environ["DGPU_LANES"] = old
+        try:
+            lib = ctx.lib
+            _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, c.pk, len(c.pk)))
+            bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+            reason = np.zeros(n, dtype=np.uint8)
+            _lib.check(lib.dgpu_verify_batch(ctx.handle, _lib.SCHEME_CHAINED, n, _lib.ptr(c.rounds),
+                                             _lib.ptr(c.sigs), c.sigs.shape[1], _lib.ptr(c.sig_len),
+                                             _lib.ptr(c.prev), c.prev.shape[1], _lib.ptr(c.prev_len),
+                                             _lib.MODE_PER_ROUND, 0, _lib.ptr(bits), _lib.ptr(reason)))
+            assert np.array_equal(np.unpackbits(bits, bitorder="little")[:n].astype(bool), reason == 0)
+            return reason
+        finally:
+            ctx.close()
+
+    two, one = run("2"), run("1")
+    assert two.tolist() == one.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(two == 0, expect)

@@ -75,7 +75,9 @@ int dgpu_abi_version(void);
 const char *dgpu_last_error(void);
 
 /* Open device `device` (HIP ordinal).  Replaces nothing in the reference: the
- * Go side would hold one context per GPU inside crypto/gpu.BatchVerifier. */
+ * Go side would hold one context per GPU inside crypto/gpu.BatchVerifier.
+ * Read once here: DGPU_LANES=1 keeps large per-round G2 batches on one stream
+ * (default: two streams over the batch halves; verdicts are identical). */
 int dgpu_open(int device, dgpu_ctx **out);
 void dgpu_close(dgpu_ctx *ctx);
 

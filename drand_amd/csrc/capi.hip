@@ -99,6 +99,7 @@ struct dgpu_ctx {
   // second lane's scratch (same roles as h_pts .. eng_n1)
   DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1;
   int lanes = 2;  // DGPU_LANES=1: one stream (A/B)
+  bool fused_fixed = true;  // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
   int grp_t = 0, grp_n = 0;
@@ -187,6 +188,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->legacy_pairing = pm && !strcmp(pm, "legacy");
   const char* lv = getenv("DGPU_LANES");
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
+  const char* gl = getenv("DGPU_G1_LINES");
+  if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
@@ -412,7 +415,12 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
   for (size_t r0 = 0; r0 < n; r0 += cap) {
     const size_t cnt = std::min(cap, n - r0);
     const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
-    if (fixed_table) {  // on-G1: h and sg are affine G1 points, the G2 arguments fixed
+    if (fixed_table && c->fused_fixed) {  // on-G1, lines formed inside the Miller kernel
+      mark(c, s, "eng_miller");
+      hipLaunchKernelGGL(k_eng_miller_fixed, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, consts, h, sg,
+                         fixed_table, f, n1);
+      HIP_TRY(hipGetLastError());
+    } else if (fixed_table) {  // on-G1: h and sg are affine G1 points, the G2 arguments fixed
       mark(c, s, "eng_lines_fixed");
       hipLaunchKernelGGL(k_eng_lines_fixed, dim3(blocks, ENG_LINE_STEPS), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, sg,
                          fixed_table, lines);
@@ -421,10 +429,12 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
       hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
                          pk_items, consts, lines);
     }
-    HIP_TRY(hipGetLastError());
-    mark(c, s, "eng_miller");
-    hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
-    HIP_TRY(hipGetLastError());
+    if (!(fixed_table && c->fused_fixed)) {
+      HIP_TRY(hipGetLastError());
+      mark(c, s, "eng_miller");
+      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
+      HIP_TRY(hipGetLastError());
+    }
     const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
     mark(c, s, "eng_inv");
     hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, lines, st);

@@ -89,9 +89,15 @@ struct eng_io {
   uint32_t* fbuf;    // blocked, 2 planes of 12 components (f / t, then t2)
   uint32_t* n1;      // [limb][cnt]
   size_t cnt;
+  const uint32_t* table = nullptr;  // FIXED: on-G1 line table (k_eng_lines_fixed's layout)
+  fp mlt{};                         // FIXED: this lane's export multiplier (P coordinate)
+  bool scale = false;               // FIXED: export L.k is linear in a P coordinate
 };
 
 // The program interpreter (one inlined copy of the op interpreter per kernel).
+// FIXED: LDLINE reads the per-key line table and scales it by the lane's P
+// coordinate (the on-G1 lines, computed in place of k_eng_lines_fixed).
+template <bool FIXED = false>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
@@ -109,7 +115,13 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     } else if (opc == ENG_OPC_STEP) {
       ++step;
     } else if (opc == ENG_OPC_LDLINE) {
-      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, L.k)));
+      if constexpr (FIXED) {
+        fp v = ld_blk(io.table, (size_t)step * FP_LIMBS * ENG_WAVE_WORDS + L.k);
+        if (io.scale) v = fp_mul(v, io.mlt);
+        eng_st(g + (a + L.k) * ENG_SLOT_WORDS, v);
+      } else {
+        eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, L.k)));
+      }
       ++step;
     } else if (opc == ENG_OPC_LD12) {
       eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k)));
@@ -270,6 +282,38 @@ __global__ void __launch_bounds__(64) k_eng_lines_fixed(size_t n, size_t r0, siz
     v = fp_mul(v, (pair && k >= 4) ? fp_neg(c) : c);
   }
   st_blk(lines, (((size_t)blockIdx.x * ENG_LINE_STEPS + step) * FP_LIMBS) * ENG_WAVE_WORDS + lane, v);
+}
+
+// ---------------------------------------------------------------- k_eng_miller_fixed
+// On-G1 Miller loop with the fixed-Q lines formed at each LDLINE from the
+// per-key table (same scaling as k_eng_lines_fixed: export e = 6 pair + k,
+// k in 2..3 scaled by -x, k in 4..5 by y of P0 = H_i / P1 = -sig_i), so the
+// 45.7 KB/round line buffer is neither written nor read.
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller_fixed(size_t n, size_t r0, size_t cnt,
+                                                                const uint32_t* __restrict__ consts,
+                                                                const uint32_t* __restrict__ h_pts,
+                                                                const uint32_t* __restrict__ s_pts,
+                                                                const uint32_t* __restrict__ table,
+                                                                uint32_t* __restrict__ fbuf,
+                                                                uint32_t* __restrict__ n1) {
+  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS];
+  uint32_t* c = lds;
+  eng_load_consts(c, consts);
+  const eng_lane L = eng_lane_id(cnt);
+  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS;
+  eng_io io{nullptr, fbuf, n1, cnt};
+  io.table = table;
+  const int pair = L.k / 6, k = L.k % 6;
+  io.scale = k >= 2;
+  if (io.scale) {
+    const uint32_t* pts = pair ? s_pts : h_pts;
+    const fp cc = k < 4 ? fp_neg(ld_fp(pts, n, r0 + L.i)) : ld_fp(pts + FP_WORDS * n, n, r0 + L.i);
+    io.mlt = (pair && k >= 4) ? fp_neg(cc) : cc;
+  }
+  eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
+  asm volatile("" ::: "memory");
+  eng_exec<true>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, io);
+  if (L.valid) st_blk(fbuf, eng_blk_off(2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 
 }  // namespace dgpu

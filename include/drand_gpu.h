@@ -77,7 +77,9 @@ const char *dgpu_last_error(void);
 /* Open device `device` (HIP ordinal).  Replaces nothing in the reference: the
  * Go side would hold one context per GPU inside crypto/gpu.BatchVerifier.
  * Read once here: DGPU_LANES=1 keeps large per-round G2 batches on one stream
- * (default: two streams over the batch halves; verdicts are identical). */
+ * (default: two streams over the batch halves; verdicts are identical), and
+ * DGPU_G1_LINES=buffer runs the on-G1 fixed-Q lines through a line buffer
+ * (default: formed inside the Miller kernel; verdicts are identical). */
 int dgpu_open(int device, dgpu_ctx **out);
 void dgpu_close(dgpu_ctx *ctx);
 
@@ -127,7 +129,8 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
  * stage durations (ms) and names of the last call, summed per name over
  * chunks (per-round mode: hash_to_g2, h_affine, decode_g2, eng_lines,
  * eng_miller, eng_inv, eng_fe, pack_verdicts; G1 signatures: hash_to_g1,
- * h_affine, decode_g1, eng_lines_fixed, ...; RLC mode: rlc_hash_to_g2_raw,
+ * h_affine, decode_g1, eng_miller (eng_lines_fixed first under
+ * DGPU_G1_LINES=buffer), ...; RLC mode: rlc_hash_to_g2_raw,
  * decode_g2, rlc_leaves_tree, rlc_prep and the engine stages of the node
  * checks, rlc_bisection; recovery: recover_hash, recover_decode, engine
  * stages, recover_msm, recover_verdict) and returns the number written. */

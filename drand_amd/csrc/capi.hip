@@ -67,8 +67,13 @@ inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + bloc
 inline bool sig_on_g1(int scheme) { return scheme == DGPU_SCHEME_UNCHAINED_G1 || scheme == DGPU_SCHEME_G1_RFC9380; }
 inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && scheme <= DGPU_SCHEME_G1_RFC9380; }
 
-// rounds per pairing-engine chunk: the line buffer takes 45.7 KB per round (6 GB at 128Ki)
-constexpr size_t ENG_CHUNK = 131072;
+// rounds per pairing-engine chunk: the line buffer takes 45.7 KB per round
+// (24 GB at 512Ki, per lane).  r01u A/B at 1M rounds: 64Ki 1.333M, 128Ki 1.362M,
+// 256Ki 1.383M, 512Ki 1.394M rounds/s (fewer launch tails, one inversion
+// thread per 64 rounds of a larger chunk).
+constexpr size_t ENG_CHUNK = 524288;
+// per-round G2 batches of at least this many rounds run on two lanes
+constexpr size_t LANE_MIN = 262144;
 
 // Per-round G2 path scratch of one "lane" (a stream working on a contiguous
 // slice of the batch).  Two lanes overlap one slice's register-bound hash /
@@ -99,6 +104,7 @@ struct dgpu_ctx {
   // second lane's scratch (same roles as h_pts .. eng_n1)
   DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1;
   int lanes = 2;  // DGPU_LANES=1: one stream (A/B)
+  size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds>: engine chunk size (A/B)
   bool fused_fixed = true;  // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
@@ -188,6 +194,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->legacy_pairing = pm && !strcmp(pm, "legacy");
   const char* lv = getenv("DGPU_LANES");
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
+  const char* ec = getenv("DGPU_ENG_CHUNK");
+  if (ec && atol(ec) >= 4096) c->eng_chunk = (size_t)atol(ec);
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
@@ -399,7 +407,7 @@ static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const ui
                               hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
                               const uint32_t* fixed_table, const lane_bufs* L) {
   if (!h_stride) h_stride = n;
-  const size_t cap = std::min<size_t>(n, ENG_CHUNK);
+  const size_t cap = std::min<size_t>(n, c->eng_chunk);
   const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
   DevBuf* b_lines = L ? L->lines : &c->eng_lines;
   DevBuf* b_f = L ? L->f : &c->eng_f;
@@ -602,7 +610,7 @@ static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_
     // than one engine chunk; lane 1 starts when lane 0's hash/decode kernels
     // are done, so its register-bound hash runs beside lane 0's LDS-bound
     // engine.  Profiled passes stay on one stream (clean per-kernel times).
-    const bool two = c->lanes > 1 && !c->profile && !c->legacy_pairing && n >= 2 * ENG_CHUNK;
+    const bool two = c->lanes > 1 && !c->profile && !c->legacy_pairing && n >= LANE_MIN;
     const size_t n0 = two ? ((n / 2 + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
     if ((rc = g2_lane_hash_locked(c, L0, n0, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len,
                                   chained, st, s)))

@@ -176,7 +176,8 @@ def test_two_lane_per_round_large_chain():
     """A batch spanning two engine chunks runs on two lanes (streams, half the
     batch each, capi.hip verify_device_locked): 2*131072 + 1001 rounds (odd
     split), 0.1% corrupted -- reasons equal the one-lane context's
-    (DGPU_LANES=1) and the construction."""
+    (DGPU_LANES=1, 64Ki-round engine chunks: five chunks) and the
+    construction."""
     import os
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
@@ -184,16 +185,17 @@ def test_two_lane_per_round_large_chain():
     c = make_chain(13, n, _lib.SCHEME_CHAINED, seg_len=64)
     bad = corrupt(c, 13, rate=1e-3)
 
-    def run(lanes):
-        old = os.environ.get("DGPU_LANES")
-        os.environ["DGPU_LANES"] = lanes
+    def run(env):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         try:
             ctx = _lib.Context(0)
         finally:
-            if old is None:
-                del os.environ["DGPU_LANES"]
-            else:
-                os.environ["DGPU_LANES"] = old
+            for k, v in saved.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
         try:
             lib = ctx.lib
             _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, c.pk, len(c.pk)))
@@ -208,7 +210,7 @@ def test_two_lane_per_round_large_chain():
         finally:
             ctx.close()
 
-    two, one = run("2"), run("1")
+    two, one = run({"DGPU_LANES": "2"}), run({"DGPU_LANES": "1", "DGPU_ENG_CHUNK": "65536"})
     assert two.tolist() == one.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False

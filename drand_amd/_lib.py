@@ -57,7 +57,24 @@ SYMBOLS = [
     ("dgpu_recover_batch_device", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P, _P]),
     ("dgpu_make_partials", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _c.c_size_t, _P]),
     ("dgpu_recover_batch", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P]),
+    ("dgpu_shard_range", None, [_c.c_size_t, _c.c_int, _c.c_int, _c.POINTER(_c.c_size_t), _c.POINTER(_c.c_size_t)]),
+    ("dgpu_verify_beacons", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P,
+                                       _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P]),
+    ("dgpu_verify_beacons_device", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _c.c_size_t, _P,
+                                              _P, _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P, _P]),
+    ("dgpu_verify_recovered", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _c.c_size_t, _P, _P,
+                                         _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P]),
+    ("dgpu_hash_to_curve", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _c.c_size_t, _P, _P]),
+    ("dgpu_sign", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P]),
+    ("dgpu_decode_g1_points", _c.c_int, [_P, _c.c_size_t, _P, _P, _P]),
+    ("dgpu_multi_open", _c.c_int, [_c.c_int, _P, _c.POINTER(_P)]),
+    ("dgpu_multi_close", None, [_P]),
+    ("dgpu_multi_context", _c.c_int, [_P, _c.c_int, _c.POINTER(_P)]),
+    ("dgpu_verify_multi", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P,
+                                     _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P]),
 ]
+
+ABI_VERSION = 2
 
 
 class DrandGPUError(RuntimeError):
@@ -84,7 +101,7 @@ def load(path=None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.dgpu_abi_version() != 1:
+        if lib.dgpu_abi_version() != ABI_VERSION:
             raise DrandGPUError(DGPU_EINVAL, "ABI version mismatch")
         if path is None:
             _lib = lib
@@ -96,6 +113,14 @@ def check(rc):
         lib = load()
         raise DrandGPUError(rc, lib.dgpu_last_error().decode(errors="replace"))
     return rc
+
+
+def shard_range(n, ndev, k):
+    """dgpu_shard_range: item range [lo, hi) of device k (host-only bookkeeping)."""
+    lib = load()
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    lib.dgpu_shard_range(n, ndev, k, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
 
 
 def ptr(buf):
@@ -122,6 +147,30 @@ class Context:
     def close(self):
         if self.handle:
             self.lib.dgpu_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiContext:
+    """dgpu_multi handle: one context per listed GPU and an RCCL communicator
+    over them (dgpu_multi_open)."""
+
+    def __init__(self, devices):
+        self.lib = load()
+        self.devices = list(devices)
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        check(self.lib.dgpu_multi_open(len(self.devices), arr, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.dgpu_multi_close(self.handle)
             self.handle = None
 
     def __del__(self):

@@ -16,6 +16,7 @@ GPU; constructing a Verifier without the HIP library or a gfx950 device
 raises DrandGPUError.
 """
 import hashlib
+import secrets
 import struct
 import threading
 from dataclasses import dataclass
@@ -103,15 +104,26 @@ def pack_beacons(beacons, sig_stride=96, prev_stride=None):
     return rounds, sigs, sig_len, prev, prev_len
 
 
+def rlc_seed_for(mode, rlc_seed):
+    """RLC coefficients must be unpredictable to whoever produced the
+    beacons: without an explicit seed, RLC mode draws a fresh 64-bit one per
+    call (a known seed lets an attacker choose corruptions that cancel)."""
+    if mode == _lib.MODE_RLC and rlc_seed is None:
+        return secrets.randbits(64)
+    return 0 if rlc_seed is None else int(rlc_seed)
+
+
 class Verifier:
     """chain.Verifier (chain/verify.go:13-20): stateless apart from the scheme;
-    safe for concurrent use (the GPU context serializes)."""
+    safe for concurrent use (the GPU context serializes).  The public key is
+    passed per call, like VerifyBeacon(b, pubkey) (chain/verify.go:38); the
+    context caches decoded keys, so verifiers of different chains and schemes
+    can share one GPU context."""
 
     def __init__(self, scheme: Scheme, device=0):
         self.scheme = scheme
         self.ctx = get_context(device)
         self._code = scheme_code(scheme)
-        self._pk_loaded = None
 
     def is_prev_sig_meaningful(self):
         """chain/verify.go:47-49"""
@@ -137,29 +149,24 @@ class Verifier:
                                          _lib.ptr(plen), _lib.ptr(out)))
         return [bytes(row) for row in out]
 
-    def _set_key(self, pubkey):
-        if self._pk_loaded != pubkey:
-            _lib.check(self.ctx.lib.dgpu_set_pubkey(self.ctx.handle, self._code, pubkey, len(pubkey)))
-            self._pk_loaded = pubkey
-
-    def verify_beacons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=0):
+    def verify_beacons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=None):
         """Batch VerifyBeacon: returns a list of (None | VerifyError), one per beacon."""
         reasons = self.verify_reasons(beacons, pubkey, mode, rlc_seed)
         return [None if r == _lib.REASON_OK else VerifyError(b.round, int(r)) for b, r in zip(beacons, reasons)]
 
-    def verify_reasons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=0):
+    def verify_reasons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=None):
         n = len(beacons)
         if n == 0:
             return np.zeros(0, dtype=np.uint8)
         rounds, sigs, sig_len, prev, prev_len = pack_beacons(beacons)
         bits = np.zeros((n + 7) // 8, dtype=np.uint8)
         reason = np.zeros(n, dtype=np.uint8)
+        pk = np.frombuffer(bytes(pubkey), dtype=np.uint8).copy()
         lib = self.ctx.lib
-        with _ctx_lock:
-            self._set_key(pubkey)
-            _lib.check(lib.dgpu_verify_batch(self.ctx.handle, self._code, n, _lib.ptr(rounds), _lib.ptr(sigs),
-                                             sigs.shape[1], _lib.ptr(sig_len), _lib.ptr(prev), prev.shape[1],
-                                             _lib.ptr(prev_len), mode, rlc_seed, _lib.ptr(bits), _lib.ptr(reason)))
+        _lib.check(lib.dgpu_verify_beacons(self.ctx.handle, self._code, _lib.ptr(pk), pk.size, n, _lib.ptr(rounds),
+                                           _lib.ptr(sigs), sigs.shape[1], _lib.ptr(sig_len), _lib.ptr(prev),
+                                           prev.shape[1], _lib.ptr(prev_len), mode, rlc_seed_for(mode, rlc_seed),
+                                           _lib.ptr(bits), _lib.ptr(reason)))
         valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
         if not np.array_equal(valid, reason == _lib.REASON_OK):
             raise _lib.DrandGPUError(_lib.DGPU_EINVAL, "verdict bitmap and reasons disagree")
@@ -176,6 +183,89 @@ class Verifier:
 def new_verifier(scheme: Scheme, device=0):
     """chain.NewVerifier (chain/verify.go:18-20)."""
     return Verifier(scheme, device)
+
+
+def _pack_msgs(msgs):
+    n = len(msgs)
+    stride = max([1] + [len(m) for m in msgs])
+    buf = np.zeros((n, stride), dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint32)
+    for i, m in enumerate(msgs):
+        if m:
+            buf[i, : len(m)] = np.frombuffer(bytes(m), dtype=np.uint8)
+        lens[i] = len(m)
+    return buf, lens
+
+
+def verify_recovered(scheme: Scheme, pubkey, msgs, sigs, mode=_lib.MODE_PER_ROUND, rlc_seed=None, device=0):
+    """Batch key.Scheme.VerifyRecovered(pk, msg, sig) (chain/verify.go:44,
+    chain/beacon/chain.go:165; kyber bls.Verify (R)) over raw messages of any
+    length.  Returns the DGPU_REASON_* code per message (0 = valid)."""
+    ctx = get_context(device)
+    n = len(msgs)
+    if n == 0:
+        return np.zeros(0, dtype=np.uint8)
+    mb, ml = _pack_msgs(msgs)
+    sb, sl = _pack_msgs(sigs)
+    width = 48 if scheme_code(scheme) in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380) else 96
+    if sb.shape[1] < width:
+        sb = np.pad(sb, ((0, 0), (0, width - sb.shape[1])))
+    pk = np.frombuffer(bytes(pubkey), dtype=np.uint8).copy()
+    bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+    reason = np.zeros(n, dtype=np.uint8)
+    _lib.check(ctx.lib.dgpu_verify_recovered(ctx.handle, scheme_code(scheme), _lib.ptr(pk), pk.size, n, _lib.ptr(mb),
+                                             mb.shape[1], _lib.ptr(ml), _lib.ptr(sb), sb.shape[1], _lib.ptr(sl), mode,
+                                             rlc_seed_for(mode, rlc_seed), _lib.ptr(bits), _lib.ptr(reason)))
+    return reason
+
+
+def hash_to_curve(msgs, scheme: Scheme = None, device=0):
+    """Hash raw messages of any length to the scheme's signature group
+    (compressed: 96-byte G2 under drand's DST, 48-byte G1 for the G1 schemes)."""
+    from .scheme import get_scheme_by_id_with_default
+    code = scheme_code(scheme or get_scheme_by_id_with_default(""))
+    ctx = get_context(device)
+    n = len(msgs)
+    mb, ml = _pack_msgs(msgs)
+    width = 48 if code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380) else 96
+    out = np.zeros(n * width, dtype=np.uint8)
+    if n:
+        _lib.check(ctx.lib.dgpu_hash_to_curve(ctx.handle, code, n, _lib.ptr(mb), mb.shape[1], _lib.ptr(ml),
+                                              _lib.ptr(out)))
+    return [bytes(out[i * width:(i + 1) * width]) for i in range(n)]
+
+
+def sign(secret, msgs, scheme: Scheme = None, device=0):
+    """key.Scheme.Sign / AuthScheme.Sign (key/curve.go:36-39) of raw messages
+    with a secret scalar (int or 32 big-endian bytes): test/tool surface."""
+    from .scheme import get_scheme_by_id_with_default
+    code = scheme_code(scheme or get_scheme_by_id_with_default(""))
+    ctx = get_context(device)
+    sk = secret.to_bytes(32, "big") if isinstance(secret, int) else bytes(secret)
+    skb = np.frombuffer(sk, dtype=np.uint8).copy()
+    n = len(msgs)
+    mb, ml = _pack_msgs(msgs)
+    width = 48 if code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380) else 96
+    out = np.zeros(n * width, dtype=np.uint8)
+    if n:
+        _lib.check(ctx.lib.dgpu_sign(ctx.handle, code, _lib.ptr(skb), n, _lib.ptr(mb), mb.shape[1], _lib.ptr(ml),
+                                     _lib.ptr(out)))
+    return [bytes(out[i * width:(i + 1) * width]) for i in range(n)]
+
+
+def decode_g1_points(points, device=0):
+    """Batch G1 decode (KeyGroup.Point().UnmarshalBinary, chain/convert.go:20-23):
+    returns (rc list, [(x, y) ints or None])."""
+    ctx = get_context(device)
+    n = len(points)
+    buf = np.frombuffer(b"".join(bytes(p) for p in points), dtype=np.uint8).copy()
+    rc = np.zeros(n, dtype=np.int32)
+    xy = np.zeros(n * 96, dtype=np.uint8)
+    if n:
+        _lib.check(ctx.lib.dgpu_decode_g1_points(ctx.handle, n, _lib.ptr(buf), _lib.ptr(rc), _lib.ptr(xy)))
+    coords = [(int.from_bytes(bytes(xy[i * 96:i * 96 + 48]), "big"), int.from_bytes(bytes(xy[i * 96 + 48:i * 96 + 96]), "big"))
+              if rc[i] == 0 else None for i in range(n)]
+    return rc.tolist(), coords
 
 
 def hash_to_g2(msgs, device=0):

@@ -1,7 +1,10 @@
 // libdrand_gpu.so: the C-ABI boundary (include/drand_gpu.h) over the gfx950
-// kernels.  Host side of the product path: device memory, streams, launches.
+// kernels.  Host side of the product path: device memory, streams, launches,
+// the per-context key cache and the multi-GPU (RCCL) driver.
 // There is deliberately no CPU fallback anywhere in this file.
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
@@ -9,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/drand_gpu.h"
@@ -40,16 +44,21 @@ int set_err(int code, const char* fmt, ...) {
     if (_e != hipSuccess) return set_err(DGPU_EDEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
   } while (0)
 
-// Grow-only device scratch buffer.
+// Grow-only device scratch buffer.  Growth frees the old allocation only
+// after the device is idle: a kernel enqueued earlier (this call or an
+// earlier asynchronous one) may still read it.
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return DGPU_OK;
-    if (p) hipFree(p);
+    if (p) {
+      hipDeviceSynchronize();
+      hipFree(p);
+    }
     p = nullptr;
     cap = 0;
-    hipError_t e = hipMalloc(&p, bytes);
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
     if (e != hipSuccess) return set_err(DGPU_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
     cap = bytes;
     return DGPU_OK;
@@ -67,13 +76,19 @@ inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + bloc
 inline bool sig_on_g1(int scheme) { return scheme == DGPU_SCHEME_UNCHAINED_G1 || scheme == DGPU_SCHEME_G1_RFC9380; }
 inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && scheme <= DGPU_SCHEME_G1_RFC9380; }
 
-// rounds per pairing-engine chunk: the line buffer takes 45.7 KB per round
-// (24 GB at 512Ki, per lane).  r01u A/B at 1M rounds: 64Ki 1.333M, 128Ki 1.362M,
-// 256Ki 1.383M, 512Ki 1.394M rounds/s (fewer launch tails, one inversion
-// thread per 64 rounds of a larger chunk).
+// rounds per pairing-engine chunk (upper bound; dgpu_open lowers it to fit a
+// quarter of the free HBM): the line buffer takes 45.7 KB per round (24 GB at
+// 512Ki, per lane).  r01u A/B at 1M rounds: 64Ki 1.333M, 128Ki 1.362M,
+// 256Ki 1.383M, 512Ki 1.394M rounds/s.
 constexpr size_t ENG_CHUNK = 524288;
+constexpr size_t ENG_CHUNK_MIN = 16384;
+// engine bytes per round and lane: line buffer + f planes + N1
+constexpr size_t ENG_BYTES_PER_ROUND =
+    (size_t)ENG_LINE_STEPS * FP_LIMBS * 12 * 4 + 2 * FP_LIMBS * 12 * 4 + FP_LIMBS * 4;
 // per-round G2 batches of at least this many rounds run on two lanes
 constexpr size_t LANE_MIN = 262144;
+// decoded public keys cached per context (chain/verify.go:38 passes the key per call)
+constexpr int KEY_SLOTS = 8;
 
 // Per-round G2 path scratch of one "lane" (a stream working on a contiguous
 // slice of the batch).  Two lanes overlap one slice's register-bound hash /
@@ -82,6 +97,48 @@ struct lane_bufs {
   DevBuf *h_pts, *sig_pts, *h_z, *h_pre, *h_tmp, *lines, *f, *n1;
 };
 
+// One decoded public key: the engine's block constants carry its pairing
+// point; G2 keys (G1-signature schemes) also own the fixed-Q line table.
+struct key_entry {
+  bool used = false;
+  bool g2key = false;
+  uint8_t bytes[96] = {};
+  g1_key pk{};
+  DevBuf consts, table;
+  uint64_t stamp = 0;
+};
+
+// Signature group and message source of one verify call.
+struct verify_args {
+  int scheme;
+  size_t n;
+  msg_src m;
+  const uint8_t* sigs;
+  size_t sig_stride;
+  const uint32_t* sig_len;
+  int mode;
+  uint64_t seed;
+};
+
+msg_src beacon_src(const uint64_t* rounds, const uint8_t* prev, size_t prev_stride, const uint32_t* prev_len,
+                   bool chained) {
+  msg_src m{};
+  m.rounds = rounds;
+  m.chained = chained ? 1 : 0;
+  m.prev = chained ? prev : nullptr;
+  m.prev_stride = chained ? prev_stride : 0;
+  m.prev_len = chained ? prev_len : nullptr;
+  return m;
+}
+
+msg_src raw_src(const uint8_t* msgs, size_t stride, const uint32_t* len) {
+  msg_src m{};
+  m.msgs = msgs;
+  m.msg_stride = stride;
+  m.msg_len = len;
+  return m;
+}
+
 }  // namespace
 
 struct dgpu_ctx {
@@ -89,30 +146,31 @@ struct dgpu_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // second lane of the per-round G2 path
   hipEvent_t lane_ev[2] = {nullptr, nullptr};
+  // end of the last call's enqueued work: every call orders its stream after it
+  hipEvent_t done = nullptr;
   std::mutex mu;
-  bool have_key = false;
-  int key_scheme = -1;
-  g1_key pk{};
-  // on-G1 schemes: the G2 public key and the fixed-Q line table (k_eng_lines_fixed)
-  DevBuf g1_table, g1_aux;
+  key_entry keys[KEY_SLOTS];
+  key_entry* cur = nullptr;  // key installed by dgpu_set_pubkey (dgpu_verify_batch[_device])
+  uint64_t clock = 0;
+  // engine block constants without a key (recovery: per-item keys)
+  DevBuf eng_consts;
   // scratch
   DevBuf h_pts, sig_pts, status, h_z, h_pre, h_tmp;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
-  DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st;
-  // pairing engine (per-round mode): block constants, per-chunk lines / f / norms
-  DevBuf eng_consts, eng_lines, eng_f, eng_n1, eng_pre;
+  DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st, rlc_root;
+  // pairing engine (per-round mode): per-chunk lines / f / norms
+  DevBuf eng_lines, eng_f, eng_n1;
   // second lane's scratch (same roles as h_pts .. eng_n1)
   DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1;
-  int lanes = 2;  // DGPU_LANES=1: one stream (A/B)
-  size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds>: engine chunk size (A/B)
-  bool fused_fixed = true;  // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
-  bool legacy_pairing = false;  // DGPU_PAIRING=legacy: one-thread-per-pairing kernel (A/B only)
+  int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
+  size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
+  bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
   int grp_t = 0, grp_n = 0;
-  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok, rec_pts, rec_vpk, rec_sel, rec_part,
-      rec_st;
+  DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok,
+      rec_pts, rec_vpk, rec_sel, rec_part, rec_st;
   // staging for host-pointer entry points
-  DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, out_bits, out_reason, misc;
+  DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call (event pool;
   // durations are summed per stage name: chunked stages repeat)
   bool profile = false;
@@ -121,9 +179,22 @@ struct dgpu_ctx {
   int n_ev = 0;
 };
 
+namespace {
+
+// Calls on one context are ordered: each entry point makes its stream wait
+// for the previous call's work (which may sit on another stream) and records
+// `done` when it has enqueued its own, so shared scratch is never
+// overwritten mid-flight whatever streams the caller uses.
+struct stream_order {
+  dgpu_ctx* c;
+  hipStream_t s;
+  stream_order(dgpu_ctx* c_, hipStream_t s_) : c(c_), s(s_) { hipStreamWaitEvent(s, c->done, 0); }
+  ~stream_order() { hipEventRecord(c->done, s); }
+};
+
 // Stage markers: mark(c, s, name) records an event that *starts* stage `name`
 // (and ends the previous one); mark(c, s, nullptr) closes the last stage.
-static void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
+void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
   if (!c->profile || c->n_ev >= 1024) return;
   if ((size_t)c->n_ev == c->ev.size()) {
     hipEvent_t e = nullptr;
@@ -137,30 +208,579 @@ static void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
 }
 
 // Engine block constants (slot order of tools/gen_engine.py: ONE, the two
-// pairing points (-x, y) -- the group key (zero until dgpu_set_pubkey) and
-// -g1 --, gamma1_1..5, gamma2_1..5).  unit_points: both points (1, 1), for
-// the on-G1 fixed-line table (written to `dst` instead of the context's block).
-static int upload_eng_consts(dgpu_ctx* c, bool unit_points = false, DevBuf* dst = nullptr) {
+// pairing points (-x, y) -- the key (zero without one) and -g1 --,
+// gamma1_1..5, gamma2_1..5).  unit_points: both points (1, 1), for the on-G1
+// fixed-line table.  Synchronous upload.
+int upload_eng_consts(DevBuf* dst, const g1_key* key, bool unit_points = false) {
   eng_const_block cb;
+  memset(&cb, 0, sizeof cb);
   const fp2 g1c[5] = {C_FROB1_1, C_FROB1_2, C_FROB1_3, C_FROB1_4, C_FROB1_5};
   const fp2 g2c[5] = {C_FROB2_1, C_FROB2_2, C_FROB2_3, C_FROB2_4, C_FROB2_5};
   auto put = [&](int slot, const fp& v) { memcpy(cb.w + (slot - 64) * ENG_SLOT_WORDS, v.l, FP_LIMBS * 4); };
+  const g1_key zero{fp_zero(), fp_zero()};
+  const g1_key& k = key ? *key : zero;
   put(ENG_C_ONE, fp_one());
-  put(ENG_C_NXP0, unit_points ? fp_one() : c->pk.neg_x);
-  put(ENG_C_YP0, unit_points ? fp_one() : c->pk.y);
+  put(ENG_C_NXP0, unit_points ? fp_one() : k.neg_x);
+  put(ENG_C_YP0, unit_points ? fp_one() : k.y);
   put(ENG_C_NXP1, unit_points ? fp_one() : fp_neg(C_G1_X));
   put(ENG_C_YP1, unit_points ? fp_one() : C_G1_NEG_Y);
-  for (int k = 0; k < 5; ++k) {
-    put(ENG_C_G1 + 2 * k, g1c[k].c0);
-    put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
-    put(ENG_C_G2 + k, g2c[k].c0);
+  for (int j = 0; j < 5; ++j) {
+    put(ENG_C_G1 + 2 * j, g1c[j].c0);
+    put(ENG_C_G1 + 2 * j + 1, g1c[j].c1);
+    put(ENG_C_G2 + j, g2c[j].c0);
   }
   int rc;
-  DevBuf* b = dst ? dst : &c->eng_consts;
-  if ((rc = b->ensure(sizeof cb))) return rc;
-  HIP_TRY(hipMemcpy(b->p, &cb, sizeof cb, hipMemcpyHostToDevice));
+  if ((rc = dst->ensure(sizeof cb))) return rc;
+  HIP_TRY(hipMemcpy(dst->p, &cb, sizeof cb, hipMemcpyHostToDevice));
   return DGPU_OK;
 }
+
+// Decode a 48-byte G1 key into e (public-key decode of InfoFromProto,
+// chain/convert.go:20-23); synchronous on the context's stream.
+int decode_g1_key_locked(dgpu_ctx* c, key_entry* e, const uint8_t* pk) {
+  int rc = c->misc.ensure(256);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  uint8_t* d = (uint8_t*)c->misc.p;
+  HIP_TRY(hipMemcpyAsync(d, pk, 48, hipMemcpyHostToDevice, s));
+  uint32_t* d_out = (uint32_t*)(d + 64);
+  int* d_rc = (int*)(d + 64 + 2 * FP_LIMBS * 4);
+  hipLaunchKernelGGL(k_decode_g1_pk, dim3(1), dim3(64), 0, s, d, d_out, d_rc);
+  HIP_TRY(hipGetLastError());
+  uint32_t host[2 * FP_LIMBS + 1];
+  HIP_TRY(hipMemcpyAsync(host, d_out, sizeof host, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int drc = (int)host[2 * FP_LIMBS];
+  if (drc != DEC_OK) return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
+  memcpy(e->pk.neg_x.l, host, FP_LIMBS * 4);
+  memcpy(e->pk.y.l, host + FP_LIMBS, FP_LIMBS * 4);
+  return upload_eng_consts(&e->consts, &e->pk);
+}
+
+// G2 key (on-G1 schemes): decode (subgroup-checked) and compute the fixed-Q
+// line table: the LINES program for (pk, g2) at P = (1, 1).
+int decode_g2_key_locked(dgpu_ctx* c, key_entry* e, const uint8_t* pk) {
+  int rc;
+  const size_t tbl_words = (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS;
+  if ((rc = e->table.ensure(tbl_words * 4)) || (rc = c->misc.ensure(4096))) return rc;
+  if ((rc = upload_eng_consts(&e->consts, nullptr))) return rc;
+  DevBuf unit;
+  if ((rc = upload_eng_consts(&unit, nullptr, true))) return rc;
+  uint8_t* aux = (uint8_t*)c->misc.p;
+  uint32_t* d_pk = (uint32_t*)aux;           // affine G2, stride 1 (224 B)
+  uint32_t* d_g2 = (uint32_t*)(aux + 1024);  // generator, stride 1
+  int* d_rc = (int*)(aux + 2048);
+  uint8_t* d_in = aux + 3072;
+  g2a gen{C_G2_X, C_G2_Y};
+  uint32_t gw[G2A_WORDS];
+  memcpy(gw, gen.x.c0.l, 56);
+  memcpy(gw + 14, gen.x.c1.l, 56);
+  memcpy(gw + 28, gen.y.c0.l, 56);
+  memcpy(gw + 42, gen.y.c1.l, 56);
+  hipStream_t s = c->stream;
+  hipError_t err = hipMemcpyAsync(d_in, pk, 96, hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(d_g2, gw, sizeof gw, hipMemcpyHostToDevice, s);
+  if (err == hipSuccess) {
+    hipLaunchKernelGGL(k_decode_g2_pk, dim3(1), dim3(64), 0, s, d_in, d_pk, d_rc);
+    err = hipGetLastError();
+  }
+  int drc = -1;
+  if (err == hipSuccess) err = hipMemcpyAsync(&drc, d_rc, sizeof drc, hipMemcpyDeviceToHost, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (err != hipSuccess) {
+    unit.release();
+    return set_err(DGPU_EDEVICE, "set_pubkey: %s", hipGetErrorString(err));
+  }
+  if (drc != DEC_OK) {
+    unit.release();
+    return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
+  }
+  hipLaunchKernelGGL(k_eng_lines, dim3(1), dim3(ENG_BLOCK), 0, s, (size_t)1, (size_t)0, (size_t)1,
+                     (const uint32_t*)d_pk, (size_t)1, (const uint32_t*)nullptr, (const uint32_t*)d_g2,
+                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)e->table.p);
+  err = hipGetLastError();
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  unit.release();
+  if (err != hipSuccess) return set_err(DGPU_EDEVICE, "set_pubkey lines: %s", hipGetErrorString(err));
+  return DGPU_OK;
+}
+
+// The cached key entry for (scheme's key group, pk bytes), decoding it into a
+// free or least-recently-used slot on a miss.  Chains, schemes and callers
+// can interleave on one context: nothing key-specific lives outside the
+// entries.
+int get_key_locked(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len, key_entry** out) {
+  if (!pk) return set_err(DGPU_EINVAL, "null public key");
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  const bool g2key = sig_on_g1(scheme);
+  const size_t want = g2key ? 96 : 48;
+  if (len != want)
+    return set_err(DGPU_EINVAL, "public key must be %zu bytes (compressed %s), got %zu", want, g2key ? "G2" : "G1", len);
+  key_entry* victim = nullptr;
+  for (key_entry& e : c->keys) {
+    if (e.used && e.g2key == g2key && !memcmp(e.bytes, pk, want)) {
+      e.stamp = ++c->clock;
+      *out = &e;
+      return DGPU_OK;
+    }
+    if (!victim || (!e.used && victim->used) || (e.used == victim->used && e.stamp < victim->stamp)) victim = &e;
+  }
+  // the victim's buffers may still be read by an earlier asynchronous call
+  HIP_TRY(hipEventSynchronize(c->done));
+  if (c->cur == victim) c->cur = nullptr;
+  victim->used = false;
+  int rc = g2key ? decode_g2_key_locked(c, victim, pk) : decode_g1_key_locked(c, victim, pk);
+  if (rc) return rc;
+  victim->used = true;
+  victim->g2key = g2key;
+  memcpy(victim->bytes, pk, want);
+  victim->stamp = ++c->clock;
+  *out = victim;
+  return DGPU_OK;
+}
+
+int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint32_t* h, const uint32_t* sg,
+                       uint8_t* st, hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
+                       const uint32_t* pk_items = nullptr, const uint32_t* fixed_table = nullptr,
+                       const lane_bufs* L = nullptr);
+
+// ---------------------------------------------------------------- RLC
+// The segment trees of one RLC batch (level l: P[l], S[l], sz[l] nodes).
+struct rlc_trees {
+  std::vector<size_t> sz;
+  std::vector<uint32_t*> P, S;
+  int top() const { return (int)sz.size() - 1; }
+};
+
+// RLC phase 1: R_i = pre-cofactor H(m_i) (affine), sig_i decoded (+ subgroup),
+// leaves P_i = r_i R_i, S_i = r_i sig_i (r_i from the seed and the batch
+// position i), segment tree of sums up to the root.  Asynchronous on s.
+int rlc_build_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+  const unsigned B = 256;
+  const size_t n = a.n;
+  T.sz.assign(1, n);
+  while (T.sz.back() > 1) T.sz.push_back((T.sz.back() + 1) / 2);
+  size_t total = 0;
+  for (size_t v : T.sz) total += v;
+  int rc;
+  if ((rc = c->rlc_tree.ensure(2 * total * G2J_WORDS * 4 + n * G2J_WORDS * 4))) return rc;
+  if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
+  if ((rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
+  uint32_t* tree = (uint32_t*)c->rlc_tree.p;
+  T.P.assign(T.sz.size(), nullptr);
+  T.S.assign(T.sz.size(), nullptr);
+  size_t off = 0;
+  for (size_t l = 0; l < T.sz.size(); ++l) {
+    T.P[l] = tree + off;
+    off += T.sz[l] * G2J_WORDS;
+    T.S[l] = tree + off;
+    off += T.sz[l] * G2J_WORDS;
+  }
+  uint32_t* rpts = tree + off;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  mark(c, s, "rlc_hash_to_g2_raw");
+  {
+    // the per-round hash's field and SSWU stages, then Q0 + Q1 without the cofactor
+    uint32_t* u = (uint32_t*)c->h_tmp.p;
+    uint32_t* q = u + 4 * FP_WORDS * n;
+    hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.m, u);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_h2c_sum, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, rpts);
+    HIP_TRY(hipGetLastError());
+  }
+  mark(c, s, "decode_g2");
+  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
+                     sg, st);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "rlc_leaves_tree");
+  // R_i to affine in place (X, Y slots; Z follows them in the Jacobian SoA)
+  hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, rpts,
+                     (const uint32_t*)(rpts + 4 * FP_WORDS * n), (uint32_t*)c->h_pre.p);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed, rpts, sg, st, T.P[0], T.S[0]);
+  HIP_TRY(hipGetLastError());
+  for (size_t l = 0; l + 1 < T.sz.size(); ++l) {
+    hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(2 * T.sz[l + 1], B)), dim3(B), 0, s, T.sz[l], T.P[l], T.S[l],
+                       T.sz[l + 1], T.P[l + 1], T.S[l + 1]);
+    HIP_TRY(hipGetLastError());
+  }
+  return DGPU_OK;
+}
+
+// Check candidate nodes cand of a level (P_lvl, S_lvl, n_level nodes) on the
+// pairing engine: e(pk, h_eff P) e(-g1, S) == 1.  Fail flags stay on the
+// device (d_fail, one byte per candidate); `fail` (optional) receives them on
+// the host (synchronizes the stream).
+int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32_t>& cand, size_t n_level,
+                     const uint32_t* P_lvl, const uint32_t* S_lvl, hipStream_t s, std::vector<uint8_t>* fail) {
+  const unsigned B = 256;
+  const size_t m = cand.size();
+  int rc;
+  if ((rc = c->rlc_idx.ensure(m * 4)) || (rc = c->rlc_fail.ensure(m))) return rc;
+  if ((rc = c->rlc_h.ensure(m * G2A_WORDS * 4)) || (rc = c->rlc_s.ensure(m * G2A_WORDS * 4)) ||
+      (rc = c->rlc_st.ensure(m)))
+    return rc;
+  uint32_t* d_idx = (uint32_t*)c->rlc_idx.p;
+  uint8_t* d_fail = (uint8_t*)c->rlc_fail.p;
+  HIP_TRY(hipMemcpyAsync(d_idx, cand.data(), m * 4, hipMemcpyHostToDevice, s));
+  uint32_t* ch = (uint32_t*)c->rlc_h.p;
+  uint32_t* cs = (uint32_t*)c->rlc_s.p;
+  uint8_t* cst = (uint8_t*)c->rlc_st.p;
+  mark(c, s, "rlc_prep");
+  hipLaunchKernelGGL(k_rlc_prep, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, n_level, P_lvl, S_lvl, ch, cs, cst);
+  HIP_TRY(hipGetLastError());
+  if ((rc = eng_pairing_locked(c, (const uint32_t*)key->consts.p, m, ch, cs, cst, s))) return rc;
+  mark(c, s, "rlc_bisection");
+  hipLaunchKernelGGL(k_rlc_fail, dim3(grid_for(m, B)), dim3(B), 0, s, m, cst, d_fail);
+  HIP_TRY(hipGetLastError());
+  if (fail) {
+    fail->resize(m);
+    HIP_TRY(hipMemcpyAsync(fail->data(), d_fail, m, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  return DGPU_OK;
+}
+
+// RLC phase 2, root first: the whole batch is one node check (one final
+// exponentiation) when every round is valid.  Otherwise the wide descent:
+// check every node of the level with <= 64Ki nodes (a multiple of D = 5 levels
+// up from the leaves), then all descendants D levels down of each failing
+// node, to the leaves; a failing leaf is an invalid round (ST_PAIRING).
+int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hipStream_t s) {
+  const unsigned B = 256;
+  const int D = 5;
+  const int top = T.top();
+  uint8_t* st = (uint8_t*)c->status.p;
+  std::vector<uint8_t> fail;
+  std::vector<uint32_t> cand{0};
+  mark(c, s, "rlc_bisection");
+  if (top > 0) {
+    int rc = rlc_check_locked(c, key, cand, 1, T.P[top], T.S[top], s, &fail);
+    if (rc) return rc;
+    if (!fail[0]) return DGPU_OK;  // every decodable round verifies
+  }
+  int S0 = 0;
+  while (S0 + D <= top && T.sz[S0] > 65536) S0 += D;
+  if (T.sz[S0] > 65536 && S0 < top) S0 = top;
+  int l = S0;
+  if (S0 == top && top > 0) {  // the root failed: its descendants D levels down
+    l = top >= D ? top - D : 0;
+    cand.clear();
+    for (size_t j = 0; j < T.sz[l]; ++j) cand.push_back((uint32_t)j);
+  } else {
+    cand.resize(T.sz[S0]);
+    for (size_t j = 0; j < T.sz[S0]; ++j) cand[j] = (uint32_t)j;
+  }
+  while (!cand.empty()) {
+    int rc = rlc_check_locked(c, key, cand, T.sz[l], T.P[l], T.S[l], s, l == 0 ? nullptr : &fail);
+    if (rc) return rc;
+    if (l == 0) {
+      hipLaunchKernelGGL(k_rlc_mark, dim3(grid_for(cand.size(), B)), dim3(B), 0, s, cand.size(),
+                         (const uint32_t*)c->rlc_idx.p, (const uint8_t*)c->rlc_fail.p, st);
+      HIP_TRY(hipGetLastError());
+      break;
+    }
+    const int nl = l >= D ? l - D : 0;
+    const size_t span = (size_t)1 << (l - nl);
+    std::vector<uint32_t> next;
+    for (size_t k = 0; k < cand.size(); ++k) {
+      if (!fail[k]) continue;
+      const size_t lo = (size_t)cand[k] * span, hi = std::min(lo + span, T.sz[nl]);
+      for (size_t j = lo; j < hi; ++j) next.push_back((uint32_t)j);
+    }
+    cand.swap(next);
+    l = nl;
+  }
+  return DGPU_OK;
+}
+
+// Per-round pairing checks on the lane-cooperative engine, chunk by chunk
+// (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
+// final exponentiation.  Decode verdicts in `st` stay final.
+int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint32_t* h, const uint32_t* sg,
+                       uint8_t* st, hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
+                       const uint32_t* fixed_table, const lane_bufs* L) {
+  if (!h_stride) h_stride = n;
+  // equal chunks of at most eng_chunk items (whole 5-item blocks): no short tail launch
+  const size_t nchunks = (n + c->eng_chunk - 1) / c->eng_chunk;
+  size_t cap = (n + nchunks - 1) / nchunks;
+  cap = std::min(n, (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK * ENG_ROUNDS_PER_BLOCK);
+  const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
+  DevBuf* b_lines = L ? L->lines : &c->eng_lines;
+  DevBuf* b_f = L ? L->f : &c->eng_f;
+  DevBuf* b_n1 = L ? L->n1 : &c->eng_n1;
+  const bool need_lines = !(fixed_table && c->fused_fixed);
+  int rc;
+  if (need_lines && (rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
+  if ((rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
+  if ((rc = b_n1->ensure(cap * FP_LIMBS * 4))) return rc;
+  // k_eng_inv's prefix products reuse the line buffer (or f, on the fused path)
+  uint32_t* lines = need_lines ? (uint32_t*)b_lines->p : nullptr;
+  uint32_t* f = (uint32_t*)b_f->p;
+  uint32_t* n1 = (uint32_t*)b_n1->p;
+  uint32_t* pre = need_lines ? lines : nullptr;
+  if (!pre) {
+    if ((rc = c->eng_lines.ensure(cap * FP_LIMBS * 4))) return rc;
+    pre = (uint32_t*)c->eng_lines.p;
+  }
+  for (size_t r0 = 0; r0 < n; r0 += cap) {
+    const size_t cnt = std::min(cap, n - r0);
+    const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
+    if (!need_lines) {  // on-G1, lines formed inside the Miller kernel
+      mark(c, s, "eng_miller");
+      hipLaunchKernelGGL(k_eng_miller_fixed, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, consts, h, sg,
+                         fixed_table, f, n1);
+      HIP_TRY(hipGetLastError());
+    } else {
+      if (fixed_table) {  // on-G1: h and sg are affine G1 points, the G2 arguments fixed
+        mark(c, s, "eng_lines_fixed");
+        hipLaunchKernelGGL(k_eng_lines_fixed, dim3(blocks, ENG_LINE_STEPS), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, sg,
+                           fixed_table, lines);
+      } else {
+        mark(c, s, "eng_lines");
+        hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
+                           pk_items, consts, lines);
+      }
+      HIP_TRY(hipGetLastError());
+      mark(c, s, "eng_miller");
+      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
+      HIP_TRY(hipGetLastError());
+    }
+    const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
+    mark(c, s, "eng_inv");
+    hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, pre, st);
+    HIP_TRY(hipGetLastError());
+    mark(c, s, "eng_fe");
+    hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
+    HIP_TRY(hipGetLastError());
+  }
+  return DGPU_OK;
+}
+
+// Signatures on G1: H(m) in G1 (+ batch affine), G1 signature decode, then
+// the engine's Miller (fixed-Q lines) / inversion / final-exponentiation kernels.
+int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, uint8_t* st, hipStream_t s) {
+  const unsigned B = 256;
+  const size_t n = a.n;
+  int rc;
+  if ((rc = c->h_pts.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->sig_pts.ensure(n * 2 * FP_WORDS * 4)) ||
+      (rc = c->h_z.ensure(n * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4)))
+    return rc;
+  uint32_t* h = (uint32_t*)c->h_pts.p;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  mark(c, s, "hash_to_g1");
+  hipLaunchKernelGGL(k_hash_to_g1_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.m,
+                     a.scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, h, (uint32_t*)c->h_z.p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "h_affine");
+  hipLaunchKernelGGL(k_g1_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
+                     (const uint32_t*)c->h_z.p, (uint32_t*)c->h_pre.p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "decode_g1");
+  hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
+                     sg, st);
+  HIP_TRY(hipGetLastError());
+  return eng_pairing_locked(c, (const uint32_t*)key->consts.p, n, h, sg, st, s, 0, nullptr, nullptr,
+                            (const uint32_t*)key->table.p);
+}
+
+// Per-round G2 path, first half of one lane: hash-to-G2 (field, SSWU, finish),
+// batch affine, signature decode of `n` items into the lane's buffers.
+int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src& m, const uint8_t* sigs,
+                        size_t sig_stride, const uint32_t* sig_len, uint8_t* st, hipStream_t s) {
+  const unsigned B = 256;
+  int rc;
+  if ((rc = L.h_pts->ensure(n * G2A_WORDS * 4)) || (rc = L.sig_pts->ensure(n * G2A_WORDS * 4)) ||
+      (rc = L.h_z->ensure(n * 2 * FP_WORDS * 4)) || (rc = L.h_pre->ensure(n * FP_WORDS * 4)) ||
+      (rc = L.h_tmp->ensure(n * (4 + 12) * FP_WORDS * 4)))
+    return rc;
+  uint32_t* h = (uint32_t*)L.h_pts->p;
+  uint32_t* sg = (uint32_t*)L.sig_pts->p;
+  uint32_t* u = (uint32_t*)L.h_tmp->p;
+  uint32_t* q = u + 4 * FP_WORDS * n;
+  mark(c, s, "hash_to_g2");
+  hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, m, u);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
+                     (uint32_t*)L.h_z->p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "h_affine");
+  hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
+                     (const uint32_t*)L.h_z->p, (uint32_t*)L.h_pre->p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "decode_g2");
+  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m, sg, st);
+  HIP_TRY(hipGetLastError());
+  return DGPU_OK;
+}
+
+// msg_src of items [off, off + cnt) of m
+msg_src src_slice(const msg_src& m, size_t off) {
+  msg_src r = m;
+  if (m.msgs) {
+    r.msgs = m.msgs + off * m.msg_stride;
+    r.msg_len = m.msg_len + off;
+  } else {
+    r.rounds = m.rounds + off;
+    if (m.chained) {
+      r.prev = m.prev + off * m.prev_stride;
+      r.prev_len = m.prev_len + off;
+    }
+  }
+  return r;
+}
+
+int check_args(const dgpu_ctx* c, const key_entry* key, const verify_args& a) {
+  if (!scheme_known(a.scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", a.scheme);
+  if (a.mode != DGPU_MODE_PER_ROUND && a.mode != DGPU_MODE_RLC) return set_err(DGPU_EINVAL, "bad mode %d", a.mode);
+  if (!key) return set_err(DGPU_ENOKEY, "no public key installed (dgpu_set_pubkey)");
+  if (sig_on_g1(a.scheme) != key->g2key)
+    return set_err(DGPU_ENOKEY, "the public key is on the wrong group for scheme %d", a.scheme);
+  if (a.n == 0) return DGPU_OK;
+  const size_t sig_bytes = sig_on_g1(a.scheme) ? 48 : 96;
+  if (!a.sigs || !a.sig_len || a.sig_stride < sig_bytes) return set_err(DGPU_EINVAL, "bad signature buffers");
+  if (a.m.msgs || a.m.msg_len) {
+    if (!a.m.msgs || !a.m.msg_len) return set_err(DGPU_EINVAL, "bad message buffers");
+  } else {
+    if (!a.m.rounds) return set_err(DGPU_EINVAL, "null rounds");
+    if (a.m.chained && (!a.m.prev_len || (!a.m.prev && a.m.prev_stride)))
+      return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
+  }
+  if (sig_on_g1(a.scheme) && a.mode != DGPU_MODE_PER_ROUND)
+    return set_err(DGPU_EUNSUPPORTED, "RLC mode is built for G2 signatures only");
+  (void)c;
+  return DGPU_OK;
+}
+
+// Everything up to the per-item status (ST_*): G1 or G2 signatures, per-round
+// or RLC.  Asynchronous on s (RLC descent synchronizes between its levels).
+int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s) {
+  const size_t n = a.n;
+  int rc;
+  if ((rc = c->status.ensure(n))) return rc;
+  uint8_t* st = (uint8_t*)c->status.p;
+  c->n_ev = 0;
+  if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
+  if (a.mode == DGPU_MODE_RLC) {
+    rlc_trees T;
+    if ((rc = rlc_build_locked(c, a, s, T))) return rc;
+    return rlc_descend_locked(c, key, T, s);
+  }
+  const uint32_t* consts = (const uint32_t*)key->consts.p;
+  const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z, &c->h_pre, &c->h_tmp, &c->eng_lines, &c->eng_f, &c->eng_n1};
+  const lane_bufs L1{&c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp, &c->l2_lines, &c->l2_f,
+                     &c->l2_n1};
+  // Two lanes (streams) on the two halves of the batch once it spans more
+  // than one engine chunk; lane 1 starts when lane 0's hash/decode kernels
+  // are done, so its register-bound hash runs beside lane 0's LDS-bound
+  // engine.  Profiled passes stay on one stream (clean per-kernel times).
+  const bool two = c->lanes > 1 && !c->profile && n >= LANE_MIN;
+  const size_t n0 = two ? ((n / 2 + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
+  if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s))) return rc;
+  if (!two)
+    return eng_pairing_locked(c, consts, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
+                              nullptr, nullptr, nullptr, &L0);
+  const size_t n1 = n - n0;
+  hipStream_t s2 = c->stream2;
+  HIP_TRY(hipEventRecord(c->lane_ev[0], s));
+  HIP_TRY(hipStreamWaitEvent(s2, c->lane_ev[0], 0));
+  if ((rc = eng_pairing_locked(c, consts, n0, (const uint32_t*)L0.h_pts->p, (const uint32_t*)L0.sig_pts->p, st, s, 0,
+                               nullptr, nullptr, nullptr, &L0)))
+    return rc;
+  if ((rc = g2_lane_hash_locked(c, L1, n1, src_slice(a.m, n0), a.sigs + n0 * a.sig_stride, a.sig_stride,
+                                a.sig_len + n0, st + n0, s2)))
+    return rc;
+  if ((rc = eng_pairing_locked(c, consts, n1, (const uint32_t*)L1.h_pts->p, (const uint32_t*)L1.sig_pts->p, st + n0,
+                               s2, 0, nullptr, nullptr, nullptr, &L1)))
+    return rc;
+  HIP_TRY(hipEventRecord(c->lane_ev[1], s2));
+  HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
+  return DGPU_OK;
+}
+
+// status -> verdict bitmap and optional reasons (device buffers)
+int verify_device_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, uint8_t* d_bits,
+                         uint8_t* d_reason, hipStream_t s) {
+  int rc = check_args(c, key, a);
+  if (rc || a.n == 0) return rc;
+  if (!d_bits) return set_err(DGPU_EINVAL, "null verdict buffer");
+  if ((rc = verify_status_locked(c, key, a, s))) return rc;
+  const unsigned B = 256;
+  const uint8_t* st = (const uint8_t*)c->status.p;
+  mark(c, s, "pack_verdicts");
+  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((a.n + 7) / 8, B)), dim3(B), 0, s, a.n, st, d_bits);
+  HIP_TRY(hipGetLastError());
+  mark(c, s);
+  if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, a.n, hipMemcpyDeviceToDevice, s));
+  return DGPU_OK;
+}
+
+// Stage the host records of a verify call into the context's input buffers;
+// rewrites a's pointers to the device copies.  Records with a length above
+// their stride are rejected here (the host path reports them as EINVAL).
+int stage_inputs_locked(dgpu_ctx* c, verify_args& a, hipStream_t s) {
+  const size_t n = a.n;
+  int rc;
+  if ((rc = c->in_sigs.ensure(n * a.sig_stride)) || (rc = c->in_sig_len.ensure(n * 4))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, a.sigs, n * a.sig_stride, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->in_sig_len.p, a.sig_len, n * 4, hipMemcpyHostToDevice, s));
+  a.sigs = (const uint8_t*)c->in_sigs.p;
+  a.sig_len = (const uint32_t*)c->in_sig_len.p;
+  msg_src& m = a.m;
+  if (m.msgs) {
+    for (size_t i = 0; i < n; ++i)
+      if (m.msg_len[i] > m.msg_stride) return set_err(DGPU_EINVAL, "msg_len[%zu]=%u > msg_stride", i, m.msg_len[i]);
+    if ((rc = c->in_msgs.ensure(n * m.msg_stride + 1)) || (rc = c->in_msg_len.ensure(n * 4))) return rc;
+    if (m.msg_stride) HIP_TRY(hipMemcpyAsync(c->in_msgs.p, m.msgs, n * m.msg_stride, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->in_msg_len.p, m.msg_len, n * 4, hipMemcpyHostToDevice, s));
+    m.msgs = (const uint8_t*)c->in_msgs.p;
+    m.msg_len = (const uint32_t*)c->in_msg_len.p;
+    return DGPU_OK;
+  }
+  if ((rc = c->in_rounds.ensure(n * 8))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_rounds.p, m.rounds, n * 8, hipMemcpyHostToDevice, s));
+  m.rounds = (const uint64_t*)c->in_rounds.p;
+  if (m.chained) {
+    for (size_t i = 0; i < n; ++i)
+      if (m.prev_len[i] > m.prev_stride) return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, m.prev_len[i]);
+    if ((rc = c->in_prev.ensure(n * m.prev_stride + 1)) || (rc = c->in_prev_len.ensure(n * 4))) return rc;
+    if (m.prev_stride) HIP_TRY(hipMemcpyAsync(c->in_prev.p, m.prev, n * m.prev_stride, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->in_prev_len.p, m.prev_len, n * 4, hipMemcpyHostToDevice, s));
+    m.prev = (const uint8_t*)c->in_prev.p;
+    m.prev_len = (const uint32_t*)c->in_prev_len.p;
+  }
+  return DGPU_OK;
+}
+
+// Host-buffer verify: stage, verify, copy the verdicts back (synchronous).
+int verify_host_locked(dgpu_ctx* c, const key_entry* key, verify_args a, uint8_t* verdict_bits, uint8_t* reason) {
+  int rc = check_args(c, key, a);
+  if (rc || a.n == 0) return rc;
+  if (!verdict_bits) return set_err(DGPU_EINVAL, "null verdict buffer");
+  hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  if ((rc = stage_inputs_locked(c, a, s))) return rc;
+  if ((rc = c->out_bits.ensure((a.n + 7) / 8)) || (rc = c->out_reason.ensure(a.n))) return rc;
+  if ((rc = verify_device_locked(c, key, a, (uint8_t*)c->out_bits.p, (uint8_t*)c->out_reason.p, s))) return rc;
+  HIP_TRY(hipMemcpyAsync(verdict_bits, c->out_bits.p, (a.n + 7) / 8, hipMemcpyDeviceToHost, s));
+  if (reason) HIP_TRY(hipMemcpyAsync(reason, c->out_reason.p, a.n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+size_t size_engine_chunk(int lanes) {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return ENG_CHUNK;
+  const size_t fit = free_b / 4 / ((size_t)std::max(lanes, 1) * ENG_BYTES_PER_ROUND);
+  return std::max(ENG_CHUNK_MIN, std::min(ENG_CHUNK, fit));
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -174,6 +794,18 @@ int dgpu_scheme_from_name(const char* name) {
   if (!strcmp(name, "bls-unchained-on-g1")) return DGPU_SCHEME_UNCHAINED_G1;
   if (!strcmp(name, "bls-unchained-g1-rfc9380")) return DGPU_SCHEME_G1_RFC9380;
   return set_err(DGPU_EINVAL, "scheme [%s] is not valid", name);
+}
+
+void dgpu_shard_range(size_t n, int ndev, int k, size_t* lo, size_t* hi) {
+  // contiguous shards of a multiple of 8 items (whole verdict-bitmap bytes),
+  // the last one takes the remainder
+  if (ndev < 1) ndev = 1;
+  size_t per = (n + (size_t)ndev - 1) / (size_t)ndev;
+  per = (per + 7) & ~(size_t)7;
+  size_t a = std::min(n, (size_t)k * per), b = std::min(n, a + per);
+  if (k < 0) a = b = 0;
+  if (lo) *lo = a;
+  if (hi) *hi = b;
 }
 
 int dgpu_open(int device, dgpu_ctx** out) {
@@ -190,23 +822,22 @@ int dgpu_open(int device, dgpu_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   dgpu_ctx* c = new dgpu_ctx();
   c->device = device;
-  const char* pm = getenv("DGPU_PAIRING");
-  c->legacy_pairing = pm && !strcmp(pm, "legacy");
   const char* lv = getenv("DGPU_LANES");
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
   const char* ec = getenv("DGPU_ENG_CHUNK");
-  if (ec && atol(ec) >= 4096) c->eng_chunk = (size_t)atol(ec);
+  c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[1], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e != hipSuccess) {
-    delete c;
+    dgpu_close(c);
     return set_err(DGPU_EDEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
   }
-  if (upload_eng_consts(c) != DGPU_OK) {
+  if (upload_eng_consts(&c->eng_consts, nullptr) != DGPU_OK) {
     std::string msg = g_last_error;
     dgpu_close(c);
     return set_err(DGPU_EDEVICE, "%s", msg.c_str());
@@ -218,435 +849,39 @@ int dgpu_open(int device, dgpu_ctx** out) {
 void dgpu_close(dgpu_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
-  hipStreamSynchronize(c->stream);
+  if (c->stream) hipStreamSynchronize(c->stream);
   if (c->stream2) hipStreamSynchronize(c->stream2);
+  if (c->done) hipEventSynchronize(c->done);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (hipEvent_t e : c->lane_ev)
     if (e) hipEventDestroy(e);
+  if (c->done) hipEventDestroy(c->done);
+  for (key_entry& k : c->keys) {
+    k.consts.release();
+    k.table.release();
+  }
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
-                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk, &c->rec_st, &c->rec_sel, &c->rec_part, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_pre, &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->g1_table, &c->g1_aux, &c->in_rounds, &c->in_sigs, &c->in_sig_len, &c->in_prev,
-                    &c->in_prev_len, &c->out_bits, &c->out_reason, &c->misc, &c->l2_h_pts, &c->l2_sig_pts,
-                    &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp, &c->l2_lines, &c->l2_f, &c->l2_n1})
+                    &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk,
+                    &c->rec_st, &c->rec_sel, &c->rec_part, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1,
+                    &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
+                    &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->in_rounds, &c->in_sigs,
+                    &c->in_sig_len, &c->in_prev, &c->in_prev_len, &c->in_msgs, &c->in_msg_len, &c->out_bits,
+                    &c->out_reason, &c->misc, &c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp,
+                    &c->l2_lines, &c->l2_f, &c->l2_n1})
     b->release();
   if (c->stream2) hipStreamDestroy(c->stream2);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
-static int set_pubkey_g2_locked(dgpu_ctx* c, int scheme, const uint8_t* pk);
-
 int dgpu_set_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len) {
   if (!c || !pk) return set_err(DGPU_EINVAL, "null argument");
-  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
-  if (sig_on_g1(scheme)) {
-    if (len != 96) return set_err(DGPU_EINVAL, "public key must be 96 bytes (compressed G2), got %zu", len);
-    std::lock_guard<std::mutex> lk(c->mu);
-    HIP_TRY(hipSetDevice(c->device));
-    return set_pubkey_g2_locked(c, scheme, pk);
-  }
-  if (len != 48) return set_err(DGPU_EINVAL, "public key must be 48 bytes (compressed G1), got %zu", len);
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  int rc = c->misc.ensure(256);
+  key_entry* k = nullptr;
+  int rc = get_key_locked(c, scheme, pk, len, &k);
   if (rc) return rc;
-  uint8_t* d = (uint8_t*)c->misc.p;
-  HIP_TRY(hipMemcpyAsync(d, pk, 48, hipMemcpyHostToDevice, c->stream));
-  uint32_t* d_out = (uint32_t*)(d + 64);
-  int* d_rc = (int*)(d + 64 + 2 * FP_LIMBS * 4);
-  hipLaunchKernelGGL(k_decode_g1_pk, dim3(1), dim3(64), 0, c->stream, d, d_out, d_rc);
-  HIP_TRY(hipGetLastError());
-  uint32_t host[2 * FP_LIMBS + 1];
-  HIP_TRY(hipMemcpyAsync(host, d_out, sizeof host, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  int drc = (int)host[2 * FP_LIMBS];
-  if (drc != DEC_OK) return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
-  memcpy(c->pk.neg_x.l, host, FP_LIMBS * 4);
-  memcpy(c->pk.y.l, host + FP_LIMBS, FP_LIMBS * 4);
-  if ((rc = upload_eng_consts(c))) return rc;
-  c->have_key = true;
-  c->key_scheme = scheme;
-  return DGPU_OK;
-}
-
-static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
-                              hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
-                              const uint32_t* pk_items = nullptr, const uint32_t* fixed_table = nullptr,
-                              const lane_bufs* L = nullptr);
-
-// RLC batch verification with exact per-round verdicts (mode DGPU_MODE_RLC).
-// 1. R_i = pre-cofactor H(m_i) (Jacobian), sig_i decoded (+ subgroup), status.
-// 2. Leaves P_i = r_i R_i, S_i = r_i sig_i; segment tree of sums up to the root.
-// 3. Descent: check the nodes of one level, then the descendants of failing
-//    nodes D levels down, to the leaves; a failing leaf is an invalid round
-//    (ST_PAIRING).  Host-synchronous per descent step.
-// Stage events: hash, decode, leaves+tree, bisection.
-static int rlc_locked(dgpu_ctx* c, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs, size_t sig_stride,
-                      const uint32_t* d_sig_len, const uint8_t* d_prev, size_t prev_stride, const uint32_t* d_prev_len,
-                      bool chained, uint64_t seed, hipStream_t s) {
-  const unsigned B = 256;
-  // level sizes
-  std::vector<size_t> sz{n};
-  while (sz.back() > 1) sz.push_back((sz.back() + 1) / 2);
-  size_t total = 0;
-  for (size_t v : sz) total += v;
-  int rc;
-  if ((rc = c->rlc_tree.ensure(2 * total * G2J_WORDS * 4 + n * G2J_WORDS * 4))) return rc;
-  if ((rc = c->rlc_idx.ensure(65536 * 4))) return rc;
-  if ((rc = c->rlc_fail.ensure(65536))) return rc;
-  uint32_t* tree = (uint32_t*)c->rlc_tree.p;
-  std::vector<uint32_t*> P(sz.size()), S(sz.size());
-  size_t off = 0;
-  for (size_t l = 0; l < sz.size(); ++l) {
-    P[l] = tree + off;
-    off += sz[l] * G2J_WORDS;
-    S[l] = tree + off;
-    off += sz[l] * G2J_WORDS;
-  }
-  uint32_t* rpts = tree + off;
-  uint32_t* sg = (uint32_t*)c->sig_pts.p;
-  uint8_t* st = (uint8_t*)c->status.p;
-  mark(c, s, "rlc_hash_to_g2_raw");
-  {
-    // the per-round hash's field and SSWU stages, then Q0 + Q1 without the cofactor
-    if ((rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4))) return rc;
-    uint32_t* u = (uint32_t*)c->h_tmp.p;
-    uint32_t* q = u + 4 * FP_WORDS * n;
-    hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride, d_prev_len,
-                       chained ? 1 : 0, u);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_h2c_sum, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, rpts);
-    HIP_TRY(hipGetLastError());
-  }
-  mark(c, s, "decode_g2");
-  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
-  HIP_TRY(hipGetLastError());
-  mark(c, s, "rlc_leaves_tree");
-  // R_i to affine in place (X, Y slots; Z follows them in the Jacobian SoA)
-  if ((rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
-  hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, rpts,
-                     (const uint32_t*)(rpts + 4 * FP_WORDS * n), (uint32_t*)c->h_pre.p);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, d_rounds, seed, rpts, sg, st, P[0],
-                     S[0]);
-  HIP_TRY(hipGetLastError());
-  for (size_t l = 0; l + 1 < sz.size(); ++l) {
-    hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(2 * sz[l + 1], B)), dim3(B), 0, s, sz[l], P[l], S[l], sz[l + 1],
-                       P[l + 1], S[l + 1]);
-    HIP_TRY(hipGetLastError());
-  }
-  mark(c, s, "rlc_bisection");
-  // Wide descent: check every node of level S (a multiple of D = 5 with
-  // <= 64Ki nodes), then all level-(l-D) descendants of each failing node,
-  // down to the leaves: 2-3 sequential launches at 1M-10M rounds, each one
-  // wide enough to fill the GPU; with uniform corruption at rate rho the
-  // pairings spent are ~n/32 + (bad rounds) * 32.
-  const int D = 5;
-  int top = (int)sz.size() - 1;
-  int S0 = 0;
-  while (S0 + D <= top && sz[S0] > 65536) S0 += D;
-  if (sz[S0] > 65536 && S0 < top) S0 = top;
-  std::vector<uint32_t> cand(sz[S0]);
-  for (size_t j = 0; j < sz[S0]; ++j) cand[j] = (uint32_t)j;
-  uint32_t* d_idx = (uint32_t*)c->rlc_idx.p;
-  uint8_t* d_fail = (uint8_t*)c->rlc_fail.p;
-  std::vector<uint8_t> fail;
-  for (int l = S0; l >= 0 && !cand.empty();) {
-    size_t m = cand.size();
-    if ((rc = c->rlc_idx.ensure(m * 4))) return rc;
-    if ((rc = c->rlc_fail.ensure(m))) return rc;
-    d_idx = (uint32_t*)c->rlc_idx.p;
-    d_fail = (uint8_t*)c->rlc_fail.p;
-    HIP_TRY(hipMemcpyAsync(d_idx, cand.data(), m * 4, hipMemcpyHostToDevice, s));
-    if (c->legacy_pairing) {
-      hipLaunchKernelGGL(k_rlc_check, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], c->pk, d_fail);
-      HIP_TRY(hipGetLastError());
-    } else {
-      // node checks on the pairing engine: e(pk, h_eff P) e(-g1, S) == 1
-      if ((rc = c->rlc_h.ensure(m * G2A_WORDS * 4)) || (rc = c->rlc_s.ensure(m * G2A_WORDS * 4)) ||
-          (rc = c->rlc_st.ensure(m)))
-        return rc;
-      uint32_t* ch = (uint32_t*)c->rlc_h.p;
-      uint32_t* cs = (uint32_t*)c->rlc_s.p;
-      uint8_t* cst = (uint8_t*)c->rlc_st.p;
-      mark(c, s, "rlc_prep");
-      hipLaunchKernelGGL(k_rlc_prep, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, sz[l], P[l], S[l], ch, cs, cst);
-      HIP_TRY(hipGetLastError());
-      if ((rc = eng_pairing_locked(c, m, ch, cs, cst, s))) return rc;
-      mark(c, s, "rlc_bisection");
-      hipLaunchKernelGGL(k_rlc_fail, dim3(grid_for(m, B)), dim3(B), 0, s, m, cst, d_fail);
-      HIP_TRY(hipGetLastError());
-    }
-    if (l == 0) {
-      hipLaunchKernelGGL(k_rlc_mark, dim3(grid_for(m, B)), dim3(B), 0, s, m, d_idx, d_fail, st);
-      HIP_TRY(hipGetLastError());
-      break;
-    }
-    fail.resize(m);
-    HIP_TRY(hipMemcpyAsync(fail.data(), d_fail, m, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    int nl = l >= D ? l - D : 0;
-    size_t span = (size_t)1 << (l - nl);
-    std::vector<uint32_t> next;
-    for (size_t k = 0; k < m; ++k) {
-      if (!fail[k]) continue;
-      size_t lo = (size_t)cand[k] * span, hi = std::min(lo + span, sz[nl]);
-      for (size_t j = lo; j < hi; ++j) next.push_back((uint32_t)j);
-    }
-    cand.swap(next);
-    l = nl;
-  }
-  return DGPU_OK;
-}
-
-// Per-round pairing checks on the lane-cooperative engine, chunk by chunk
-// (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
-// final exponentiation.  Decode verdicts in `st` stay final.
-static int eng_pairing_locked(dgpu_ctx* c, size_t n, const uint32_t* h, const uint32_t* sg, uint8_t* st,
-                              hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
-                              const uint32_t* fixed_table, const lane_bufs* L) {
-  if (!h_stride) h_stride = n;
-  const size_t cap = std::min<size_t>(n, c->eng_chunk);
-  const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
-  DevBuf* b_lines = L ? L->lines : &c->eng_lines;
-  DevBuf* b_f = L ? L->f : &c->eng_f;
-  DevBuf* b_n1 = L ? L->n1 : &c->eng_n1;
-  int rc;
-  if ((rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
-  if ((rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
-  if ((rc = b_n1->ensure(cap * FP_LIMBS * 4))) return rc;
-  const uint32_t* consts = (const uint32_t*)c->eng_consts.p;
-  uint32_t* lines = (uint32_t*)b_lines->p;
-  uint32_t* f = (uint32_t*)b_f->p;
-  uint32_t* n1 = (uint32_t*)b_n1->p;
-  for (size_t r0 = 0; r0 < n; r0 += cap) {
-    const size_t cnt = std::min(cap, n - r0);
-    const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
-    if (fixed_table && c->fused_fixed) {  // on-G1, lines formed inside the Miller kernel
-      mark(c, s, "eng_miller");
-      hipLaunchKernelGGL(k_eng_miller_fixed, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, consts, h, sg,
-                         fixed_table, f, n1);
-      HIP_TRY(hipGetLastError());
-    } else if (fixed_table) {  // on-G1: h and sg are affine G1 points, the G2 arguments fixed
-      mark(c, s, "eng_lines_fixed");
-      hipLaunchKernelGGL(k_eng_lines_fixed, dim3(blocks, ENG_LINE_STEPS), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, sg,
-                         fixed_table, lines);
-    } else {
-      mark(c, s, "eng_lines");
-      hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
-                         pk_items, consts, lines);
-    }
-    if (!(fixed_table && c->fused_fixed)) {
-      HIP_TRY(hipGetLastError());
-      mark(c, s, "eng_miller");
-      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
-      HIP_TRY(hipGetLastError());
-    }
-    const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
-    mark(c, s, "eng_inv");
-    hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, lines, st);
-    HIP_TRY(hipGetLastError());
-    mark(c, s, "eng_fe");
-    hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
-    HIP_TRY(hipGetLastError());
-  }
-  return DGPU_OK;
-}
-
-// On-G1 schemes: decode the G2 public key (subgroup-checked) and compute the
-// fixed-Q line table: the LINES program for (pk, g2) at P = (1, 1).
-static int set_pubkey_g2_locked(dgpu_ctx* c, int scheme, const uint8_t* pk) {
-  int rc;
-  const size_t tbl_words = (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS;
-  if ((rc = c->g1_table.ensure(tbl_words * 4)) || (rc = c->g1_aux.ensure(4096)) || (rc = c->misc.ensure(256))) return rc;
-  DevBuf unit;
-  if ((rc = upload_eng_consts(c, true, &unit))) return rc;
-  uint8_t* aux = (uint8_t*)c->g1_aux.p;
-  uint32_t* d_pk = (uint32_t*)aux;                       // affine G2, stride 1 (224 B)
-  uint32_t* d_g2 = (uint32_t*)(aux + 1024);              // generator, stride 1
-  int* d_rc = (int*)(aux + 2048);
-  uint8_t* d_in = aux + 3072;
-  g2a gen{C_G2_X, C_G2_Y};
-  uint32_t gw[G2A_WORDS];
-  memcpy(gw, gen.x.c0.l, 56);
-  memcpy(gw + 14, gen.x.c1.l, 56);
-  memcpy(gw + 28, gen.y.c0.l, 56);
-  memcpy(gw + 42, gen.y.c1.l, 56);
-  hipStream_t s = c->stream;
-  hipError_t e = hipMemcpyAsync(d_in, pk, 96, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) e = hipMemcpyAsync(d_g2, gw, sizeof gw, hipMemcpyHostToDevice, s);
-  if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_decode_g2_pk, dim3(1), dim3(64), 0, s, d_in, d_pk, d_rc);
-    e = hipGetLastError();
-  }
-  int drc = -1;
-  if (e == hipSuccess) e = hipMemcpyAsync(&drc, d_rc, sizeof drc, hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) {
-    unit.release();
-    return set_err(DGPU_EDEVICE, "set_pubkey: %s", hipGetErrorString(e));
-  }
-  if (drc != DEC_OK) {
-    unit.release();
-    return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
-  }
-  hipLaunchKernelGGL(k_eng_lines, dim3(1), dim3(ENG_BLOCK), 0, s, (size_t)1, (size_t)0, (size_t)1,
-                     (const uint32_t*)d_pk, (size_t)1, (const uint32_t*)nullptr, (const uint32_t*)d_g2,
-                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)c->g1_table.p);
-  e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  unit.release();
-  if (e != hipSuccess) return set_err(DGPU_EDEVICE, "set_pubkey lines: %s", hipGetErrorString(e));
-  c->have_key = true;
-  c->key_scheme = scheme;
-  return DGPU_OK;
-}
-
-// Signatures on G1: H(m) in G1 (+ batch affine), G1 signature decode, fixed-Q
-// lines, then the engine's Miller / inversion / final-exponentiation kernels.
-static int verify_g1_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
-                            size_t sig_stride, const uint32_t* d_sig_len, uint8_t* d_bits, uint8_t* d_reason,
-                            hipStream_t s) {
-  const unsigned B = 256;
-  int rc;
-  if ((rc = c->h_pts.ensure(n * 2 * FP_WORDS * 4)) || (rc = c->sig_pts.ensure(n * 2 * FP_WORDS * 4)) ||
-      (rc = c->status.ensure(n)) || (rc = c->h_z.ensure(n * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4)))
-    return rc;
-  uint32_t* h = (uint32_t*)c->h_pts.p;
-  uint32_t* sg = (uint32_t*)c->sig_pts.p;
-  uint8_t* st = (uint8_t*)c->status.p;
-  c->n_ev = 0;
-  mark(c, s, "hash_to_g1");
-  hipLaunchKernelGGL(k_hash_to_g1_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds,
-                     scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, h, (uint32_t*)c->h_z.p);
-  HIP_TRY(hipGetLastError());
-  mark(c, s, "h_affine");
-  hipLaunchKernelGGL(k_g1_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
-                     (const uint32_t*)c->h_z.p, (uint32_t*)c->h_pre.p);
-  HIP_TRY(hipGetLastError());
-  mark(c, s, "decode_g1");
-  hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
-  HIP_TRY(hipGetLastError());
-  if ((rc = eng_pairing_locked(c, n, h, sg, st, s, 0, nullptr, nullptr, (const uint32_t*)c->g1_table.p))) return rc;
-  mark(c, s, "pack_verdicts");
-  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);
-  HIP_TRY(hipGetLastError());
-  mark(c, s);
-  if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, n, hipMemcpyDeviceToDevice, s));
-  return DGPU_OK;
-}
-
-// Per-round G2 path, first half of one lane: hash-to-G2 (field, SSWU, finish),
-// batch affine, signature decode of `n` rounds into the lane's buffers.
-static int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const uint64_t* d_rounds,
-                               const uint8_t* d_sigs, size_t sig_stride, const uint32_t* d_sig_len,
-                               const uint8_t* d_prev, size_t prev_stride, const uint32_t* d_prev_len, bool chained,
-                               uint8_t* st, hipStream_t s) {
-  const unsigned B = 256;
-  int rc;
-  if ((rc = L.h_pts->ensure(n * G2A_WORDS * 4)) || (rc = L.sig_pts->ensure(n * G2A_WORDS * 4)) ||
-      (rc = L.h_z->ensure(n * 2 * FP_WORDS * 4)) || (rc = L.h_pre->ensure(n * FP_WORDS * 4)) ||
-      (rc = L.h_tmp->ensure(n * (4 + 12) * FP_WORDS * 4)))
-    return rc;
-  uint32_t* h = (uint32_t*)L.h_pts->p;
-  uint32_t* sg = (uint32_t*)L.sig_pts->p;
-  uint32_t* u = (uint32_t*)L.h_tmp->p;
-  uint32_t* q = u + 4 * FP_WORDS * n;
-  mark(c, s, "hash_to_g2");
-  hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_rounds, d_prev, prev_stride, d_prev_len,
-                     chained ? 1 : 0, u);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
-                     (uint32_t*)L.h_z->p);
-  HIP_TRY(hipGetLastError());
-  mark(c, s, "h_affine");
-  hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
-                     (const uint32_t*)L.h_z->p, (uint32_t*)L.h_pre->p);
-  HIP_TRY(hipGetLastError());
-  mark(c, s, "decode_g2");
-  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, d_sigs, sig_stride, d_sig_len, sg, st);
-  HIP_TRY(hipGetLastError());
-  return DGPU_OK;
-}
-
-static int verify_device_locked(dgpu_ctx* c, int scheme, size_t n, const uint64_t* d_rounds, const uint8_t* d_sigs,
-                                size_t sig_stride, const uint32_t* d_sig_len, const uint8_t* d_prev,
-                                size_t prev_stride, const uint32_t* d_prev_len, int mode, uint64_t rlc_seed,
-                                uint8_t* d_bits, uint8_t* d_reason, hipStream_t s) {
-  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
-  if (mode != DGPU_MODE_PER_ROUND && mode != DGPU_MODE_RLC) return set_err(DGPU_EINVAL, "bad mode %d", mode);
-  if (!c->have_key) return set_err(DGPU_ENOKEY, "no public key installed (dgpu_set_pubkey)");
-  if (sig_on_g1(scheme) != sig_on_g1(c->key_scheme))
-    return set_err(DGPU_ENOKEY, "installed public key is for scheme %d, whose signatures are on the other group",
-                   c->key_scheme);
-  if (n == 0) return DGPU_OK;
-  bool chained = scheme == DGPU_SCHEME_CHAINED;
-  if (sig_on_g1(scheme)) {
-    if (mode != DGPU_MODE_PER_ROUND) return set_err(DGPU_EUNSUPPORTED, "RLC mode is built for G2 signatures only");
-    if (!d_rounds || !d_sigs || !d_sig_len || !d_bits || sig_stride < 48) return set_err(DGPU_EINVAL, "bad buffers");
-    return verify_g1_locked(c, scheme, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_bits, d_reason, s);
-  }
-  if (!d_rounds || !d_sigs || !d_sig_len || !d_bits || sig_stride < 96) return set_err(DGPU_EINVAL, "bad buffers");
-  if (chained && (!d_prev || !d_prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
-  int rc;
-  if ((rc = c->status.ensure(n))) return rc;
-  uint8_t* st = (uint8_t*)c->status.p;
-  const unsigned B = 256;
-  c->n_ev = 0;
-  if (mode == DGPU_MODE_RLC) {
-    if ((rc = c->h_pts.ensure(n * G2A_WORDS * 4))) return rc;
-    if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
-    rc = rlc_locked(c, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len, chained, rlc_seed,
-                    s);
-    if (rc) return rc;
-  } else {
-    const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z, &c->h_pre, &c->h_tmp, &c->eng_lines, &c->eng_f, &c->eng_n1};
-    const lane_bufs L1{&c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp, &c->l2_lines, &c->l2_f,
-                       &c->l2_n1};
-    // Two lanes (streams) on the two halves of the batch once it spans more
-    // than one engine chunk; lane 1 starts when lane 0's hash/decode kernels
-    // are done, so its register-bound hash runs beside lane 0's LDS-bound
-    // engine.  Profiled passes stay on one stream (clean per-kernel times).
-    const bool two = c->lanes > 1 && !c->profile && !c->legacy_pairing && n >= LANE_MIN;
-    const size_t n0 = two ? ((n / 2 + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
-    if ((rc = g2_lane_hash_locked(c, L0, n0, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len,
-                                  chained, st, s)))
-      return rc;
-    if (two) {
-      const size_t n1 = n - n0;
-      hipStream_t s2 = c->stream2;
-      HIP_TRY(hipEventRecord(c->lane_ev[0], s));
-      HIP_TRY(hipStreamWaitEvent(s2, c->lane_ev[0], 0));
-      if ((rc = eng_pairing_locked(c, n0, (const uint32_t*)L0.h_pts->p, (const uint32_t*)L0.sig_pts->p, st, s, 0,
-                                   nullptr, nullptr, nullptr, &L0)))
-        return rc;
-      if ((rc = g2_lane_hash_locked(c, L1, n1, d_rounds + n0, d_sigs + n0 * sig_stride, sig_stride, d_sig_len + n0,
-                                    chained ? d_prev + n0 * prev_stride : nullptr, prev_stride,
-                                    chained ? d_prev_len + n0 : nullptr, chained, st + n0, s2)))
-        return rc;
-      if ((rc = eng_pairing_locked(c, n1, (const uint32_t*)L1.h_pts->p, (const uint32_t*)L1.sig_pts->p, st + n0, s2,
-                                   0, nullptr, nullptr, nullptr, &L1)))
-        return rc;
-      HIP_TRY(hipEventRecord(c->lane_ev[1], s2));
-      HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
-    } else if (c->legacy_pairing) {
-      mark(c, s, "pairing_check");
-      hipLaunchKernelGGL(k_pairing_check, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)c->h_pts.p,
-                         (const uint32_t*)c->sig_pts.p, st, c->pk);
-      HIP_TRY(hipGetLastError());
-    } else if ((rc = eng_pairing_locked(c, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
-                                        nullptr, nullptr, nullptr, &L0))) {
-      return rc;
-    }
-  }
-  mark(c, s, "pack_verdicts");
-  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((n + 7) / 8, B)), dim3(B), 0, s, n, st, d_bits);
-  HIP_TRY(hipGetLastError());
-  mark(c, s);
-  if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, n, hipMemcpyDeviceToDevice, s));
+  c->cur = k;
   return DGPU_OK;
 }
 
@@ -658,50 +893,71 @@ int dgpu_verify_batch_device(dgpu_ctx* c, int scheme, size_t n, const uint64_t* 
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  return verify_device_locked(c, scheme, n, d_rounds, d_sigs, sig_stride, d_sig_len, d_prev, prev_stride, d_prev_len,
-                              mode, rlc_seed, d_bits, d_reason, s);
+  stream_order ord(c, s);
+  const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
+                      d_sigs, sig_stride, d_sig_len, mode, rlc_seed};
+  return verify_device_locked(c, c->cur, a, d_bits, d_reason, s);
 }
 
 int dgpu_verify_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds, const uint8_t* sigs,
                       size_t sig_stride, const uint32_t* sig_len, const uint8_t* prev, size_t prev_stride,
                       const uint32_t* prev_len, int mode, uint64_t rlc_seed, uint8_t* verdict_bits, uint8_t* reason) {
   if (!c) return set_err(DGPU_EINVAL, "null ctx");
-  if (n == 0) return DGPU_OK;
-  if (!rounds || !sigs || !sig_len || !verdict_bits) return set_err(DGPU_EINVAL, "null buffer");
-  bool chained = scheme == DGPU_SCHEME_CHAINED;
-  if (chained && (!prev || !prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  int rc;
-  if ((rc = c->in_rounds.ensure(n * 8))) return rc;
-  if ((rc = c->in_sigs.ensure(n * sig_stride))) return rc;
-  if ((rc = c->in_sig_len.ensure(n * 4))) return rc;
-  if ((rc = c->out_bits.ensure((n + 7) / 8))) return rc;
-  if ((rc = c->out_reason.ensure(n))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->in_rounds.p, rounds, n * 8, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, sigs, n * sig_stride, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(c->in_sig_len.p, sig_len, n * 4, hipMemcpyHostToDevice, s));
-  const uint8_t* d_prev = nullptr;
-  const uint32_t* d_prev_len = nullptr;
-  if (chained) {
-    if ((rc = c->in_prev.ensure(n * prev_stride + 1))) return rc;
-    if ((rc = c->in_prev_len.ensure(n * 4))) return rc;
-    for (size_t i = 0; i < n; ++i)
-      if (prev_len[i] > prev_stride) return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, prev_len[i]);
-    if (prev_stride) HIP_TRY(hipMemcpyAsync(c->in_prev.p, prev, n * prev_stride, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->in_prev_len.p, prev_len, n * 4, hipMemcpyHostToDevice, s));
-    d_prev = (const uint8_t*)c->in_prev.p;
-    d_prev_len = (const uint32_t*)c->in_prev_len.p;
-  }
-  rc = verify_device_locked(c, scheme, n, (const uint64_t*)c->in_rounds.p, (const uint8_t*)c->in_sigs.p, sig_stride,
-                            (const uint32_t*)c->in_sig_len.p, d_prev, prev_stride, d_prev_len, mode, rlc_seed,
-                            (uint8_t*)c->out_bits.p, (uint8_t*)c->out_reason.p, s);
+  const verify_args a{scheme, n, beacon_src(rounds, prev, prev_stride, prev_len, scheme == DGPU_SCHEME_CHAINED), sigs,
+                      sig_stride, sig_len, mode, rlc_seed};
+  return verify_host_locked(c, c->cur, a, verdict_bits, reason);
+}
+
+int dgpu_verify_beacons(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_len, size_t n, const uint64_t* rounds,
+                        const uint8_t* sigs, size_t sig_stride, const uint32_t* sig_len, const uint8_t* prev,
+                        size_t prev_stride, const uint32_t* prev_len, int mode, uint64_t rlc_seed,
+                        uint8_t* verdict_bits, uint8_t* reason) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  key_entry* k = nullptr;
+  int rc = get_key_locked(c, scheme, pk, pk_len, &k);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(verdict_bits, c->out_bits.p, (n + 7) / 8, hipMemcpyDeviceToHost, s));
-  if (reason) HIP_TRY(hipMemcpyAsync(reason, c->out_reason.p, n, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  return DGPU_OK;
+  const verify_args a{scheme, n, beacon_src(rounds, prev, prev_stride, prev_len, scheme == DGPU_SCHEME_CHAINED), sigs,
+                      sig_stride, sig_len, mode, rlc_seed};
+  return verify_host_locked(c, k, a, verdict_bits, reason);
+}
+
+int dgpu_verify_beacons_device(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_len, size_t n,
+                               const uint64_t* d_rounds, const uint8_t* d_sigs, size_t sig_stride,
+                               const uint32_t* d_sig_len, const uint8_t* d_prev, size_t prev_stride,
+                               const uint32_t* d_prev_len, int mode, uint64_t rlc_seed, uint8_t* d_bits,
+                               uint8_t* d_reason, void* stream) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  key_entry* k = nullptr;
+  int rc = get_key_locked(c, scheme, pk, pk_len, &k);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  stream_order ord(c, s);
+  const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
+                      d_sigs, sig_stride, d_sig_len, mode, rlc_seed};
+  return verify_device_locked(c, k, a, d_bits, d_reason, s);
+}
+
+int dgpu_verify_recovered(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_len, size_t n, const uint8_t* msgs,
+                          size_t msg_stride, const uint32_t* msg_len, const uint8_t* sigs, size_t sig_stride,
+                          const uint32_t* sig_len, int mode, uint64_t rlc_seed, uint8_t* verdict_bits,
+                          uint8_t* reason) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  if (n && (!msg_len || (!msgs && msg_stride))) return set_err(DGPU_EINVAL, "null message buffers");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  key_entry* k = nullptr;
+  int rc = get_key_locked(c, scheme, pk, pk_len, &k);
+  if (rc) return rc;
+  static const uint8_t empty = 0;
+  const verify_args a{scheme, n, raw_src(msgs ? msgs : &empty, msg_stride, msg_len), sigs, sig_stride, sig_len, mode,
+                      rlc_seed};
+  return verify_host_locked(c, k, a, verdict_bits, reason);
 }
 
 int dgpu_set_profiling(dgpu_ctx* c, int enable) {
@@ -744,10 +1000,11 @@ int dgpu_digest_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds,
   if (!c || !rounds || !out32) return set_err(DGPU_EINVAL, "null argument");
   if (n == 0) return DGPU_OK;
   bool chained = scheme == DGPU_SCHEME_CHAINED;
-  if (chained && (!prev || !prev_len)) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
+  if (chained && (!prev_len || (!prev && prev_stride))) return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  stream_order ord(c, s);
   int rc;
   if ((rc = c->in_rounds.ensure(n * 8))) return rc;
   if ((rc = c->misc.ensure(n * 32))) return rc;
@@ -772,42 +1029,51 @@ int dgpu_digest_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds,
   return DGPU_OK;
 }
 
-int dgpu_hash_to_g2(dgpu_ctx* c, size_t n, const uint8_t* msg32, uint8_t* out96) {
-  if (!c || !msg32 || !out96) return set_err(DGPU_EINVAL, "null argument");
+int dgpu_hash_to_curve(dgpu_ctx* c, int scheme, size_t n, const uint8_t* msgs, size_t msg_stride,
+                       const uint32_t* msg_len, uint8_t* out) {
+  if (!c || !msg_len || !out || (!msgs && msg_stride)) return set_err(DGPU_EINVAL, "null argument");
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
   if (n == 0) return DGPU_OK;
+  for (size_t i = 0; i < n; ++i)
+    if (msg_len[i] > msg_stride) return set_err(DGPU_EINVAL, "msg_len[%zu]=%u > msg_stride", i, msg_len[i]);
+  const bool g1 = sig_on_g1(scheme);
+  const size_t ob = g1 ? 48 : 96;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  stream_order ord(c, s);
   int rc;
-  if ((rc = c->in_sigs.ensure(n * 32))) return rc;
-  if ((rc = c->misc.ensure(n * 96))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, msg32, n * 32, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_hash_to_g2_msgs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const uint8_t*)c->in_sigs.p,
-                     (uint8_t*)c->misc.p);
+  if ((rc = c->in_msgs.ensure(n * msg_stride + 1)) || (rc = c->in_msg_len.ensure(n * 4)) ||
+      (rc = c->misc.ensure(n * ob)))
+    return rc;
+  if (msg_stride) HIP_TRY(hipMemcpyAsync(c->in_msgs.p, msgs, n * msg_stride, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->in_msg_len.p, msg_len, n * 4, hipMemcpyHostToDevice, s));
+  const msg_src m = raw_src((const uint8_t*)c->in_msgs.p, msg_stride, (const uint32_t*)c->in_msg_len.p);
+  if (g1)
+    hipLaunchKernelGGL(k_hash_to_g1_msgs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, m,
+                       scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, (uint8_t*)c->misc.p);
+  else
+    hipLaunchKernelGGL(k_hash_to_g2_msgs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, m, (uint8_t*)c->misc.p);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out96, c->misc.p, n * 96, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out, c->misc.p, n * ob, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return DGPU_OK;
+}
+
+int dgpu_hash_to_g2(dgpu_ctx* c, size_t n, const uint8_t* msg32, uint8_t* out96) {
+  if (!c || !msg32 || !out96) return set_err(DGPU_EINVAL, "null argument");
+  std::vector<uint32_t> len(n, 32);
+  return dgpu_hash_to_curve(c, DGPU_SCHEME_CHAINED, n, msg32, 32, len.data(), out96);
 }
 
 int dgpu_hash_to_g1(dgpu_ctx* c, int scheme, size_t n, const uint8_t* msg32, uint8_t* out48) {
   if (!c || !msg32 || !out48) return set_err(DGPU_EINVAL, "null argument");
   if (!sig_on_g1(scheme)) return set_err(DGPU_EINVAL, "scheme %d does not sign on G1", scheme);
-  if (n == 0) return DGPU_OK;
-  std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  int rc;
-  if ((rc = c->in_sigs.ensure(n * 32))) return rc;
-  if ((rc = c->misc.ensure(n * 48))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->in_sigs.p, msg32, n * 32, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_hash_to_g1_msgs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, (const uint8_t*)c->in_sigs.p,
-                     scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, (uint8_t*)c->misc.p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out48, c->misc.p, n * 48, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  return DGPU_OK;
+  std::vector<uint32_t> len(n, 32);
+  return dgpu_hash_to_curve(c, scheme, n, msg32, 32, len.data(), out48);
 }
+
+}  // extern "C"
 
 static scalar256 scalar_from_be32(const uint8_t* b) {
   scalar256 k;
@@ -817,6 +1083,57 @@ static scalar256 scalar_from_be32(const uint8_t* b) {
   return k;
 }
 
+extern "C" {
+
+int dgpu_sign(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n, const uint8_t* msgs, size_t msg_stride,
+              const uint32_t* msg_len, uint8_t* out_sigs) {
+  if (!c || !sk_be32 || !msg_len || !out_sigs || (!msgs && msg_stride)) return set_err(DGPU_EINVAL, "null argument");
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (n == 0) return DGPU_OK;
+  for (size_t i = 0; i < n; ++i)
+    if (msg_len[i] > msg_stride) return set_err(DGPU_EINVAL, "msg_len[%zu]=%u > msg_stride", i, msg_len[i]);
+  const bool g1 = sig_on_g1(scheme);
+  const size_t ob = g1 ? 48 : 96;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  int rc;
+  if ((rc = c->in_msgs.ensure(n * msg_stride + 1)) || (rc = c->in_msg_len.ensure(n * 4)) ||
+      (rc = c->misc.ensure(n * ob)))
+    return rc;
+  if (msg_stride) HIP_TRY(hipMemcpyAsync(c->in_msgs.p, msgs, n * msg_stride, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->in_msg_len.p, msg_len, n * 4, hipMemcpyHostToDevice, s));
+  const msg_src m = raw_src((const uint8_t*)c->in_msgs.p, msg_stride, (const uint32_t*)c->in_msg_len.p);
+  hipLaunchKernelGGL(k_sign_msgs, dim3(grid_for(n, 64)), dim3(64), 0, s, n, m, g1 ? 1 : 0,
+                     scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, scalar_from_be32(sk_be32), (uint8_t*)c->misc.p, ob);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out_sigs, c->misc.p, n * ob, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+int dgpu_decode_g1_points(dgpu_ctx* c, size_t n, const uint8_t* in48, int* rc_out, uint8_t* xy96) {
+  if (!c || !in48 || !rc_out) return set_err(DGPU_EINVAL, "null argument");
+  if (n == 0) return DGPU_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  int rc;
+  if ((rc = c->in_msgs.ensure(n * 48)) || (rc = c->misc.ensure(n * (4 + 96)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->in_msgs.p, in48, n * 48, hipMemcpyHostToDevice, s));
+  int* d_rc = (int*)c->misc.p;
+  uint8_t* d_xy = (uint8_t*)c->misc.p + n * 4;
+  hipLaunchKernelGGL(k_decode_g1_points, dim3(grid_for(n, 64)), dim3(64), 0, s, n, (const uint8_t*)c->in_msgs.p, d_rc,
+                     d_xy);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(rc_out, d_rc, n * 4, hipMemcpyDeviceToHost, s));
+  if (xy96) HIP_TRY(hipMemcpyAsync(xy96, d_xy, n * 96, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
 int dgpu_derive_pubkey(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, uint8_t* pk_out, size_t pk_len) {
   if (!c || !sk_be32 || !pk_out) return set_err(DGPU_EINVAL, "null argument");
   if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
@@ -824,6 +1141,7 @@ int dgpu_derive_pubkey(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, uint8_t*
   if (pk_len != want) return set_err(DGPU_EINVAL, "pk_len must be %zu", want);
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
+  stream_order ord(c, c->stream);
   int rc = c->misc.ensure(128);
   if (rc) return rc;
   if (sig_on_g1(scheme))
@@ -850,12 +1168,21 @@ int dgpu_make_chain(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n_se
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  stream_order ord(c, s);
   int rc;
   DevBuf d_first, d_prev, d_plen, d_sigs;
-  if ((rc = d_first.ensure(n_seg * 8))) return rc;
-  if ((rc = d_prev.ensure(n_seg * 96))) { d_first.release(); return rc; }
-  if ((rc = d_plen.ensure(n_seg * 4))) { d_first.release(); d_prev.release(); return rc; }
-  if ((rc = d_sigs.ensure(n_seg * seg_len * 96))) { d_first.release(); d_prev.release(); d_plen.release(); return rc; }
+  auto cleanup = [&]() {
+    hipStreamSynchronize(s);
+    d_first.release();
+    d_prev.release();
+    d_plen.release();
+    d_sigs.release();
+  };
+  if ((rc = d_first.ensure(n_seg * 8)) || (rc = d_prev.ensure(n_seg * 96)) || (rc = d_plen.ensure(n_seg * 4)) ||
+      (rc = d_sigs.ensure(n_seg * seg_len * 96))) {
+    cleanup();
+    return rc;
+  }
   std::vector<uint8_t> pv(n_seg * 96, 0);
   std::vector<uint32_t> pl(n_seg, 0);
   if (chained) {
@@ -885,7 +1212,7 @@ int dgpu_make_chain(dgpu_ctx* c, int scheme, const uint8_t* sk_be32, size_t n_se
   if (e == hipSuccess) e = hipMemcpyAsync(sigs_out, d_sigs.p, n_seg * seg_len * 96, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) ret = set_err(DGPU_EDEVICE, "make_chain: %s", hipGetErrorString(e));
-  d_first.release(); d_prev.release(); d_plen.release(); d_sigs.release();
+  cleanup();
   return ret;
 }
 
@@ -896,6 +1223,9 @@ int dgpu_set_group(dgpu_ctx* c, int t, int n, const uint8_t* commits48) {
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  // the group's tables may still be read by an earlier asynchronous recovery
+  HIP_TRY(hipEventSynchronize(c->done));
   int rc;
   if ((rc = c->misc.ensure(t * 48 + t * 4))) return rc;
   if ((rc = c->grp_commits.ensure((size_t)t * 2 * FP_LIMBS * 4))) return rc;
@@ -908,6 +1238,7 @@ int dgpu_set_group(dgpu_ctx* c, int t, int n, const uint8_t* commits48) {
   std::vector<int> hrc(t);
   HIP_TRY(hipMemcpyAsync(hrc.data(), d_rc, t * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  c->grp_t = 0;
   for (int j = 0; j < t; ++j)
     if (hrc[j] != DEC_OK) return set_err(DGPU_EINVAL, "group commitment %d rejected (decode code %d)", j, hrc[j]);
   hipLaunchKernelGGL(k_pubpoly_table, dim3(grid_for(n, 64)), dim3(64), 0, s, n, t, (const uint32_t*)c->grp_commits.p,
@@ -930,6 +1261,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
   const size_t items = n_rounds * m;
   if (items > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "batch too large (%zu items)", items);
+  const uint32_t* consts = (const uint32_t*)c->eng_consts.p;
   int rc;
   if ((rc = c->rec_hidx.ensure(items * 4))) return rc;
   if ((rc = c->rec_pk.ensure(items * 2 * FP_LIMBS * 4))) return rc;
@@ -957,7 +1289,8 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
                      (uint32_t*)c->rec_pk.p, (uint32_t*)c->rec_idx.p, st);
   HIP_TRY(hipGetLastError());
   // VerifyPartial of every partial: e(Eval(i), H(msg)) e(-g1, sig) == 1 on the engine
-  if ((rc = eng_pairing_locked(c, items, h, sg, st, s, n_rounds, hidx, (const uint32_t*)c->rec_pk.p))) return rc;
+  if ((rc = eng_pairing_locked(c, consts, items, h, sg, st, s, n_rounds, hidx, (const uint32_t*)c->rec_pk.p)))
+    return rc;
   uint32_t* rpts = (uint32_t*)c->rec_pts.p;
   uint32_t* rpk = (uint32_t*)c->rec_vpk.p;
   uint8_t* rst = (uint8_t*)c->rec_st.p;
@@ -986,7 +1319,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
                      (const uint32_t*)part, d_out, rpts, rst);
   HIP_TRY(hipGetLastError());
   // VerifyRecovered: e(C_0, H(msg)) e(-g1, sig) == 1
-  if ((rc = eng_pairing_locked(c, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;
+  if ((rc = eng_pairing_locked(c, consts, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;
   mark(c, s, "recover_verdict");
   hipLaunchKernelGGL(k_recover_verdict, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds, rst, d_out, d_ok);
   HIP_TRY(hipGetLastError());
@@ -1007,6 +1340,7 @@ int dgpu_recover_batch_device(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msg
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  stream_order ord(c, s);
   return recover_device_locked(c, n_rounds, d_msgs32, m, d_partials, partial_stride, d_partial_len, d_out_sigs96,
                                d_ok, d_status, s);
 }
@@ -1021,6 +1355,7 @@ int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size
   if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  stream_order ord(c, s);
   const size_t items = n_rounds * m;
   for (size_t i = 0; i < items; ++i)
     if (partial_len[i] > partial_stride) return set_err(DGPU_EINVAL, "partial_len[%zu] > stride", i);
@@ -1063,9 +1398,18 @@ int dgpu_make_partials(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
+  stream_order ord(c, s);
   int rc;
   DevBuf d_msgs, d_h, d_si, d_lb, d_sh, d_out;
-  auto cleanup = [&]() { d_msgs.release(); d_h.release(); d_si.release(); d_lb.release(); d_sh.release(); d_out.release(); };
+  auto cleanup = [&]() {
+    hipStreamSynchronize(s);
+    d_msgs.release();
+    d_h.release();
+    d_si.release();
+    d_lb.release();
+    d_sh.release();
+    d_out.release();
+  };
   if ((rc = d_msgs.ensure(n_rounds * 32)) || (rc = d_h.ensure(n_rounds * G2A_WORDS * 4)) ||
       (rc = d_si.ensure(items * 4)) || (rc = d_lb.ensure(items * 4)) || (rc = d_sh.ensure(n_shares * sizeof(scalar256))) ||
       (rc = d_out.ensure(items * 98))) {
@@ -1095,3 +1439,5 @@ int dgpu_make_partials(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size
 }
 
 }  // extern "C"
+
+#include "multi_gpu.h"

@@ -85,9 +85,19 @@ DG_FN g1j g1_mul_absx(const g1j& p) {
   return r;
 }
 
+// map_to_curve of the two field elements in a 128-byte expand_message_xmd
+// output, then cofactor clearing by h_eff = 1 - x = 1 + |x|.
+template <bool INL>
+DG_FN g1j hash_to_g1_from_uni(const uint32_t uni[32]) {
+  const fp u0 = fp_from_be64_words(uni);
+  const fp u1 = fp_from_be64_words(uni + 16);
+  const g1j q = INL ? g1_add_body(map_to_curve_sswu_iso11_body(u0), map_to_curve_sswu_iso11_body(u1))
+                   : g1_add(map_to_curve_sswu_iso11(u0), map_to_curve_sswu_iso11(u1));
+  return g1_add_body(q, g1_mul_absx(q));
+}
+
 // hash_to_curve for G1 of a 32-byte digest; g1dst selects the G1 suite's DST
 // (bls-unchained-g1-rfc9380) over the G2 suite's (bls-unchained-on-g1).
-// Cofactor clearing by h_eff = 1 - x = 1 + |x|.
 template <bool INL>
 DG_FN g1j hash_to_g1_t(const uint32_t msg[8], bool g1dst) {
   uint32_t uni[32];
@@ -95,11 +105,7 @@ DG_FN g1j hash_to_g1_t(const uint32_t msg[8], bool g1dst) {
     expand_xmd<true, 4>(uni, msg);
   else
     expand_xmd<false, 4>(uni, msg);
-  const fp u0 = fp_from_be64_words(uni);
-  const fp u1 = fp_from_be64_words(uni + 16);
-  const g1j q = INL ? g1_add_body(map_to_curve_sswu_iso11_body(u0), map_to_curve_sswu_iso11_body(u1))
-                   : g1_add(map_to_curve_sswu_iso11(u0), map_to_curve_sswu_iso11(u1));
-  return g1_add_body(q, g1_mul_absx(q));
+  return hash_to_g1_from_uni<INL>(uni);
 }
 
 DG_NOINL g1j hash_to_g1(const uint32_t msg[8], bool g1dst) { return hash_to_g1_t<false>(msg, g1dst); }
@@ -140,31 +146,35 @@ DG_NOINL int g1_decompress_sig(g1a* out, const uint8_t* in) {
 
 #ifndef DG_NO_KERNELS  // (the host-emulation test build takes the device functions only)
 // ---------------------------------------------------------------- kernels
-// H(m) in G1 for m = SHA-256(BE64(round)) (unchained DigestMessage,
-// chain/verify.go:24-32): X, Y into h_out ([x, y][limb][n]), Z into z_out.
-__global__ void __launch_bounds__(256, 2) k_hash_to_g1_beacons(size_t n, const uint64_t* __restrict__ rounds, int g1dst,
+// H(m) in G1 of each item's message (msg_src: the unchained DigestMessage
+// SHA-256(BE64(round)), chain/verify.go:24-32, or raw bytes): X, Y into h_out
+// ([x, y][limb][n]), Z into z_out.
+__global__ void __launch_bounds__(256, 2) k_hash_to_g1_beacons(size_t n, msg_src m, int g1dst,
                                                              uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t msg[8];
-  drand_digest(msg, nullptr, 0u, rounds[i]);
-  const g1j h = hash_to_g1_t<true>(msg, g1dst != 0);
+  uint32_t uni[32];
+  if (g1dst)
+    msg_expand<true, 4>(m, i, uni);
+  else
+    msg_expand<false, 4>(m, i, uni);
+  const g1j h = hash_to_g1_from_uni<true>(uni);
   st_fp(h_out, n, i, h.x);
   st_fp(h_out + FP_WORDS * n, n, i, h.y);
   st_fp(z_out, n, i, h.z);
 }
 
-// H(m) in G1 of raw 32-byte messages, compressed (parity/debug: dgpu_hash_to_g1)
-__global__ void __launch_bounds__(256) k_hash_to_g1_msgs(size_t n, const uint8_t* __restrict__ msgs, int g1dst,
-                                                          uint8_t* __restrict__ out48) {
+// H(m) in G1 of raw messages of any length, compressed (parity surface:
+// dgpu_hash_to_g1 / dgpu_hash_to_curve)
+__global__ void __launch_bounds__(256) k_hash_to_g1_msgs(size_t n, msg_src m, int g1dst, uint8_t* __restrict__ out48) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t msg[8];
-  for (int w = 0; w < 8; ++w) {
-    const uint8_t* b = msgs + i * 32 + 4 * w;
-    msg[w] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
-  }
-  const g1j h = hash_to_g1(msg, g1dst != 0);
+  uint32_t uni[32];
+  if (g1dst)
+    msg_expand<true, 4>(m, i, uni);
+  else
+    msg_expand<false, 4>(m, i, uni);
+  const g1j h = hash_to_g1_from_uni<false>(uni);
   const bool inf = g1_is_inf(h);
   g1_compress(out48 + i * 48, inf ? g1a{fp_zero(), fp_zero()} : g1_to_affine(h), inf);
 }
@@ -201,13 +211,13 @@ __global__ void __launch_bounds__(256) k_g1_batch_affine(size_t n, uint32_t* __r
 
 // G1 signature decode + membership: affine [x, y][limb][n], status ST_*.
 __global__ void __launch_bounds__(256, 2) k_decode_g1_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
-                                                         const uint32_t* __restrict__ sig_len,
+                                                         const uint32_t* __restrict__ sig_len, msg_src m,
                                                          uint32_t* __restrict__ sig_out, uint8_t* __restrict__ status) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t st;
   g1a p{fp_zero(), fp_zero()};
-  if (sig_len[i] != 48) {
+  if (sig_len[i] != 48 || msg_bad_record(m, i)) {
     st = ST_DECODE;
   } else {
     uint8_t buf[48];
@@ -253,6 +263,54 @@ __global__ void __launch_bounds__(256) k_sign_step_g1(size_t S, const uint64_t* 
   uint8_t out[48];
   g1_compress(out, inf ? g1a{fp_zero(), fp_zero()} : g1_to_affine(sg), inf);
   for (int k = 0; k < 48; ++k) sig_out[s * sig_stride + k] = out[k];
+}
+
+// Sign n raw messages with one secret (test/tool surface of key.Scheme.Sign /
+// AuthScheme.Sign, key/curve.go:36-39; key/curve_test.go:10-30 signs this
+// way): sig = sk * H(msg), compressed.  on_g1: 48-byte G1 signatures under
+// the DST g1dst selects; else 96-byte G2 signatures.
+__global__ void __launch_bounds__(64) k_sign_msgs(size_t n, msg_src m, int on_g1, int g1dst, scalar256 sk,
+                                                  uint8_t* __restrict__ out, size_t out_stride) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (on_g1) {
+    uint32_t uni[32];
+    if (g1dst)
+      msg_expand<true, 4>(m, i, uni);
+    else
+      msg_expand<false, 4>(m, i, uni);
+    const g1j sg = g1_mul_words(hash_to_g1_from_uni<false>(uni), sk.w, 8);
+    const bool inf = g1_is_inf(sg);
+    g1_compress(out + i * out_stride, inf ? g1a{fp_zero(), fp_zero()} : g1_to_affine(sg), inf);
+  } else {
+    uint32_t uni[64];
+    msg_expand<false, 8>(m, i, uni);
+    const fp2 u0{fp_from_be64_words(uni), fp_from_be64_words(uni + 16)};
+    const fp2 u1{fp_from_be64_words(uni + 32), fp_from_be64_words(uni + 48)};
+    const g2j h = g2_clear_cofactor(g2_add(map_to_curve_sswu_iso3(u0), map_to_curve_sswu_iso3(u1)));
+    const g2j sg = g2_mul_words(h, sk.w, 8);
+    const bool inf = g2_is_inf(sg);
+    g2_compress(out + i * out_stride, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(sg), inf);
+  }
+}
+
+// Batch decode of compressed G1 points (48 bytes each, kilic G1.FromCompressed
+// semantics (R) with the endomorphism membership test): public keys and
+// commitments (chain/convert.go:20-23, deploy/*/group.toml).  rc[i] = DEC_*,
+// out (optional) = canonical big-endian x || y (96 bytes) of decoded points.
+__global__ void __launch_bounds__(64) k_decode_g1_points(size_t n, const uint8_t* __restrict__ in48,
+                                                         int* __restrict__ rc, uint8_t* __restrict__ out96) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t buf[48];
+  for (int k = 0; k < 48; ++k) buf[k] = in48[i * 48 + k];
+  g1a p{fp_zero(), fp_zero()};
+  const int r = g1_decompress_sig(&p, buf);
+  rc[i] = r;
+  if (out96) {
+    fp_std_to_be48(fp_from_mont(p.x), out96 + i * 96);
+    fp_std_to_be48(fp_from_mont(p.y), out96 + i * 96 + 48);
+  }
 }
 
 #endif  // DG_NO_KERNELS

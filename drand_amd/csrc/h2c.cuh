@@ -112,6 +112,39 @@ DG_NOINL void drand_digest(uint32_t out[8], const uint8_t* prev, uint32_t prev_l
   for (int i = 0; i < 8; ++i) out[i] = s.h[i];
 }
 
+// SHA-256 continued from state `s` (which has absorbed `pre_bytes` bytes, a
+// multiple of 64) over L more bytes get(0) .. get(L - 1), with the padding
+// of the whole (pre_bytes + L)-byte message.  Streams block by block, so any
+// length works (raw VerifyRecovered messages, key/curve.go:36-39).
+template <class Get>
+DG_FN void sha_stream(sha_state& s, uint32_t L, uint64_t pre_bytes, Get&& get) {
+  const uint32_t nblk = (L + 9 + 63) / 64;
+  const uint64_t bitlen = (pre_bytes + L) * 8;
+#pragma unroll 1
+  for (uint32_t bidx = 0; bidx < nblk; ++bidx) {
+    uint32_t blk[16];
+#pragma unroll 1
+    for (int wd = 0; wd < 16; ++wd) {
+      uint32_t word = 0;
+      for (int byte = 0; byte < 4; ++byte) {
+        const uint32_t pos = bidx * 64 + wd * 4 + byte;
+        uint32_t v;
+        if (pos < L)
+          v = get(pos);
+        else if (pos == L)
+          v = 0x80;
+        else if (pos >= nblk * 64 - 8)
+          v = (uint32_t)(bitlen >> (8 * (nblk * 64 - 1 - pos))) & 0xff;
+        else
+          v = 0;
+        word = (word << 8) | v;
+      }
+      blk[wd] = word;
+    }
+    sha_compress(s, blk);
+  }
+}
+
 // ================================================================ expand_message_xmd
 // DST bytes as big-endian words: "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_" (43 bytes)
 // followed by I2OSP(43, 1): DST_prime = 44 bytes = 11 words.
@@ -124,6 +157,60 @@ constexpr uint32_t DST_G2_PRIME[11] = {0x424c535f, 0x5349475f, 0x424c5331, 0x323
 template <bool G1DST>
 DG_FN uint32_t dst_word(int i) {
   return (G1DST && i == 4) ? 0x47315f58u : DST_G2_PRIME[i];
+}
+
+// b1 .. b_ELL of expand_message_xmd from b0:
+//  bi: (b0 xor b_{i-1})(32) || i(1) || DST'(44) = 77 bytes, 2 blocks
+template <bool G1DST, int ELL>
+DG_FN void expand_xmd_tail(uint32_t out[8 * ELL], const uint32_t b0[8]) {
+  uint32_t prev[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) prev[i] = 0;
+  for (int idx = 1; idx <= ELL; ++idx) {
+    sha_state s = sha_init();
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) blk[i] = b0[i] ^ prev[i];
+    blk[8] = ((uint32_t)idx << 24) | (dst_word<G1DST>(0) >> 8);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) blk[8 + i] = (dst_word<G1DST>(i - 1) << 24) | (dst_word<G1DST>(i) >> 8);
+    sha_compress(s, blk);
+    // bytes 64..76: DST'[31..43] (13 bytes), 0x80, zeros, length 77*8 = 616
+    uint32_t blk2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) blk2[i] = 0;
+    blk2[0] = (dst_word<G1DST>(7) << 24) | (dst_word<G1DST>(8) >> 8);
+    blk2[1] = (dst_word<G1DST>(8) << 24) | (dst_word<G1DST>(9) >> 8);
+    blk2[2] = (dst_word<G1DST>(9) << 24) | (dst_word<G1DST>(10) >> 8);
+    blk2[3] = (dst_word<G1DST>(10) << 24) | 0x00800000u;
+    blk2[15] = 77 * 8;
+    sha_compress(s, blk2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      prev[i] = s.h[i];
+      out[(idx - 1) * 8 + i] = s.h[i];
+    }
+  }
+}
+
+// expand_message_xmd of an arbitrary-length message (len bytes at msg,
+// device or host memory): b0 = H(Z_pad || msg || I2OSP(32 ELL, 2) || 0x00 ||
+// DST'), streamed from the Z_pad midstate.
+template <bool G1DST, int ELL>
+DG_NOINL void expand_xmd_var(uint32_t out[8 * ELL], const uint8_t* msg, uint32_t len) {
+  sha_state s0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s0.h[i] = SHA_ZPAD_MIDSTATE[i];
+  sha_stream(s0, len + 47, 64, [&](uint32_t pos) -> uint32_t {
+    if (pos < len) return msg[pos];
+    const uint32_t k = pos - len;
+    if (k == 0) return (32u * ELL) >> 8;
+    if (k == 1) return (32u * ELL) & 0xffu;
+    if (k == 2) return 0u;
+    const uint32_t j = k - 3;  // DST' byte
+    return (dst_word<G1DST>((int)(j >> 2)) >> (24 - 8 * (j & 3))) & 0xffu;
+  });
+  expand_xmd_tail<G1DST, ELL>(out, s0.h);
 }
 
 // expand_message_xmd(msg (32 bytes), DST, 32 ELL bytes) -> 8 ELL big-endian words
@@ -157,37 +244,7 @@ DG_NOINL void expand_xmd(uint32_t out[8 * ELL], const uint32_t msg[8]) {
     blk2[15] = 143 * 8;
     sha_compress(s0, blk2);
   }
-  uint32_t b0[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) b0[i] = s0.h[i];
-  uint32_t prev[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) prev[i] = 0;
-  for (int idx = 1; idx <= ELL; ++idx) {
-    sha_state s = sha_init();
-    uint32_t blk[16];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) blk[i] = b0[i] ^ prev[i];
-    blk[8] = ((uint32_t)idx << 24) | (dst_word<G1DST>(0) >> 8);
-#pragma unroll
-    for (int i = 1; i < 8; ++i) blk[8 + i] = (dst_word<G1DST>(i - 1) << 24) | (dst_word<G1DST>(i) >> 8);
-    sha_compress(s, blk);
-    // bytes 64..76: DST'[31..43] (13 bytes), 0x80, zeros, length 77*8 = 616
-    uint32_t blk2[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) blk2[i] = 0;
-    blk2[0] = (dst_word<G1DST>(7) << 24) | (dst_word<G1DST>(8) >> 8);
-    blk2[1] = (dst_word<G1DST>(8) << 24) | (dst_word<G1DST>(9) >> 8);
-    blk2[2] = (dst_word<G1DST>(9) << 24) | (dst_word<G1DST>(10) >> 8);
-    blk2[3] = (dst_word<G1DST>(10) << 24) | 0x00800000u;
-    blk2[15] = 77 * 8;
-    sha_compress(s, blk2);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      prev[i] = s.h[i];
-      out[(idx - 1) * 8 + i] = s.h[i];
-    }
-  }
+  expand_xmd_tail<G1DST, ELL>(out, s0.h);
 }
 
 DG_NOINL void expand_xmd_g2(uint32_t out[64], const uint32_t msg[8]) { expand_xmd<false, 8>(out, msg); }

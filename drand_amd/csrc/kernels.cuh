@@ -4,7 +4,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "h2c.cuh"
-#include "pairing.cuh"
 
 namespace dgpu {
 
@@ -70,41 +69,63 @@ struct g1_key {  // public key prepared for line evaluation: (-x, y), Montgomery
   fp neg_x, y;
 };
 
-// ---------------------------------------------------------------- kernels
-// H(m) for m = DigestMessage(round, prev) (chain/verify.go:24-32), Jacobian:
-// X, Y into h_out (the affine slots, finished in place by k_g2_batch_affine),
-// Z into z_out.  chained != 0: prev bytes are hashed (any length up to prev_stride).
-__global__ void __launch_bounds__(256) k_hash_to_g2_beacons(size_t n, const uint64_t* __restrict__ rounds,
-                                                             const uint8_t* __restrict__ prev, size_t prev_stride,
-                                                             const uint32_t* __restrict__ prev_len, int chained,
-                                                             uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t msg[8];
-  uint32_t plen = chained ? prev_len[i] : 0u;
-  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, plen, rounds[i]);
-  g2j h = hash_to_g2(msg);
-  st_g2a(h_out, n, i, g2a{h.x, h.y});
-  st_fp(z_out, n, i, h.z.c0);
-  st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
+// Where a batch item's message comes from: drand's DigestMessage of a beacon
+// record (chain/verify.go:24-32: SHA-256(prev || BE64(round)), prev ignored
+// unless chained), or raw message bytes (msgs != nullptr: key.Scheme.
+// VerifyRecovered(pk, msg, sig) with any msg, key/curve.go:36-39,
+// chain/beacon/chain.go:165).  A record whose length exceeds its stride
+// (prev_len > prev_stride, msg_len > msg_stride) is never read past the
+// stride and fails verification (msg_bad_record -> ST_DECODE).
+struct msg_src {
+  const uint64_t* rounds;
+  const uint8_t* prev;
+  size_t prev_stride;
+  const uint32_t* prev_len;
+  int chained;
+  const uint8_t* msgs;
+  size_t msg_stride;
+  const uint32_t* msg_len;
+};
+
+__device__ __forceinline__ uint32_t clamp_len(uint32_t len, size_t stride) {
+  return (size_t)len > stride ? (uint32_t)stride : len;
 }
 
+__device__ __forceinline__ bool msg_bad_record(const msg_src& m, size_t i) {
+  if (m.msgs) return (size_t)m.msg_len[i] > m.msg_stride;
+  return m.chained && (size_t)m.prev_len[i] > m.prev_stride;
+}
+
+// drand digest of a beacon record (32 bytes as 8 big-endian words)
+__device__ __forceinline__ void msg_digest(const msg_src& m, size_t i, uint32_t msg[8]) {
+  const uint32_t plen = m.chained ? clamp_len(m.prev_len[i], m.prev_stride) : 0u;
+  drand_digest(msg, m.chained ? m.prev + i * m.prev_stride : nullptr, plen, m.rounds[i]);
+}
+
+// expand_message_xmd of item i's message under DST G1DST with ELL 32-byte blocks
+template <bool G1DST, int ELL>
+__device__ __forceinline__ void msg_expand(const msg_src& m, size_t i, uint32_t* uni) {
+  if (m.msgs) {
+    expand_xmd_var<G1DST, ELL>(uni, m.msgs + i * m.msg_stride, clamp_len(m.msg_len[i], m.msg_stride));
+  } else {
+    uint32_t msg[8];
+    msg_digest(m, i, msg);
+    expand_xmd<G1DST, ELL>(uni, msg);
+  }
+}
+
+// ---------------------------------------------------------------- kernels
 // The per-round hash to G2 as three launches (the fused kernel needs 512
 // registers per lane -- one wave per SIMD -- and 6 KB of scratch; each stage
 // alone is far lighter, and the SSWU stage has 2n independent items):
-//   k_h2c_field   DigestMessage + expand_message_xmd -> u0, u1 ([4 fp][n])
+//   k_h2c_field   message (DigestMessage or raw) + expand_message_xmd -> u0, u1 ([4 fp][n])
 //   k_h2c_sswu    SSWU + 3-isogeny of each of the 2n field elements -> Jacobian ([2][6 fp][n])
 //   k_h2c_finish  Q0 + Q1, cofactor clearing -> X, Y (h_out) and Z (z_out)
-__global__ void __launch_bounds__(256) k_h2c_field(size_t n, const uint64_t* __restrict__ rounds,
-                                                    const uint8_t* __restrict__ prev, size_t prev_stride,
-                                                    const uint32_t* __restrict__ prev_len, int chained,
-                                                    uint32_t* __restrict__ u_out) {
+__global__ void __launch_bounds__(256) k_h2c_field(size_t n, msg_src m, uint32_t* __restrict__ u_out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t msg[8];
-  drand_digest(msg, chained ? prev + i * prev_stride : nullptr, chained ? prev_len[i] : 0u, rounds[i]);
   uint32_t uni[64];
-  expand_xmd_g2(uni, msg);
+  msg_expand<false, 8>(m, i, uni);
 #pragma unroll 1
   for (int k = 0; k < 4; ++k) st_fp(u_out + (size_t)k * FP_WORDS * n, n, i, fp_from_be64_words(uni + 16 * k));
 }
@@ -174,17 +195,16 @@ __global__ void __launch_bounds__(256) k_g2_batch_affine(size_t n, uint32_t* __r
   }
 }
 
-// H(m) for raw 32-byte messages (parity/debug: dgpu_hash_to_g2)
-__global__ void __launch_bounds__(256) k_hash_to_g2_msgs(size_t n, const uint8_t* __restrict__ msgs,
-                                                          uint8_t* __restrict__ out96) {
+// H(m) for raw messages of any length, compressed (parity surface:
+// dgpu_hash_to_g2 / dgpu_hash_to_curve)
+__global__ void __launch_bounds__(256) k_hash_to_g2_msgs(size_t n, msg_src m, uint8_t* __restrict__ out96) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint32_t msg[8];
-  for (int w = 0; w < 8; ++w) {
-    const uint8_t* b = msgs + i * 32 + 4 * w;
-    msg[w] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
-  }
-  g2j h = hash_to_g2(msg);
+  uint32_t uni[64];
+  msg_expand<false, 8>(m, i, uni);
+  const fp2 u0{fp_from_be64_words(uni), fp_from_be64_words(uni + 16)};
+  const fp2 u1{fp_from_be64_words(uni + 32), fp_from_be64_words(uni + 48)};
+  g2j h = g2_clear_cofactor(g2_add(map_to_curve_sswu_iso3(u0), map_to_curve_sswu_iso3(u1)));
   bool inf = g2_is_inf(h);
   g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h);
   g2_compress(out96 + i * 96, a, inf);
@@ -208,14 +228,16 @@ __global__ void __launch_bounds__(256) k_digest(size_t n, const uint64_t* __rest
 }
 
 // Signature decode (kilic G2.FromCompressed semantics (R)) + G2 membership.
+// A record whose message part overruns its stride (msg_bad_record) fails as a
+// decode error without its signature being read.
 __global__ void __launch_bounds__(256, 4) k_decode_g2_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
-                                                         const uint32_t* __restrict__ sig_len,
+                                                         const uint32_t* __restrict__ sig_len, msg_src m,
                                                          uint32_t* __restrict__ sig_out, uint8_t* __restrict__ status) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t st;
   g2a p{fp2_zero(), fp2_zero()};
-  if (sig_len[i] != 96) {
+  if (sig_len[i] != 96 || msg_bad_record(m, i)) {
     st = ST_DECODE;
   } else {
     uint8_t buf[96];
@@ -226,23 +248,6 @@ __global__ void __launch_bounds__(256, 4) k_decode_g2_sigs(size_t n, const uint8
   }
   st_g2a(sig_out, n, i, p);
   status[i] = st;
-}
-
-// e(pk, H) * e(-g1, sig) == 1 per round.
-__global__ void __launch_bounds__(256) k_pairing_check(size_t n, const uint32_t* __restrict__ h_pts,
-                                                        const uint32_t* __restrict__ sig_pts,
-                                                        uint8_t* __restrict__ status, g1_key pk) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t st = status[i];
-  if (st != ST_OK) return;  // decode verdicts are final
-  g2a h = ld_g2a(h_pts, n, i);
-  g2a s = ld_g2a(sig_pts, n, i);
-  fp g1_negx = fp_neg(C_G1_X);
-  // pair 2 is (-g1, sig): (-x(-g1), y(-g1)) = (-x_g1, -y_g1)
-  fp12 f = miller_loop_2(h, pk.neg_x, pk.y, s, g1_negx, C_G1_NEG_Y);
-  fp12 e = final_exponentiation(f);
-  status[i] = fp12_is_one(e) ? ST_OK : ST_PAIRING;
 }
 
 // Synthetic-chain generator (test-data tool, not the verify path): one step
@@ -296,9 +301,12 @@ __global__ void k_derive_pubkey(scalar256 sk, uint8_t* __restrict__ out48) {
 // with R_i the pre-cofactor hash point (h_eff applied once per checked node,
 // by linearity) and d_i = e(pk, H_i) e(-g1, sig_i).  Jacobian G2 arrays are
 // SoA [6 Fp][limb][index].
-// SplitMix64-derived nonzero 64-bit coefficient for round `round` under `seed`.
-__device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t round) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (round + 1);
+// SplitMix64-derived nonzero 64-bit coefficient for batch position `idx`
+// under `seed`.  Keyed on the position, never on the record's Round field:
+// two records with equal Round (duplicated store rows) must get independent
+// coefficients, or a +D / -D pair of corruptions cancels in every node.
+__device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   z ^= z >> 31;
@@ -315,8 +323,7 @@ __device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t round) {
 // the identity).  2n threads: j < n computes P_j, j >= n computes S_{j-n}.
 // Two waves per SIMD with psi(q) recomputed at its digits measured fastest
 // (1 or 3 waves, or psi(q) held live: 120 vs 123-157 ms per 1M rounds).
-__global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, const uint64_t* __restrict__ rounds,
-                                                            uint64_t seed, const uint32_t* __restrict__ r_aff,
+__global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, uint64_t seed, const uint32_t* __restrict__ r_aff,
                                                             const uint32_t* __restrict__ sig_pts,
                                                             const uint8_t* __restrict__ status,
                                                             uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
@@ -328,7 +335,7 @@ __global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, const uint64_t*
   if (status[i] == ST_OK) {
     const g2a q = ld_g2a(sig ? sig_pts : r_aff, n, i);
     if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) {
-      const uint64_t z = rlc_coeff(seed, rounds[i]);
+      const uint64_t z = rlc_coeff(seed, i);
       acc = g2_mul2_naf32_affine<true>(q, q, (uint32_t)z, (uint32_t)(z >> 32));
     }
   }
@@ -349,31 +356,6 @@ __global__ void __launch_bounds__(256) k_rlc_level(size_t n_in, const uint32_t* 
   g2j P = ld_g2j(in, n_in, a);
   if (b < n_in) P = g2_add_body(P, ld_g2j(in, n_in, b));
   st_g2j(sig ? s_out : p_out, n_out, j, P);
-}
-
-// Check candidate nodes of one level: fail[c] = 1 iff
-// e(pk, h_eff * P) * e(-g1, S) != 1 for node idx[c].
-__global__ void __launch_bounds__(256) k_rlc_check(size_t n_cand, const uint32_t* __restrict__ idx, size_t n_level,
-                                                    const uint32_t* __restrict__ p_lvl,
-                                                    const uint32_t* __restrict__ s_lvl, g1_key pk,
-                                                    uint8_t* __restrict__ fail) {
-  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n_cand) return;
-  size_t j = idx[c];
-  g2j P = g2_clear_cofactor(ld_g2j(p_lvl, n_level, j));
-  g2j S = ld_g2j(s_lvl, n_level, j);
-  bool pi = g2_is_inf(P), si = g2_is_inf(S);
-  bool ok;
-  if (pi && si) {
-    ok = true;
-  } else if (pi || si) {
-    ok = false;  // e(Q, .) of a non-trivial prime-order point alone is never 1
-  } else {
-    g2a Pa = g2_to_affine(P), Sa = g2_to_affine(S);
-    fp12 f = miller_loop_2(Pa, pk.neg_x, pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);
-    ok = fp12_is_one(final_exponentiation(f));
-  }
-  fail[c] = ok ? 0 : 1;
 }
 
 // Candidate nodes for the pairing engine: h[c] = affine h_eff * P, sg[c] =
@@ -403,6 +385,18 @@ __global__ void __launch_bounds__(256) k_rlc_fail(size_t n_cand, const uint8_t* 
   size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n_cand) return;
   fail[c] = (st[c] == ST_OK || st[c] == RLC_TRIVIAL) ? 0 : 1;
+}
+
+// Multi-GPU RLC: the per-device roots (P, S), gathered over RCCL as
+// [dev][P (G2J_WORDS), S (G2J_WORDS)] (each a stride-1 Jacobian SoA), summed
+// into one node (stride 1) that is checked once for the whole node.
+__global__ void k_rlc_sum_roots(int ndev, const uint32_t* __restrict__ roots, uint32_t* __restrict__ p_out,
+                                uint32_t* __restrict__ s_out) {
+  if (blockIdx.x != 0 || threadIdx.x >= 2) return;
+  const int w = threadIdx.x;  // 0: P, 1: S
+  g2j acc = ld_g2j(roots + w * G2J_WORDS, 1, 0);
+  for (int d = 1; d < ndev; ++d) acc = g2_add(acc, ld_g2j(roots + (size_t)d * 2 * G2J_WORDS + w * G2J_WORDS, 1, 0));
+  st_g2j(w ? s_out : p_out, 1, 0, acc);
 }
 
 // Mark the rounds of failing leaves.

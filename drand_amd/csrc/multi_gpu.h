@@ -1,0 +1,311 @@
+// Multi-GPU batch verification behind the C ABI (dgpu_multi_open /
+// dgpu_verify_multi).  Included at the end of capi.hip
+// (one translation unit: the kernels and the context live there).
+//
+// The reference's bulk caller walks the chain serially
+// (chain/beacon/sync_manager.go:188-222); every stored beacon carries its own
+// PreviousSig (chain/beacon.go:15), so round verdicts are independent and the
+// batch shards into contiguous round ranges, one per GPU, with no data-path
+// collective.  RCCL over xGMI moves only results:
+//  - per-round mode: one all-gather of the per-device verdict bitmaps (and
+//    reason bytes) -- shards are multiples of 8 rounds, so the gathered
+//    bitmaps concatenate into the batch's bitmap;
+//  - RLC mode: one all-gather of the per-device RLC roots (two Jacobian G2
+//    sums, 672 bytes), summed on device 0 and checked there with a single
+//    pairing (one final exponentiation for the whole node); only when that
+//    fails does each device descend its own tree (root first) to per-round
+//    verdicts, and the bitmaps are gathered as in per-round mode.
+// RCCL is loaded at dgpu_multi_open (dlopen), so the single-GPU library has
+// no link-time dependency on it.
+
+namespace {
+
+struct rccl_api {
+  void* h = nullptr;
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+int load_rccl(rccl_api& r) {
+  const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+  for (const char* nm : names) {
+    r.h = dlopen(nm, RTLD_NOW | RTLD_LOCAL);
+    if (r.h) break;
+  }
+  if (!r.h) return set_err(DGPU_EUNSUPPORTED, "RCCL not found (dlopen librccl.so.1: %s)", dlerror());
+  r.comm_init_all = (decltype(r.comm_init_all))dlsym(r.h, "ncclCommInitAll");
+  r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
+  r.all_gather = (decltype(r.all_gather))dlsym(r.h, "ncclAllGather");
+  r.group_start = (decltype(r.group_start))dlsym(r.h, "ncclGroupStart");
+  r.group_end = (decltype(r.group_end))dlsym(r.h, "ncclGroupEnd");
+  r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+  if (!r.comm_init_all || !r.comm_destroy || !r.all_gather || !r.group_start || !r.group_end || !r.error_string)
+    return set_err(DGPU_EUNSUPPORTED, "RCCL is missing a symbol");
+  return DGPU_OK;
+}
+
+#define NCCL_TRY(api, expr)                                                                            \
+  do {                                                                                                 \
+    ncclResult_t _r = (expr);                                                                          \
+    if (_r != ncclSuccess) return set_err(DGPU_EDEVICE, "%s: %s", #expr, (api).error_string(_r));    \
+  } while (0)
+
+// per-device buffers of the gathers
+struct multi_bufs {
+  DevBuf bits, reasons, all_bits, all_reasons, root, all_roots;
+};
+
+uint64_t splitmix_host(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+}  // namespace
+
+struct dgpu_multi {
+  int ndev = 0;
+  std::vector<int> devs;
+  std::vector<dgpu_ctx*> ctx;
+  std::vector<ncclComm_t> comm;
+  std::vector<multi_bufs> buf;
+  rccl_api api;
+  std::mutex mu;
+};
+
+extern "C" {
+
+int dgpu_multi_open(int ndev, const int* devs, dgpu_multi** out) {
+  if (!out || !devs || ndev < 1) return set_err(DGPU_EINVAL, "bad arguments");
+  *out = nullptr;
+  for (int i = 0; i < ndev; ++i)
+    for (int j = 0; j < i; ++j)
+      if (devs[i] == devs[j]) return set_err(DGPU_EINVAL, "device %d listed twice", devs[i]);
+  dgpu_multi* m = new dgpu_multi();
+  int rc = load_rccl(m->api);
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  m->ndev = ndev;
+  m->devs.assign(devs, devs + ndev);
+  m->buf.resize(ndev);
+  for (int i = 0; i < ndev; ++i) {
+    dgpu_ctx* c = nullptr;
+    if ((rc = dgpu_open(devs[i], &c))) {
+      std::string msg = g_last_error;
+      dgpu_multi_close(m);
+      return set_err(rc, "%s", msg.c_str());
+    }
+    m->ctx.push_back(c);
+  }
+  m->comm.resize(ndev);
+  ncclResult_t r = m->api.comm_init_all(m->comm.data(), ndev, devs);
+  if (r != ncclSuccess) {
+    std::string msg = m->api.error_string(r);
+    m->comm.clear();
+    dgpu_multi_close(m);
+    return set_err(DGPU_EDEVICE, "ncclCommInitAll: %s", msg.c_str());
+  }
+  *out = m;
+  return DGPU_OK;
+}
+
+void dgpu_multi_close(dgpu_multi* m) {
+  if (!m) return;
+  for (size_t i = 0; i < m->comm.size(); ++i)
+    if (m->comm[i]) m->api.comm_destroy(m->comm[i]);
+  for (size_t i = 0; i < m->ctx.size(); ++i) {
+    hipSetDevice(m->devs[i]);
+    for (DevBuf* b : {&m->buf[i].bits, &m->buf[i].reasons, &m->buf[i].all_bits, &m->buf[i].all_reasons,
+                      &m->buf[i].root, &m->buf[i].all_roots})
+      b->release();
+    dgpu_close(m->ctx[i]);
+  }
+  delete m;
+}
+
+int dgpu_multi_context(dgpu_multi* m, int k, dgpu_ctx** out) {
+  if (!m || !out || k < 0 || k >= m->ndev) return set_err(DGPU_EINVAL, "bad arguments");
+  *out = m->ctx[k];
+  return DGPU_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Run fn(k) for every device on its own host thread; the first failure's
+// code and message become this thread's.
+template <class Fn>
+int for_each_device(dgpu_multi* m, Fn&& fn) {
+  std::vector<int> rcs(m->ndev, DGPU_OK);
+  std::vector<std::string> errs(m->ndev);
+  std::vector<std::thread> th;
+  for (int k = 0; k < m->ndev; ++k)
+    th.emplace_back([&, k]() {
+      if (hipSetDevice(m->devs[k]) != hipSuccess) {
+        rcs[k] = DGPU_EDEVICE;
+        errs[k] = "hipSetDevice failed";
+        return;
+      }
+      rcs[k] = fn(k);
+      if (rcs[k]) errs[k] = g_last_error;
+    });
+  for (auto& t : th) t.join();
+  for (int k = 0; k < m->ndev; ++k)
+    if (rcs[k]) return set_err(rcs[k], "device %d: %s", m->devs[k], errs[k].c_str());
+  return DGPU_OK;
+}
+
+// status -> verdict bits / reasons of one device's shard
+int pack_shard_locked(dgpu_ctx* c, size_t cnt, uint8_t* d_bits, uint8_t* d_reason, hipStream_t s) {
+  if (cnt == 0) return DGPU_OK;
+  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((cnt + 7) / 8, 256)), dim3(256), 0, s, cnt,
+                     (const uint8_t*)c->status.p, d_bits);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(d_reason, c->status.p, cnt, hipMemcpyDeviceToDevice, s));
+  return DGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_len, size_t n, const uint64_t* rounds,
+                      const uint8_t* sigs, size_t sig_stride, const uint32_t* sig_len, const uint8_t* prev,
+                      size_t prev_stride, const uint32_t* prev_len, int mode, uint64_t rlc_seed,
+                      uint8_t* verdict_bits, uint8_t* reason) {
+  if (!m) return set_err(DGPU_EINVAL, "null handle");
+  if (n == 0) return DGPU_OK;
+  if (!verdict_bits) return set_err(DGPU_EINVAL, "null verdict buffer");
+  const bool chained = scheme == DGPU_SCHEME_CHAINED;
+  std::lock_guard<std::mutex> mlk(m->mu);
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (dgpu_ctx* c : m->ctx) locks.emplace_back(c->mu);
+  const int D = m->ndev;
+  size_t per = 0;
+  dgpu_shard_range(n, D, 0, nullptr, &per);  // shard 0 has the full per-device size
+  std::vector<key_entry*> keys(D, nullptr);
+  std::vector<verify_args> args(D);
+  int rc;
+  for (int k = 0; k < D; ++k) {
+    dgpu_ctx* c = m->ctx[k];
+    HIP_TRY(hipSetDevice(c->device));
+    if ((rc = get_key_locked(c, scheme, pk, pk_len, &keys[k]))) return rc;
+    size_t lo, hi;
+    dgpu_shard_range(n, D, k, &lo, &hi);
+    // RLC coefficients: an independent seed per device (positions restart at 0)
+    args[k] = verify_args{scheme, hi - lo, beacon_src(rounds + lo, chained ? prev + lo * prev_stride : nullptr,
+                                                      prev_stride, chained ? prev_len + lo : nullptr, chained),
+                          sigs + lo * sig_stride, sig_stride, sig_len + lo, mode,
+                          D > 1 ? splitmix_host(rlc_seed ^ (0x5EEDull * (uint64_t)(k + 1))) : rlc_seed};
+    if ((rc = check_args(c, keys[k], args[k]))) return rc;
+    multi_bufs& b = m->buf[k];
+    if ((rc = b.bits.ensure(per / 8)) || (rc = b.reasons.ensure(per)) || (rc = b.all_bits.ensure(D * per / 8)) ||
+        (rc = b.all_reasons.ensure(D * per)) || (rc = b.root.ensure(2 * G2J_WORDS * 4)) ||
+        (rc = b.all_roots.ensure((size_t)D * 2 * G2J_WORDS * 4)))
+      return rc;
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
+  }
+  const bool rlc = mode == DGPU_MODE_RLC && !sig_on_g1(scheme);
+  std::vector<rlc_trees> trees(D);
+  // phase 1: stage the shard, then per-round verification (or the RLC trees)
+  rc = for_each_device(m, [&](int k) -> int {
+    dgpu_ctx* c = m->ctx[k];
+    verify_args& a = args[k];
+    if (a.n == 0) return DGPU_OK;
+    hipStream_t s = c->stream;
+    int r;
+    if ((r = stage_inputs_locked(c, a, s))) return r;
+    if ((r = c->status.ensure(a.n))) return r;
+    c->n_ev = 0;
+    if (rlc) return rlc_build_locked(c, a, s, trees[k]);
+    if ((r = verify_status_locked(c, keys[k], a, s))) return r;
+    return pack_shard_locked(c, a.n, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, s);
+  });
+  if (rc) return rc;
+  if (rlc) {
+    bool all_ok = false;
+    if (D > 1) {
+      // the per-device roots to every device; one check of their sum on device 0
+      g2j inf = g2_infinity();
+      uint32_t inf_words[G2J_WORDS];
+      const fp* co[6] = {&inf.x.c0, &inf.x.c1, &inf.y.c0, &inf.y.c1, &inf.z.c0, &inf.z.c1};
+      for (int j = 0; j < 6; ++j) memcpy(inf_words + j * FP_LIMBS, co[j]->l, FP_LIMBS * 4);
+      for (int k = 0; k < D; ++k) {
+        dgpu_ctx* c = m->ctx[k];
+        HIP_TRY(hipSetDevice(c->device));
+        uint32_t* root = (uint32_t*)m->buf[k].root.p;
+        if (args[k].n == 0) {
+          HIP_TRY(hipMemcpyAsync(root, inf_words, sizeof inf_words, hipMemcpyHostToDevice, c->stream));
+          HIP_TRY(hipMemcpyAsync(root + G2J_WORDS, inf_words, sizeof inf_words, hipMemcpyHostToDevice, c->stream));
+        } else {
+          const int top = trees[k].top();
+          HIP_TRY(hipMemcpyAsync(root, trees[k].P[top], G2J_WORDS * 4, hipMemcpyDeviceToDevice, c->stream));
+          HIP_TRY(hipMemcpyAsync(root + G2J_WORDS, trees[k].S[top], G2J_WORDS * 4, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        }
+      }
+      NCCL_TRY(m->api, m->api.group_start());
+      for (int k = 0; k < D; ++k)
+        NCCL_TRY(m->api, m->api.all_gather(m->buf[k].root.p, m->buf[k].all_roots.p, 2 * G2J_WORDS * 4, ncclUint8,
+                                           m->comm[k], m->ctx[k]->stream));
+      NCCL_TRY(m->api, m->api.group_end());
+      dgpu_ctx* c0 = m->ctx[0];
+      HIP_TRY(hipSetDevice(c0->device));
+      if ((rc = c0->rlc_root.ensure(2 * G2J_WORDS * 4))) return rc;
+      uint32_t* sum = (uint32_t*)c0->rlc_root.p;
+      hipLaunchKernelGGL(k_rlc_sum_roots, dim3(1), dim3(64), 0, c0->stream, D, (const uint32_t*)m->buf[0].all_roots.p,
+                         sum, sum + G2J_WORDS);
+      HIP_TRY(hipGetLastError());
+      std::vector<uint8_t> fail;
+      if ((rc = rlc_check_locked(c0, keys[0], std::vector<uint32_t>{0}, 1, sum, sum + G2J_WORDS, c0->stream, &fail)))
+        return rc;
+      all_ok = !fail[0];
+    }
+    rc = for_each_device(m, [&](int k) -> int {
+      dgpu_ctx* c = m->ctx[k];
+      const size_t cnt = args[k].n;
+      if (cnt == 0) return DGPU_OK;
+      int r;
+      if (!all_ok && (r = rlc_descend_locked(c, keys[k], trees[k], c->stream))) return r;
+      return pack_shard_locked(c, cnt, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, c->stream);
+    });
+    if (rc) return rc;
+  }
+  // the verdicts of every shard to every device (one grouped all-gather)
+  for (int k = 0; k < D; ++k) {
+    HIP_TRY(hipSetDevice(m->ctx[k]->device));
+    if (args[k].n < per) {  // padding of a short (or empty) last shard
+      const size_t b0 = (args[k].n + 7) / 8;
+      HIP_TRY(hipMemsetAsync((uint8_t*)m->buf[k].bits.p + b0, 0, per / 8 - b0, m->ctx[k]->stream));
+    }
+  }
+  NCCL_TRY(m->api, m->api.group_start());
+  for (int k = 0; k < D; ++k) {
+    NCCL_TRY(m->api, m->api.all_gather(m->buf[k].bits.p, m->buf[k].all_bits.p, per / 8, ncclUint8, m->comm[k],
+                                       m->ctx[k]->stream));
+    if (reason)
+      NCCL_TRY(m->api, m->api.all_gather(m->buf[k].reasons.p, m->buf[k].all_reasons.p, per, ncclUint8, m->comm[k],
+                                         m->ctx[k]->stream));
+  }
+  NCCL_TRY(m->api, m->api.group_end());
+  dgpu_ctx* c0 = m->ctx[0];
+  HIP_TRY(hipSetDevice(c0->device));
+  HIP_TRY(hipMemcpyAsync(verdict_bits, m->buf[0].all_bits.p, (n + 7) / 8, hipMemcpyDeviceToHost, c0->stream));
+  if (reason) HIP_TRY(hipMemcpyAsync(reason, m->buf[0].all_reasons.p, n, hipMemcpyDeviceToHost, c0->stream));
+  for (int k = 0; k < D; ++k) {
+    HIP_TRY(hipSetDevice(m->ctx[k]->device));
+    HIP_TRY(hipEventRecord(m->ctx[k]->done, m->ctx[k]->stream));
+    HIP_TRY(hipStreamSynchronize(m->ctx[k]->stream));
+  }
+  return DGPU_OK;
+}
+
+}  // extern "C"

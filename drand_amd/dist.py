@@ -12,11 +12,15 @@ import numpy as np
 
 
 def shard_range(n_total, world, rank):
-    """Contiguous shard [lo, hi) of n_total items for `rank` (sizes differ by <= 1)."""
-    base, extra = divmod(n_total, world)
-    lo = rank * base + min(rank, extra)
-    hi = lo + base + (1 if rank < extra else 0)
-    return lo, hi
+    """Contiguous shard [lo, hi) of n_total items for `rank`: the C ABI's rule
+    (dgpu_shard_range, used by dgpu_verify_multi) -- shards of
+    ceil(n_total / world) items rounded up to a multiple of 8 (whole bitmap
+    bytes), the last one takes the remainder (possibly empty)."""
+    world = max(1, world)
+    per = -(-n_total // world)
+    per = (per + 7) & ~7
+    lo = min(n_total, rank * per)
+    return lo, min(n_total, lo + per)
 
 
 def gather_verdict_bits(local_bits, n_local, n_total, world, rank, device=None):

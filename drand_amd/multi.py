@@ -1,0 +1,49 @@
+"""Multi-GPU verification through the C ABI (dgpu_multi_open /
+dgpu_verify_multi, include/drand_gpu.h): one process drives every GPU of a
+node, as a Go caller of the crypto/gpu package would.
+Rounds shard contiguously across the devices; RCCL over xGMI gathers only
+the per-device verdict bitmaps (and, in RLC mode, the per-device RLC roots,
+checked once).  Verdicts equal chain.Verifier's on the same beacons.
+
+The one-process-per-GPU form (torch.distributed ranks, bench.py) lives in
+drand_amd/dist.py; both shard with the same contiguous rule."""
+import numpy as np
+
+from . import _lib
+from .chain import pack_beacons, rlc_seed_for
+from .scheme import Scheme, scheme_code
+
+
+class MultiVerifier:
+    """chain.Verifier's batch surface over several GPUs (one dgpu_multi handle)."""
+
+    def __init__(self, scheme: Scheme, devices):
+        self.scheme = scheme
+        self._code = scheme_code(scheme)
+        self.mctx = _lib.MultiContext(devices)
+
+    def close(self):
+        self.mctx.close()
+
+    def verify_reasons(self, beacons, pubkey, mode=_lib.MODE_PER_ROUND, rlc_seed=None):
+        n = len(beacons)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint8)
+        rounds, sigs, sig_len, prev, prev_len = pack_beacons(beacons)
+        return self.verify_records(pubkey, rounds, sigs, sig_len, prev, prev_len, mode, rlc_seed)
+
+    def verify_records(self, pubkey, rounds, sigs, sig_len, prev, prev_len, mode=_lib.MODE_PER_ROUND, rlc_seed=None):
+        """Fixed-stride host records (numpy, as chain.pack_beacons builds)."""
+        n = len(rounds)
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        reason = np.zeros(n, dtype=np.uint8)
+        pk = np.frombuffer(bytes(pubkey), dtype=np.uint8).copy()
+        lib = self.mctx.lib
+        _lib.check(lib.dgpu_verify_multi(self.mctx.handle, self._code, _lib.ptr(pk), pk.size, n, _lib.ptr(rounds),
+                                         _lib.ptr(sigs), sigs.shape[1], _lib.ptr(sig_len), _lib.ptr(prev),
+                                         prev.shape[1], _lib.ptr(prev_len), mode, rlc_seed_for(mode, rlc_seed),
+                                         _lib.ptr(bits), _lib.ptr(reason)))
+        valid = np.unpackbits(bits, bitorder="little")[:n].astype(bool)
+        if not np.array_equal(valid, reason == _lib.REASON_OK):
+            raise _lib.DrandGPUError(_lib.DGPU_EINVAL, "verdict bitmap and reasons disagree")
+        return reason

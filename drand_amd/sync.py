@@ -43,12 +43,44 @@ def beacon_marshal(b: Beacon) -> bytes:
     }, separators=(",", ":")).encode()
 
 
+def _json_field(d, name):
+    """encoding/json field lookup: exact key first, then case-insensitive."""
+    if name in d:
+        return d[name]
+    low = name.lower()
+    for k, v in d.items():
+        if isinstance(k, str) and k.lower() == low:
+            return v
+    return None
+
+
 def beacon_unmarshal(buf: bytes) -> Beacon:
-    """Beacon.Unmarshal (chain/beacon.go:34-37).  Missing fields decode to
-    their zero values, like Go's encoding/json."""
-    d = json.loads(buf)
-    return Beacon(bytes.fromhex(d.get("PreviousSig") or ""), int(d.get("Round") or 0),
-                  bytes.fromhex(d.get("Signature") or ""))
+    """Beacon.Unmarshal (chain/beacon.go:34-37, hexjson).  Missing or null
+    fields decode to their zero values, like Go's encoding/json; anything Go
+    would refuse (not a JSON object, a non-hex byte field, a Round that is not
+    a non-negative integer below 2^64) raises ValueError -- Get's unmarshal
+    error, which CheckPastBeacons counts as a faulty round."""
+    try:
+        d = json.loads(buf)
+    except (ValueError, UnicodeDecodeError, TypeError) as e:
+        raise ValueError(f"beacon: invalid JSON: {e}") from None
+    if not isinstance(d, dict):
+        raise ValueError("beacon: not a JSON object")
+
+    def hexbytes(name):
+        v = _json_field(d, name)
+        if v is None:
+            return b""
+        if not isinstance(v, str):
+            raise ValueError(f"beacon: {name} is not a hex string")
+        return bytes.fromhex(v)
+
+    r = _json_field(d, "Round")
+    if r is None:
+        r = 0
+    if isinstance(r, bool) or not isinstance(r, int) or not 0 <= r < 1 << 64:
+        raise ValueError("beacon: Round is not a uint64")
+    return Beacon(hexbytes("PreviousSig"), r, hexbytes("Signature"))
 
 
 class MemoryStore:
@@ -102,9 +134,7 @@ def check_past_beacons(store, verifier, pubkey, up_to, cb=None, window=1 << 16, 
         for r in range(i, hi):
             try:
                 rows.append(store.get(r))
-            except ErrNoBeaconSaved:
-                rows.append(None)
-            except ValueError:  # Unmarshal error: Get returns err, the round is faulty
+            except (ErrNoBeaconSaved, ValueError):  # no row, or Unmarshal error: the round is faulty
                 rows.append(None)
         present = [b for b in rows if b is not None]
         reasons = verifier.verify_reasons(present, pubkey, mode) if present else []

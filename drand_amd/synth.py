@@ -155,6 +155,55 @@ def corrupt(chain, seed, rate=1e-3, kinds=ALL_CORRUPTIONS):
     return chosen
 
 
+def corrupt_global(shard, seed, n_total, lo, rate=1e-3, kinds=ALL_CORRUPTIONS):
+    """The corruption catalog of a whole n_total-round chain (chosen from the
+    seed alone, like `corrupt`), applied to the shard holding global items
+    [lo, lo + len(shard)).  Returns {global index: kind} for the whole chain,
+    so every rank knows the expected verdict of every round whatever the
+    number of shards; a signature-of-another-round corruption takes its donor
+    from the shard (the next round, or the previous one at the shard's end)."""
+    n = len(shard)
+    count = max(len(kinds), int(round(n_total * rate))) if rate > 0 else 0
+    state = (seed ^ 0xC0FFEE) & 0xFFFFFFFFFFFFFFFF
+    chosen = {}
+    chained = shard.scheme_code == _lib.SCHEME_CHAINED
+    k = 0
+    while len(chosen) < min(count, n_total):
+        state, r = splitmix64(state)
+        i = r % n_total
+        if i in chosen:
+            continue
+        kind = kinds[k % len(kinds)]
+        k += 1
+        if kind == CORRUPT_PREV and not chained:
+            kind = CORRUPT_Y_SIGN
+        if kind == CORRUPT_OTHER_ROUND and n_total < 2:
+            kind = CORRUPT_Y_SIGN
+        chosen[int(i)] = kind
+    for gi, kind in chosen.items():
+        i = gi - lo
+        if not 0 <= i < n:
+            continue
+        if kind == CORRUPT_X_BIT:
+            shard.sigs[i, 47] ^= 0x01
+        elif kind == CORRUPT_Y_SIGN:
+            shard.sigs[i, 0] ^= 0x20
+        elif kind == CORRUPT_OTHER_ROUND:
+            j = i + 1 if i + 1 < n else i - 1
+            if j < 0:  # one-round shard: any other valid point fails too
+                shard.sigs[i, 0] ^= 0x20
+            else:
+                shard.sigs[i] = shard.sigs[j].copy()
+        elif kind == CORRUPT_PREV:
+            shard.prev[i, 0] ^= 0x01
+        elif kind == CORRUPT_INFINITY:
+            shard.sigs[i] = 0
+            shard.sigs[i, 0] = 0xC0
+        elif kind == CORRUPT_TRUNCATED:
+            shard.sig_len[i] = (shard.sig_len[i] // 2) if (gi & 1) else 0
+    return chosen
+
+
 # ---------------------------------------------------------------- threshold groups (SURVEY.md 8(d) config 5)
 class Group:
     """A t-of-n threshold group: polynomial coefficients a_0..a_{t-1} over Fr

@@ -22,8 +22,14 @@
  *  - Return codes: DGPU_OK (0) or a negative DGPU_E* value; the message is in
  *    dgpu_last_error() (thread-local).
  *  - A context is bound to one GPU and serializes its own calls internally;
- *    any thread may call.  There is no CPU fallback: without a usable GPU,
- *    dgpu_open fails with DGPU_EDEVICE.
+ *    any thread may call.  Calls on one context are also ordered on the
+ *    device: each call's work starts after the previous call's, whatever
+ *    streams the *_device entry points are given.  There is no CPU fallback:
+ *    without a usable GPU, dgpu_open fails with DGPU_EDEVICE.
+ *  - Public keys are passed per call (dgpu_verify_beacons*, like
+ *    VerifyBeacon(b, pubkey), chain/verify.go:38) and cached decoded per
+ *    context (8 keys, LRU), so one context serves any number of chains and
+ *    schemes; dgpu_set_pubkey + dgpu_verify_batch* keep the ABI-1 form.
  *  - Verdict bitmaps: bit (i % 8) of byte (i / 8) is 1 iff round i verifies,
  *    i.e. iff the reference's VerifyBeacon returns nil.
  */
@@ -37,7 +43,7 @@
 extern "C" {
 #endif
 
-#define DGPU_ABI_VERSION 1
+#define DGPU_ABI_VERSION 2
 
 /* scheme IDs (common/scheme/scheme.go:9,12; bls-unchained-on-g1 added by this build) */
 enum {
@@ -94,6 +100,39 @@ int dgpu_scheme_from_name(const char *name);
  * out-of-subgroup keys (DGPU_EINVAL). */
 int dgpu_set_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t len);
 
+/* Contiguous shard [lo, hi) of item k among ndev devices as dgpu_verify_multi
+ * splits a batch of n: shards are multiples of 8 items (whole verdict-bitmap
+ * bytes) and the last takes the remainder.  Host-only bookkeeping. */
+void dgpu_shard_range(size_t n, int ndev, int k, size_t *lo, size_t *hi);
+
+/* Batch form of Verifier.VerifyBeacon(b, pubkey) (chain/verify.go:38-45), the
+ * public key passed per call (48-byte compressed G1, or 96-byte compressed G2
+ * for the G1-signature schemes; decoded, subgroup-checked and cached by the
+ * context; DGPU_EINVAL if rejected).  Records as dgpu_verify_batch. */
+int dgpu_verify_beacons(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t pk_len, size_t n,
+                        const uint64_t *rounds, const uint8_t *sigs, size_t sig_stride, const uint32_t *sig_len,
+                        const uint8_t *prev, size_t prev_stride, const uint32_t *prev_len, int mode,
+                        uint64_t rlc_seed, uint8_t *verdict_bits, uint8_t *reason);
+
+/* dgpu_verify_beacons over device-resident records (as dgpu_verify_batch_device):
+ * a record with prev_len[i] > prev_stride is not read past its stride and
+ * fails with reason DGPU_REASON_DECODE. */
+int dgpu_verify_beacons_device(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t pk_len, size_t n,
+                               const uint64_t *d_rounds, const uint8_t *d_sigs, size_t sig_stride,
+                               const uint32_t *d_sig_len, const uint8_t *d_prev, size_t prev_stride,
+                               const uint32_t *d_prev_len, int mode, uint64_t rlc_seed, uint8_t *d_verdict_bits,
+                               uint8_t *d_reason, void *stream);
+
+/* Batch key.Scheme.VerifyRecovered(pk, msg, sig) (= bls.Verify (R); call
+ * sites chain/verify.go:44, chain/beacon/chain.go:165; AuthScheme
+ * key/curve.go:39) over raw messages of any length: message i is msg_len[i]
+ * bytes at msgs + i*msg_stride (msg_len[i] <= msg_stride, else DGPU_EINVAL).
+ * Signatures, key, mode and outputs as dgpu_verify_beacons. */
+int dgpu_verify_recovered(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t pk_len, size_t n,
+                          const uint8_t *msgs, size_t msg_stride, const uint32_t *msg_len, const uint8_t *sigs,
+                          size_t sig_stride, const uint32_t *sig_len, int mode, uint64_t rlc_seed,
+                          uint8_t *verdict_bits, uint8_t *reason);
+
 /* Batch form of Verifier.VerifyBeacon (chain/verify.go:38-45) over n beacons
  * given as fixed-stride records (host pointers):
  *   rounds[i]                   Beacon.Round
@@ -141,6 +180,27 @@ int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **
 /* Batch DigestMessage (chain/verify.go:24-32): out32 = n x 32 bytes. */
 int dgpu_digest_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *prev,
                       size_t prev_stride, const uint32_t *prev_len, uint8_t *out32);
+
+/* Hash to the scheme's signature group of n raw messages of any length
+ * (msg_len[i] <= msg_stride): 96-byte compressed G2 points under drand's G2
+ * DST (kyber G2 Hash (R), pinned by key/curve_test.go:10-30), or 48-byte
+ * compressed G1 points for the G1-signature schemes. */
+int dgpu_hash_to_curve(dgpu_ctx *ctx, int scheme, size_t n, const uint8_t *msgs, size_t msg_stride,
+                       const uint32_t *msg_len, uint8_t *out);
+
+/* Sign n raw messages with a 32-byte big-endian secret (< r): sig = sk *
+ * H(msg), compressed (96 bytes on G2, 48 on G1 for the G1-signature
+ * schemes).  Test/tool surface of key.Scheme.Sign / AuthScheme.Sign
+ * (key/curve.go:36-39), as key/curve_test.go:10-30 uses it. */
+int dgpu_sign(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, size_t n, const uint8_t *msgs, size_t msg_stride,
+              const uint32_t *msg_len, uint8_t *out_sigs);
+
+/* Decode n 48-byte compressed G1 points (public keys, commitments:
+ * chain/convert.go:20-23, key/group.go TOML keys) with kilic's
+ * FromCompressed rules (R) + subgroup check: rc_out[i] = 0 decoded, 4 the
+ * point at infinity, other values an error (flags, x >= p, not on the curve,
+ * not in the subgroup); xy96 (optional) = canonical big-endian x || y. */
+int dgpu_decode_g1_points(dgpu_ctx *ctx, size_t n, const uint8_t *in48, int *rc_out, uint8_t *xy96);
 
 /* Hash-to-G2 of n 32-byte messages with drand's DST (kyber G2 Hash (R)),
  * compressed to 96 bytes each: the parity surface for hash-to-curve. */
@@ -211,6 +271,27 @@ int dgpu_make_partials(dgpu_ctx *ctx, size_t n_rounds, const uint8_t *msgs32, si
 int dgpu_make_chain(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, size_t n_seg, size_t seg_len,
                     const uint64_t *first_round, const uint8_t *seed_prev, const uint32_t *seed_prev_len,
                     uint8_t *sigs_out);
+
+/* ---------------------------------------------------------------- multi-GPU
+ * One handle over ndev GPUs of a node: a context per device
+ * and an RCCL communicator over them (ncclCommInitAll; RCCL is loaded when
+ * the handle opens, DGPU_EUNSUPPORTED without it).  dgpu_verify_multi is
+ * dgpu_verify_beacons over host records sharded contiguously across the
+ * devices (dgpu_shard_range), as the bulk check-chain loop would call it
+ * (chain/beacon/sync_manager.go:188-222): the data path has no collective;
+ * RCCL all-gathers the per-device verdict bitmaps (and reasons), and in RLC
+ * mode first the per-device RLC roots, checked once on the first device --
+ * one final exponentiation for the whole batch when every round is valid.
+ * Verdicts equal dgpu_verify_beacons' on the same records. */
+typedef struct dgpu_multi dgpu_multi;
+int dgpu_multi_open(int ndev, const int *devs, dgpu_multi **out);
+void dgpu_multi_close(dgpu_multi *m);
+/* the k-th device's context (owned by the handle) */
+int dgpu_multi_context(dgpu_multi *m, int k, dgpu_ctx **out);
+int dgpu_verify_multi(dgpu_multi *m, int scheme, const uint8_t *pk, size_t pk_len, size_t n, const uint64_t *rounds,
+                      const uint8_t *sigs, size_t sig_stride, const uint32_t *sig_len, const uint8_t *prev,
+                      size_t prev_stride, const uint32_t *prev_len, int mode, uint64_t rlc_seed,
+                      uint8_t *verdict_bits, uint8_t *reason);
 
 #ifdef __cplusplus
 }

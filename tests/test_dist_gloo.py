@@ -55,10 +55,33 @@ def test_sharded_verify_gather_world2(tmp_path, hostsim):
 
 
 def test_shard_range_covers():
+    """Contiguous cover; every shard but the last a multiple of 8 rounds (whole
+    bitmap bytes); the Python rule equals the C ABI's dgpu_shard_range, which
+    dgpu_verify_multi uses (the library loads without a GPU)."""
+    from drand_amd import _lib
     from drand_amd.dist import shard_range
-    for n in (0, 1, 7, 10, 1000001):
-        for w in (1, 2, 3, 8):
+    for n in (0, 1, 7, 10, 1000001, 10_000_000):
+        for w in (1, 2, 3, 4, 7, 8):
             spans = [shard_range(n, w, r) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
-            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+            assert all((h - l) % 8 == 0 or h == n for l, h in spans[:-1])
+            assert all(h - l == spans[0][1] - spans[0][0] for l, h in spans[:-1] if h < n)
+            assert spans == [_lib.shard_range(n, w, r) for r in range(w)]
+
+
+def test_bench_launches_ranks():
+    """bench.py --gpus 2 starts two rank processes itself (no torchrun): the
+    DRAND_BENCH_DRYRUN stub runs the rank plumbing over gloo without a GPU."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, DRAND_BENCH_DRYRUN="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rounds", "1000"],
+                         env=env, capture_output=True, text=True, timeout=300, check=True).stdout
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert sorted(r["rank"] for r in line["ranks"]) == [0, 1]
+    assert [tuple(r["shard"]) for r in sorted(line["ranks"], key=lambda r: r["rank"])] == [(0, 504), (504, 1000)]

@@ -1,0 +1,235 @@
+"""GPU tests of the C-ABI boundary (include/drand_gpu.h, ABI 2) beyond the
+per-round verdicts of test_gpu_parity.py:
+
+  * raw-message surface (key.Scheme.VerifyRecovered / AuthScheme with any msg,
+    key/curve.go:36-39): hash-to-curve of many message lengths vs the oracle's
+    fixture, sign + verify on G2 and G1;
+  * decode of every deploy/latest/group.toml key on the GPU;
+  * the public key per call (VerifyBeacon(b, pubkey), chain/verify.go:38): two
+    chains with different keys and schemes interleaved on one context;
+  * RLC soundness with duplicated Round fields (+D / -D corruptions) and the
+    root-first check;
+  * records whose length exceeds their stride on the device entry point;
+  * the multi-GPU handle (dgpu_verify_multi) with one device equals the
+    single-context verdicts (RCCL all-gathers over one rank).
+Marked gpu."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import bls12381 as B
+
+pytestmark = pytest.mark.gpu
+
+
+def _sch(name):
+    from drand_amd.scheme import get_scheme_by_id_with_default
+    return get_scheme_by_id_with_default(name)
+
+
+def test_hash_to_curve_any_length(gpu_ctx):
+    from drand_amd.chain import hash_to_curve
+    g = load_golden("hash_var_len.json")
+    msgs = [bytes.fromhex(c["msg"]) for c in g["cases"]]
+    assert [h.hex() for h in hash_to_curve(msgs, _sch("pedersen-bls-chained"))] == [c["g2"] for c in g["cases"]]
+    for name in ("bls-unchained-on-g1", "bls-unchained-g1-rfc9380"):
+        assert [h.hex() for h in hash_to_curve(msgs, _sch(name))] == [c["g1/" + name] for c in g["cases"]]
+
+
+@pytest.mark.parametrize("name", ["pedersen-bls-chained", "bls-unchained-on-g1", "bls-unchained-g1-rfc9380"])
+def test_sign_and_verify_recovered_any_length(name, gpu_ctx):
+    """AuthScheme.Sign -> VerifyRecovered round trip over raw messages of many
+    lengths; a signature of another message, a wrong key and an empty
+    signature fail; signatures equal the oracle's sk * H(msg)."""
+    from drand_amd import _lib
+    from drand_amd.chain import sign, verify_recovered
+    from drand_amd.synth import derive_secret
+    sch = _sch(name)
+    on_g1 = name != "pedersen-bls-chained"
+    sk = derive_secret(21)
+    msgs = [bytes.fromhex(c["msg"]) for c in load_golden("hash_var_len.json")["cases"]]
+    sigs = sign(sk, msgs, sch)
+    code = _lib.SCHEME_UNCHAINED_G1 if name == "bls-unchained-on-g1" else (
+        _lib.SCHEME_G1_RFC9380 if on_g1 else _lib.SCHEME_CHAINED)
+    pk = np.zeros(96 if on_g1 else 48, dtype=np.uint8)
+    skb = np.frombuffer(sk.to_bytes(32, "big"), dtype=np.uint8).copy()
+    _lib.check(gpu_ctx.lib.dgpu_derive_pubkey(gpu_ctx.handle, code, _lib.ptr(skb), _lib.ptr(pk), pk.size))
+    pk = bytes(pk)
+    assert verify_recovered(sch, pk, msgs, sigs).tolist() == [0] * len(msgs)
+    swapped = sigs[1:] + sigs[:1]
+    assert verify_recovered(sch, pk, msgs, swapped).tolist() == [3] * len(msgs)
+    assert verify_recovered(sch, pk, msgs[:2], [b"", sigs[1][:10]]).tolist() == [1, 1]
+    other = sign(derive_secret(22), msgs[:1], sch)
+    assert verify_recovered(sch, pk, msgs[:1], other).tolist() == [3]
+    # the oracle's signature for two lengths
+    from oracle import drand_ref as D
+    for i in (0, 2):
+        if on_g1:
+            exp = B.sign_g1(sk, msgs[i], D.SIG_ON_G1_DST[name])
+        else:
+            exp = B.sign_g2(sk, msgs[i])
+        assert sigs[i] == exp
+
+
+def test_group_toml_keys_decode_on_gpu(gpu_ctx):
+    """Every key of deploy/latest/group.toml decodes on the GPU to the
+    oracle's point; malformed encodings are rejected with kilic's classes."""
+    from drand_amd.chain import decode_g1_points
+    keys = load_golden("group_toml_keys.json")["keys"]
+    rc, pts = decode_g1_points([bytes.fromhex(k["pk"]) for k in keys])
+    assert rc == [0 if k["decodes"] else rc[i] for i, k in enumerate(keys)]
+    for k, pt in zip(keys, pts):
+        if k["decodes"]:
+            assert pt == B.g1_decompress(bytes.fromhex(k["pk"]))
+    good = bytes.fromhex(keys[0]["pk"])
+    bad = [bytes([good[0] & 0x7F]) + good[1:],             # compression flag clear
+           bytes([0xC0]) + bytes(47),                       # canonical infinity
+           bytes([0xC0]) + bytes(46) + b"\x01",             # non-canonical infinity
+           bytes([0x9F]) + b"\xff" * 47]                    # x >= p
+    x = 5
+    while B.fp_sqrt(x ** 3 + 4) is not None:
+        x += 1
+    bad.append(bytes([0x80]) + x.to_bytes(48, "big")[1:])  # not on the curve
+    rc, _ = decode_g1_points(bad)
+    assert rc[1] == 4 and all(r not in (0, 4) for i, r in enumerate(rc) if i != 1)
+
+
+def test_two_chains_two_keys_one_context(gpu_ctx):
+    """Verifiers of different chains (different keys, chained / unchained /
+    on-G1) share one GPU context; calls alternate and each verdict uses the
+    key passed with it (no stale per-verifier key)."""
+    from drand_amd import _lib
+    from drand_amd.chain import Verifier
+    from drand_amd.synth import make_chain
+    ca = make_chain(31, 40, _lib.SCHEME_CHAINED, seg_len=8)
+    cb = make_chain(32, 40, _lib.SCHEME_UNCHAINED, seg_len=8)
+    cg = make_chain(33, 40, _lib.SCHEME_UNCHAINED_G1, seg_len=8)
+    va, vb, vg = (Verifier(_sch(n)) for n in ("pedersen-bls-chained", "pedersen-bls-unchained", "bls-unchained-on-g1"))
+    ba = [ca.beacon(i) for i in range(len(ca))]
+    bb = [cb.beacon(i) for i in range(len(cb))]
+    bg = [cg.beacon(i) for i in range(len(cg))]
+    for _ in range(2):
+        assert va.verify_reasons(ba, ca.pk).tolist() == [0] * 40
+        assert vb.verify_reasons(bb, cb.pk).tolist() == [0] * 40
+        assert vg.verify_reasons(bg, cg.pk).tolist() == [0] * 40
+        assert va.verify_reasons(ba, cb.pk).tolist() == [3] * 40   # the other chain's key
+        assert vb.verify_reasons(bb, ca.pk, _lib.MODE_RLC).tolist() == [3] * 40
+    with pytest.raises(_lib.DrandGPUError):
+        vg.verify_reasons(bg, ca.pk)                                # a G1 key for a G2-key scheme
+
+
+def test_rlc_duplicate_rounds_cannot_cancel(gpu_ctx):
+    """Two records with the same Round (and PreviousSig) whose signatures are
+    sig + D and sig - D: with coefficients keyed on the Round field they
+    would cancel in every RLC node; keyed on the batch position both fail,
+    as per-round mode says."""
+    from drand_amd import _lib
+    from drand_amd.chain import Beacon, Verifier
+    from drand_amd.synth import make_chain
+    c = make_chain(41, 300, _lib.SCHEME_CHAINED, seg_len=64)
+    beacons = [c.beacon(i) for i in range(len(c))]
+    i = 137
+    s = B.g2_decompress(beacons[i].signature)
+    d = B.G2_GEN
+    plus = B.g2_compress(B.g2_add(s, d))
+    minus = B.g2_compress(B.g2_add(s, B.g2_neg(d)))
+    b = beacons[i]
+    beacons[i] = Beacon(b.previous_sig, b.round, plus)
+    beacons.insert(i + 1, Beacon(b.previous_sig, b.round, minus))
+    v = Verifier(_sch("pedersen-bls-chained"))
+    per = v.verify_reasons(beacons, c.pk)
+    expect = [0] * len(beacons)
+    expect[i] = expect[i + 1] = 3
+    assert per.tolist() == expect
+    for seed in (1, 2, 0xFFFFFFFFFFFFFFFF):
+        assert v.verify_reasons(beacons, c.pk, _lib.MODE_RLC, seed).tolist() == expect
+
+
+def test_rlc_root_first_clean_and_single_bad(gpu_ctx):
+    """A clean batch passes with the root check alone; one bad round among
+    70k is found (descent from the root) -- verdicts equal per-round mode."""
+    from drand_amd import _lib
+    from drand_amd.chain import Verifier
+    from drand_amd.synth import corrupt, make_chain
+    v = Verifier(_sch("pedersen-bls-chained"))
+    c = make_chain(43, 70000, _lib.SCHEME_CHAINED, seg_len=64)
+    beacons = [c.beacon(i) for i in range(len(c))]
+    assert not v.verify_reasons(beacons, c.pk, _lib.MODE_RLC).any()
+    bad = corrupt(c, 43, rate=1e-5, kinds=(3,))  # one signature of another round
+    (k,) = bad.keys()
+    beacons[k] = c.beacon(k)
+    rlc = v.verify_reasons(beacons, c.pk, _lib.MODE_RLC)
+    assert np.nonzero(rlc)[0].tolist() == [k] and rlc[k] == 3
+
+
+def test_device_record_over_stride_fails_without_overrun(gpu_ctx):
+    """dgpu_verify_beacons_device with prev_len[i] > prev_stride: round i is
+    not read past its stride and fails (DGPU_REASON_DECODE); the others keep
+    their verdicts."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    from drand_amd.synth import make_chain
+    c = make_chain(51, 64, _lib.SCHEME_CHAINED, seg_len=64)
+    n = len(c)
+    dev = torch.device("cuda", 0)
+    prev_len = c.prev_len.copy()
+    prev_len[5] = 97        # stride is 96
+    prev_len[9] = 1 << 30   # far past the buffer
+    t = {k: torch.from_numpy(a).to(dev) for k, a in (("r", c.rounds.view(np.int64)), ("s", c.sigs),
+                                                      ("sl", c.sig_len.view(np.int32)), ("p", c.prev),
+                                                      ("pl", prev_len.view(np.int32)))}
+    bits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device=dev)
+    reason = torch.zeros(n, dtype=torch.uint8, device=dev)
+    pk = np.frombuffer(c.pk, dtype=np.uint8).copy()
+    stream = torch.cuda.current_stream(dev)
+    _lib.check(gpu_ctx.lib.dgpu_verify_beacons_device(
+        gpu_ctx.handle, _lib.SCHEME_CHAINED, _lib.ptr(pk), pk.size, n, t["r"].data_ptr(), t["s"].data_ptr(), 96,
+        t["sl"].data_ptr(), t["p"].data_ptr(), 96, t["pl"].data_ptr(), _lib.MODE_PER_ROUND, 0, bits.data_ptr(),
+        reason.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+    torch.cuda.synchronize()
+    r = reason.cpu().numpy()
+    expect = np.zeros(n, dtype=np.uint8)
+    expect[[5, 9]] = 1
+    assert r.tolist() == expect.tolist()
+    assert np.array_equal(np.unpackbits(bits.cpu().numpy(), bitorder="little")[:n].astype(bool), r == 0)
+
+
+def test_unpinned_x_ge_p_rejected(gpu_ctx):
+    """kilic's x >= p rejection is recalled, not pinned by a reference test
+    (SURVEY.md 8(c)); the GPU rejects like the oracle (reason 1).  Listed
+    apart from the verdict corpus."""
+    from drand_amd.chain import Beacon, Verifier
+    for name in ("chain_chained_s1.json", "chain_unchained_s1.json"):
+        g = load_golden(name)
+        v = Verifier(_sch(g["scheme"]))
+        cases = g["unpinned"]
+        got = v.verify_reasons([Beacon(bytes.fromhex(c["prev"]), c["round"], bytes.fromhex(c["sig"])) for c in cases],
+                               bytes.fromhex(g["pk"]))
+        assert got.tolist() == [c["reason"] for c in cases]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_verify_multi_one_device_equals_single_context(mode, gpu_ctx):
+    """dgpu_verify_multi over one device (RCCL communicator of one rank:
+    all-gather of the bitmap, and in RLC mode of the root) == the single
+    context's verdicts and reasons == construction."""
+    from drand_amd import _lib
+    from drand_amd.chain import Verifier
+    from drand_amd.multi import MultiVerifier
+    from drand_amd.synth import corrupt, make_chain
+    c = make_chain(61, 5003, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 61, rate=2e-3)
+    beacons = [c.beacon(i) for i in range(len(c))]
+    single = Verifier(_sch("pedersen-bls-chained")).verify_reasons(beacons, c.pk)
+    mv = MultiVerifier(_sch("pedersen-bls-chained"), [0])
+    try:
+        got = mv.verify_reasons(beacons, c.pk, mode)
+        clean = mv.verify_reasons([b for i, b in enumerate(beacons[:1000]) if i not in bad], c.pk, mode)
+    finally:
+        mv.close()
+    assert got.tolist() == single.tolist()
+    expect = np.ones(len(c), dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(got == 0, expect)
+    assert not clean.any()

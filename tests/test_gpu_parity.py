@@ -34,16 +34,28 @@ def test_hash_to_g2_golden(gpu_ctx):
     assert [o.hex() for o in out] == [c["h"] for c in cases]
 
 
-def test_kat_hash_times_sk(gpu_ctx):
-    """key/curve_test.go:10-30 through the GPU: the KAT signature verifies
-    under sk*g1 and H(msg) matches the oracle."""
-    from drand_amd.chain import hash_to_g2
+def test_kat_on_device(gpu_ctx):
+    """key/curve_test.go:10-30 reproduced on the GPU: AuthScheme.Sign of the
+    18-byte message with the KAT secret gives sigExp bit for bit, the
+    signature verifies (VerifyRecovered over the raw message), the public key
+    derived on the device is sk * g1, and H(msg) = sk^-1 * sig."""
+    from drand_amd.chain import hash_to_curve, sign, verify_recovered
+    from drand_amd.scheme import get_scheme_by_id_with_default
+    from drand_amd.synth import R_ORDER
     k = load_golden("kat_bls12381_compat_v112.json")
-    msg = bytes.fromhex(k["msg"])
-    # the KAT message is 18 bytes (not a drand digest): compare H via the oracle
-    assert len(msg) != 32 or True
-    m32 = hashlib.sha256(msg).digest()
-    assert hash_to_g2([m32])[0] == B.g2_compress(B.hash_to_g2(m32))
+    msg, sk, sig, pk = (bytes.fromhex(k[f]) for f in ("msg", "sk", "sig", "pk"))
+    assert len(msg) == 18
+    sch = get_scheme_by_id_with_default("")
+    assert sign(sk, [msg], sch) == [sig]
+    assert verify_recovered(sch, pk, [msg, msg + b"!", b""], [sig, sig, sig]).tolist() == [0, 3, 3]
+    from drand_amd import _lib
+    out = np.zeros(48, dtype=np.uint8)
+    skb = np.frombuffer(sk, dtype=np.uint8).copy()
+    _lib.check(gpu_ctx.lib.dgpu_derive_pubkey(gpu_ctx.handle, _lib.SCHEME_CHAINED, _lib.ptr(skb), _lib.ptr(out), 48))
+    assert bytes(out) == pk
+    h = B.g2_decompress(hash_to_curve([msg], sch)[0])
+    inv = pow(int.from_bytes(sk, "big"), -1, R_ORDER)
+    assert B.g2_compress(B.g2_mul(B.g2_decompress(sig), inv)) == B.g2_compress(h)
 
 
 def test_digest_matches_reference_rule(chained, unchained):

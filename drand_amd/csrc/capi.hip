@@ -165,6 +165,7 @@ struct dgpu_ctx {
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
+  bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
   int grp_t = 0, grp_n = 0;
   DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok,
@@ -229,6 +230,11 @@ int upload_eng_consts(DevBuf* dst, const g1_key* key, bool unit_points = false) 
     put(ENG_C_G1 + 2 * j + 1, g1c[j].c1);
     put(ENG_C_G2 + j, g2c[j].c0);
   }
+  const fp2 cx = C_PSI_CX, cy = C_PSI_CY;
+  put(ENG_C_PSI, cx.c0);
+  put(ENG_C_PSI + 1, cx.c1);
+  put(ENG_C_PSI + 2, cy.c0);
+  put(ENG_C_PSI + 3, cy.c1);
   int rc;
   if ((rc = dst->ensure(sizeof cb))) return rc;
   HIP_TRY(hipMemcpy(dst->p, &cb, sizeof cb, hipMemcpyHostToDevice));
@@ -297,7 +303,7 @@ int decode_g2_key_locked(dgpu_ctx* c, key_entry* e, const uint8_t* pk) {
   }
   hipLaunchKernelGGL(k_eng_lines, dim3(1), dim3(ENG_BLOCK), 0, s, (size_t)1, (size_t)0, (size_t)1,
                      (const uint32_t*)d_pk, (size_t)1, (const uint32_t*)nullptr, (const uint32_t*)d_g2,
-                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)e->table.p);
+                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)e->table.p, (uint8_t*)nullptr);
   err = hipGetLastError();
   if (err == hipSuccess) err = hipStreamSynchronize(s);
   unit.release();
@@ -342,7 +348,7 @@ int get_key_locked(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len, key_e
 int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint32_t* h, const uint32_t* sg,
                        uint8_t* st, hipStream_t s, size_t h_stride = 0, const uint32_t* h_idx = nullptr,
                        const uint32_t* pk_items = nullptr, const uint32_t* fixed_table = nullptr,
-                       const lane_bufs* L = nullptr);
+                       const lane_bufs* L = nullptr, bool sig_subgroup = false);
 
 // ---------------------------------------------------------------- RLC
 // The segment trees of one RLC batch (level l: P[l], S[l], sz[l] nodes).
@@ -392,8 +398,9 @@ int rlc_build_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees
     HIP_TRY(hipGetLastError());
   }
   mark(c, s, "decode_g2");
+  // RLC needs subgroup-checked signatures before the leaves (soundness)
   hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
-                     sg, st);
+                     1, sg, st);
   HIP_TRY(hipGetLastError());
   mark(c, s, "rlc_leaves_tree");
   // R_i to affine in place (X, Y slots; Z follows them in the Jacobian SoA)
@@ -502,7 +509,7 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
 // final exponentiation.  Decode verdicts in `st` stay final.
 int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint32_t* h, const uint32_t* sg,
                        uint8_t* st, hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
-                       const uint32_t* fixed_table, const lane_bufs* L) {
+                       const uint32_t* fixed_table, const lane_bufs* L, bool sig_subgroup) {
   if (!h_stride) h_stride = n;
   // equal chunks of at most eng_chunk items (whole 5-item blocks): no short tail launch
   const size_t nchunks = (n + c->eng_chunk - 1) / c->eng_chunk;
@@ -542,7 +549,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
       } else {
         mark(c, s, "eng_lines");
         hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
-                           pk_items, consts, lines);
+                           pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
       }
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_miller");
@@ -614,7 +621,9 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
                      (const uint32_t*)L.h_z->p, (uint32_t*)L.h_pre->p);
   HIP_TRY(hipGetLastError());
   mark(c, s, "decode_g2");
-  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m, sg, st);
+  // membership of the signature: checked by the lines kernel (eng_pairing_locked sig_subgroup)
+  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m,
+                     c->decode_subgroup ? 1 : 0, sg, st);
   HIP_TRY(hipGetLastError());
   return DGPU_OK;
 }
@@ -682,21 +691,22 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   const bool two = c->lanes > 1 && !c->profile && n >= LANE_MIN;
   const size_t n0 = two ? ((n / 2 + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
   if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s))) return rc;
+  const bool sub = !c->decode_subgroup;
   if (!two)
     return eng_pairing_locked(c, consts, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
-                              nullptr, nullptr, nullptr, &L0);
+                              nullptr, nullptr, nullptr, &L0, sub);
   const size_t n1 = n - n0;
   hipStream_t s2 = c->stream2;
   HIP_TRY(hipEventRecord(c->lane_ev[0], s));
   HIP_TRY(hipStreamWaitEvent(s2, c->lane_ev[0], 0));
   if ((rc = eng_pairing_locked(c, consts, n0, (const uint32_t*)L0.h_pts->p, (const uint32_t*)L0.sig_pts->p, st, s, 0,
-                               nullptr, nullptr, nullptr, &L0)))
+                               nullptr, nullptr, nullptr, &L0, sub)))
     return rc;
   if ((rc = g2_lane_hash_locked(c, L1, n1, src_slice(a.m, n0), a.sigs + n0 * a.sig_stride, a.sig_stride,
                                 a.sig_len + n0, st + n0, s2)))
     return rc;
   if ((rc = eng_pairing_locked(c, consts, n1, (const uint32_t*)L1.h_pts->p, (const uint32_t*)L1.sig_pts->p, st + n0,
-                               s2, 0, nullptr, nullptr, nullptr, &L1)))
+                               s2, 0, nullptr, nullptr, nullptr, &L1, sub)))
     return rc;
   HIP_TRY(hipEventRecord(c->lane_ev[1], s2));
   HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
@@ -828,6 +838,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
+  const char* sgv = getenv("DGPU_SUBGROUP");
+  if (sgv && !strcmp(sgv, "decode")) c->decode_subgroup = true;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);

@@ -229,10 +229,13 @@ __global__ void __launch_bounds__(256) k_digest(size_t n, const uint64_t* __rest
 
 // Signature decode (kilic G2.FromCompressed semantics (R)) + G2 membership.
 // A record whose message part overruns its stride (msg_bad_record) fails as a
-// decode error without its signature being read.
+// decode error without its signature being read.  check_subgroup = 0: the
+// membership test is left to the pairing engine's lines kernel (the Miller
+// loop's ladder of the signature gives [x] sig for free, k_eng_lines).
 __global__ void __launch_bounds__(256, 4) k_decode_g2_sigs(size_t n, const uint8_t* __restrict__ sigs, size_t sig_stride,
                                                          const uint32_t* __restrict__ sig_len, msg_src m,
-                                                         uint32_t* __restrict__ sig_out, uint8_t* __restrict__ status) {
+                                                         int check_subgroup, uint32_t* __restrict__ sig_out,
+                                                         uint8_t* __restrict__ status) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t st;
@@ -243,7 +246,7 @@ __global__ void __launch_bounds__(256, 4) k_decode_g2_sigs(size_t n, const uint8
     uint8_t buf[96];
     const uint8_t* src = sigs + i * sig_stride;
     for (int k = 0; k < 96; ++k) buf[k] = src[k];
-    int rc = g2_decompress(&p, buf, true);
+    int rc = g2_decompress(&p, buf, check_subgroup != 0);
     st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
   }
   st_g2a(sig_out, n, i, p);

@@ -189,8 +189,8 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
   std::vector<std::unique_lock<std::mutex>> locks;
   for (dgpu_ctx* c : m->ctx) locks.emplace_back(c->mu);
   const int D = m->ndev;
-  size_t per = 0;
-  dgpu_shard_range(n, D, 0, nullptr, &per);  // shard 0 has the full per-device size
+  // per-device shard capacity (a multiple of 8 rounds; dgpu_shard_range's rule)
+  const size_t per = (((n + (size_t)D - 1) / (size_t)D) + 7) & ~(size_t)7;
   std::vector<key_entry*> keys(D, nullptr);
   std::vector<verify_args> args(D);
   int rc;
@@ -296,6 +296,10 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
                                          m->ctx[k]->stream));
   }
   NCCL_TRY(m->api, m->api.group_end());
+  for (int k = 0; k < D; ++k) {
+    HIP_TRY(hipSetDevice(m->ctx[k]->device));
+    HIP_TRY(hipStreamSynchronize(m->ctx[k]->stream));
+  }
   dgpu_ctx* c0 = m->ctx[0];
   HIP_TRY(hipSetDevice(c0->device));
   HIP_TRY(hipMemcpyAsync(verdict_bits, m->buf[0].all_bits.p, (n + 7) / 8, hipMemcpyDeviceToHost, c0->stream));

@@ -153,13 +153,19 @@ __device__ __forceinline__ bool eng_eq_canon(const fp& x, const fp& K) {
 //   H_i = h_pts[h_idx ? h_idx[r0 + i] : r0 + i], S_i = sig_pts[r0 + i]
 //   (affine G2 SoA [x.c0, x.c1, y.c0, y.c1][limb][stride]),
 //   P_i = pk_items ? pk_items[r0 + i] ((-x, y) SoA [2][limb][n]) : the block constant key.
+// status (optional, per item): after the loop T of pair 1 is [|x|] S_i, and
+// the program's LSUB op tests psi(S_i) == -T (tools/gen_engine.py
+// lines_subgroup_op) -- the G2 membership check of the signature, so the
+// decoder can skip its own 63-doubling ladder; a failing item with status
+// ST_OK becomes ST_SUBGROUP.
 __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0, size_t cnt,
                                                          const uint32_t* __restrict__ h_pts, size_t h_stride,
                                                          const uint32_t* __restrict__ h_idx,
                                                          const uint32_t* __restrict__ sig_pts,
                                                          const uint32_t* __restrict__ pk_items,
                                                          const uint32_t* __restrict__ consts,
-                                                         uint32_t* __restrict__ lines) {
+                                                         uint32_t* __restrict__ lines,
+                                                         uint8_t* __restrict__ status) {
   __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_LINES) * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
@@ -183,6 +189,14 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
   }
   asm volatile("" ::: "memory");
   eng_exec(ENG_PROG_LINES, ENG_PROG_LINES_LEN, g, c, L, eng_io{lines, nullptr, nullptr, cnt});
+  if (status) {
+    // lanes 0..3 test D1, D2 == 0, lanes 4, 5 test Z (re, im) == 0
+    const int sl = L.k < 2 ? ENG_L_SUB_D1 + L.k : L.k < 4 ? ENG_L_SUB_D2 + L.k - 2 : ENG_L_SUB_Z + (L.k & 1);
+    const bool zero = eng_eq_canon(eng_ld(g + sl * ENG_SLOT_WORDS), fp_zero());
+    const uint64_t gm = (__ballot(zero) >> (12 * L.g)) & 0x3Full;
+    const bool in_g2 = (gm & 0xFull) == 0xFull && (gm & 0x30ull) != 0x30ull;
+    if (L.valid && L.k == 0 && !in_g2 && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_SUBGROUP;
+  }
 }
 
 // ---------------------------------------------------------------- k_eng_miller

@@ -302,8 +302,46 @@ void host_consts(HostGroup& G, const g1a& pk) {
     put(ENG_C_G1 + 2 * k + 1, g1c[k].c1);
     put(ENG_C_G2 + k, g2c[k].c0);
   }
+  const fp2 cx = C_PSI_CX, cy = C_PSI_CY;
+  put(ENG_C_PSI, cx.c0);
+  put(ENG_C_PSI + 1, cx.c1);
+  put(ENG_C_PSI + 2, cy.c0);
+  put(ENG_C_PSI + 3, cy.c1);
 }
+
+// x == 0 mod p for a slot value (< 2.01p)
+bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 }  // namespace
+
+// G2 membership of a decodable 96-byte point through the lines program's
+// fused test (k_eng_lines status, tools/gen_engine.py lines_subgroup_op):
+// the point is pair 1's Q (pair 0 a dummy copy).  Returns 1 in G2, 0 not,
+// -1 undecodable.
+extern "C" int hs_eng_subgroup(const uint8_t* sig96) {
+  g2a s;
+  if (g2_decompress(&s, sig96, false) != DEC_OK) return -1;
+  static HostGroup G;
+  G = HostGroup();
+  g1a dummy{C_G1_X, C_G1_Y};
+  host_consts(G, dummy);
+  for (int p = 0; p < 2; ++p) {
+    const fp v[4] = {s.x.c0, s.x.c1, s.y.c0, s.y.c1};
+    for (int comp = 0; comp < 4; ++comp) {
+      G.set(p * ENG_LINE_PAIR_SLOTS + comp, v[comp]);
+      G.set(p * ENG_LINE_PAIR_SLOTS + 6 + comp, v[comp]);
+    }
+    G.set(p * ENG_LINE_PAIR_SLOTS + 4, fp_one());
+    G.set(p * ENG_LINE_PAIR_SLOTS + 5, fp_zero());
+  }
+  G.set(ENG_L_NXP0, fp_neg(C_G1_X));
+  G.set(ENG_L_YP0, C_G1_Y);
+  G.step = 0;
+  host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
+  const bool d0 = host_slot_zero(G.get(ENG_L_SUB_D1)) && host_slot_zero(G.get(ENG_L_SUB_D1 + 1)) &&
+                  host_slot_zero(G.get(ENG_L_SUB_D2)) && host_slot_zero(G.get(ENG_L_SUB_D2 + 1));
+  const bool z0 = host_slot_zero(G.get(ENG_L_SUB_Z)) && host_slot_zero(G.get(ENG_L_SUB_Z + 1));
+  return d0 && !z0 ? 1 : 0;
+}
 
 // Engine pairing check e(pk, H(msg)) e(-g1, sig) == 1 through the generated
 // programs (k_eng_lines -> k_eng_miller -> inversion -> k_eng_fe).  out576:

@@ -30,6 +30,8 @@ def _consts(pk=None):
         g2 = B.f2_pow(xi, k * (P * P - 1) // 6)
         assert g2[1] == 0
         c[G.C_G2 + (k - 1)] = g2[0]
+    c[G.C_PSI], c[G.C_PSI + 1] = B.PSI_CX
+    c[G.C_PSI + 2], c[G.C_PSI + 3] = B.PSI_CY
     if pk is not None:
         ng1 = B.g1_neg(B.G1_GEN)
         c[G.C_NXP0], c[G.C_YP0] = (-pk[0]) % P, pk[1]
@@ -177,3 +179,28 @@ def test_full_pairing_flow(ops, kind):
     # exact GT value: FE(f_model) = FE(oracle product)^-1 (the model skips the conjugation)
     fo = B.f12_mul(B.miller_loop(pk, h), B.miller_loop(B.g1_neg(B.G1_GEN), sig))
     assert _to_tower(res) == B.f12_conj(B.final_exponentiation(fo))
+
+
+@pytest.mark.parametrize("in_g2", [True, False])
+def test_lines_fused_subgroup_op(ops, in_g2):
+    """k_lines ends with LSUB: D1 = X - x_psi Z and D2 = Y + y_psi Z of pair 1
+    vanish (with Z != 0) iff psi(sig) == [x] sig, i.e. sig in G2."""
+    rng = random.Random(5 if in_g2 else 6)
+    if in_g2:
+        q = B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))
+    else:
+        q = B.iso_map_g2(B.map_to_curve_sswu_g2((rng.randrange(P), rng.randrange(P))))
+        assert not B.g2_in_subgroup(q)
+    pk = B.g1_mul(B.G1_GEN, 7)
+    m = G.Model(ops, P, _consts(pk))
+    for p in range(2):
+        base = G.LINE_PAIR_SLOTS * p
+        for off, v in ((0, q[0]), (2, q[1]), (6, q[0]), (8, q[1])):
+            m.s[base + off], m.s[base + off + 1] = v[0] % P, v[1] % P
+        m.s[base + 4], m.s[base + 5] = 1, 0
+    m.s[G.L_NXP0], m.s[G.L_YP0] = (-pk[0]) % P, pk[1]
+    G.ProgramRunner(m).run(G.prog_lines())
+    d = [m.s[G.L_SUB_D1], m.s[G.L_SUB_D1 + 1], m.s[G.L_SUB_D2], m.s[G.L_SUB_D2 + 1]]
+    z = (m.s[G.L_SUB_Z], m.s[G.L_SUB_Z + 1])
+    assert z != (0, 0)
+    assert (d == [0, 0, 0, 0]) == in_g2

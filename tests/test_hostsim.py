@@ -198,3 +198,20 @@ def test_decompress_g1_catalog(hostsim):
             rc = hostsim.hs_decompress_g1(sig, buf(48))
             want = c["reason"] if c["reason"] != D.REASON_PAIRING else D.REASON_OK
             assert codes.get(rc, D.REASON_DECODE) == want, (c["kind"], rc)
+
+
+def test_engine_fused_subgroup_check(hostsim):
+    """The lines program's LSUB op (psi(sig) == -[|x|] sig from the Miller
+    loop's own ladder, k_eng_lines status) on the device arithmetic: G2
+    points pass, random curve points outside G2 fail -- same verdict as the
+    oracle's [r]Q test."""
+    k = load_golden("kat_bls12381_compat_v112.json")
+    assert hostsim.hs_eng_subgroup(bytes.fromhex(k["sig"])) == 1
+    g = load_golden("chain_chained_s1.json")
+    for r in g["rounds"][:3]:
+        assert hostsim.hs_eng_subgroup(bytes.fromhex(r["sig"])) == 1
+    rnd = random.Random(9)
+    for _ in range(3):
+        q = B.iso_map_g2(B.map_to_curve_sswu_g2((rnd.randrange(P), rnd.randrange(P))))
+        assert not B.g2_in_subgroup(q)
+        assert hostsim.hs_eng_subgroup(B.g2_compress(q)) == 0

@@ -39,7 +39,8 @@ C_ONE = 64
 C_NXP0, C_YP0, C_NXP1, C_YP1 = 65, 66, 67, 68      # pairing points (-x, y): pair 0 = pk, pair 1 = -g1
 C_G1 = 69                                         # gamma1_k, k = 1..5: (re, im) at 69 + 2(k-1)
 C_G2 = 79                                         # gamma2_k (Fp), k = 1..5 at 79 + (k-1)
-N_CONST = 20
+C_PSI = 84                                        # psi constants cx (re, im) at 84, 85; cy at 86, 87
+N_CONST = 24
 
 # export ids (k_lines): pair p line component e (l0.re, l0.im, l2.re, l2.im, l3.re, l3.im) -> 6p + e
 # export ids (k_miller): 0..11 = f components, 12 = N1 (the Fp norm of f)
@@ -487,6 +488,39 @@ def lines_add_op():
     return Op("LADD", [S1, S2, S3, S4, S5, S6])
 
 
+# After the loop T of pair 1 is [|x|] sigma (the ladder of |x| = 0xd201000000010000,
+# mixed additions of the affine sigma; doubling / addition steps only scale T
+# projectively).  sigma is in G2 iff psi(sigma) == [x] sigma = -T (Scott's
+# test, as curve.cuh g2_in_subgroup), so the Miller loop's own ladder replaces
+# the decoder's 63-doubling subgroup check.  An exceptional step (a 2-torsion
+# doubling, T = +-sigma in an addition) implies sigma has order dividing a
+# number below 2^64 + 1, so sigma is not in G2 -- and those steps zero Z,
+# which stays zero, so the test (Z != 0) rejects them too.
+L_SUB_XP, L_SUB_YP, L_SUB_D1, L_SUB_D2 = 34, 36, 38, 40   # pair 1's temporaries, free after the loop
+L_SUB_Z = LINE_PAIR_SLOTS + 4
+
+
+def lines_subgroup_op():
+    """D1 = X - x_psi Z, D2 = Y + y_psi Z for pair 1, with x_psi = conj(xQ) cx,
+    y_psi = conj(yQ) cy: sigma in G2 iff D1 = D2 = 0 and Z != 0."""
+    X, Y, Z = fp2(_pb(1, 0)), fp2(_pb(1, 2)), fp2(_pb(1, 4))
+    xQ, yQ = fp2(_pb(1, 6)), fp2(_pb(1, 8))
+    XP, YP, D1, D2 = fp2(L_SUB_XP), fp2(L_SUB_YP), fp2(L_SUB_D1), fp2(L_SUB_D2)
+    S1 = []
+    for src, c, dst in ((xQ, fp2(C_PSI), XP), (yQ, fp2(C_PSI + 2), YP)):
+        # conj(s) c: re = s0 c0 + s1 c1, im = s0 c1 - s1 c0
+        S1.append(Rec(dst=dst[0], terms=[T(src[0], c[0]), T(src[1], c[1])]))
+        S1.append(Rec(dst=dst[1], terms=[T(src[0], c[1]), T(src[1], c[0], -1)]))
+    S2 = []
+    a, b = mul_terms(XP, Z)
+    S2.append(Rec(dst=D1[0], cm=-1, terms=a, post=[(X[0], 1)]))
+    S2.append(Rec(dst=D1[1], cm=-1, terms=b, post=[(X[1], 1)]))
+    a, b = mul_terms(YP, Z)
+    S2.append(Rec(dst=D2[0], terms=a, post=[(Y[0], 1)]))
+    S2.append(Rec(dst=D2[1], terms=b, post=[(Y[1], 1)]))
+    return Op("LSUB", [S1, S2])
+
+
 # ---------------------------------------------------------------- k_miller slots
 M_F, M_X, M_L1, M_L2 = 0, 12, 22, 28      # F (12), xi-copies (10), line 1 (6), line 2 (6)
 M_N, M_XN2, M_T, M_XT, M_D, M_N1 = 22, 12, 14, 28, 20, 12  # norm epilogue (after the loop)
@@ -502,6 +536,7 @@ def build_ops():
     # k_lines
     ops.append(lines_dbl_op())
     ops.append(lines_add_op())
+    ops.append(lines_subgroup_op())
     # k_miller
     ops.append(op_xi_copy("M_XIF", M_F, M_X, [1, 2, 3, 4, 5]))
     ops.append(op_sqr12("M_SQR", M_F, M_X))
@@ -560,7 +595,7 @@ def prog_lines():
         prog += [("run", "LDBL"), ("step",)]
         if b:
             prog += [("run", "LADD"), ("step",)]
-    return prog
+    return prog + [("run", "LSUB")]
 
 
 def prog_miller():
@@ -728,7 +763,8 @@ def emit(path):
         f"constexpr int ENG_MAX_TERMS = {MAX_TERMS};",
         f"constexpr int ENG_NCONST = {N_CONST};",
         f"constexpr int ENG_C_ONE = {C_ONE}, ENG_C_NXP0 = {C_NXP0}, ENG_C_YP0 = {C_YP0}, ENG_C_NXP1 = {C_NXP1}, ENG_C_YP1 = {C_YP1};",
-        f"constexpr int ENG_C_G1 = {C_G1}, ENG_C_G2 = {C_G2};",
+        f"constexpr int ENG_C_G1 = {C_G1}, ENG_C_G2 = {C_G2}, ENG_C_PSI = {C_PSI};",
+        f"constexpr int ENG_L_SUB_D1 = {L_SUB_D1}, ENG_L_SUB_D2 = {L_SUB_D2}, ENG_L_SUB_Z = {L_SUB_Z};",
         f"constexpr int ENG_LINE_PAIR_SLOTS = {LINE_PAIR_SLOTS}, ENG_L_NXP0 = {L_NXP0}, ENG_L_YP0 = {L_YP0};",
         f"constexpr int ENG_M_F = {M_F}, ENG_M_L1 = {M_L1}, ENG_M_L2 = {M_L2}, ENG_EXP_N1 = {EXP_N1};",
         f"constexpr int ENG_E_F = {E_F}, ENG_E_N1I = {E_N1I}, ENG_E_R = {E_R}, ENG_E_A = {E_A};",
@@ -739,7 +775,7 @@ def emit(path):
         lines.append(f"  OP_{op.name} = {i},  // {len(op.subs)} sub-op(s), slots < {nslots[op.name]}")
     lines.append("};")
     nsl = {
-        "LINES": max(nslots["LDBL"], nslots["LADD"]),
+        "LINES": max(nslots["LDBL"], nslots["LADD"], nslots["LSUB"]),
         "MILLER": max(v for k, v in nslots.items() if k.startswith("M_")),
         "FE": max(v for k, v in nslots.items() if k.startswith("E_")),
     }

@@ -366,15 +366,15 @@ def op_cyclo_sqr(name, R, TMP):
                                 (4, s_terms(2), 3, -2), (2, s_terms(1), 3, -2), (5, t_terms(1), 3, 2)):
         recs.append(Rec(dst=f[k][0], cm=cm, terms=re, post=[(f[k][0], dd)]))
         recs.append(Rec(dst=f[k][1], cm=cm, terms=im, post=[(f[k][1], dd)]))
-    # f1' = 3 xi T(C) + 2 f1: xi (r + s u) = (r - s) + (r + s) u with T(C) = 2 x0 x1 (x0 = f2, x1 = f5)
+    # f1' = 3 xi T(C) + 2 f1: xi (r + s u) = (r - s) + (r + s) u with T(C) = 2 x0 x1
+    # (x0 = f2 = a + bu, x1 = f5 = c + du): r - s = 2a(c - d) - 2b(c + d),
+    # r + s = 2a(c + d) + 2b(c - d) -- two terms each over the LIN pass's c +- d,
+    # so no lane of this sub-op needs more than three products
     (i0, i1) = pairs[2]
     a, b = f[i0]
-    c_, d = f[i1]
-    tr = [T(a, c_, 1, 2), T(b, d, -1, 2)]
-    ti = [T(a, d, 1, 2), T(b, c_, 1, 2)]
-    neg = lambda ts: [(x, y, -sg, cf) for (x, y, sg, cf) in ts]  # noqa: E731
-    recs.append(Rec(dst=f[1][0], cm=3, terms=tr + neg(ti), post=[(f[1][0], 2)]))
-    recs.append(Rec(dst=f[1][1], cm=3, terms=tr + ti, post=[(f[1][1], 2)]))
+    _, _, cpd, cmd = tmp[2]
+    recs.append(Rec(dst=f[1][0], cm=3, terms=[T(a, cmd, 1, 2), T(b, cpd, -1, 2)], post=[(f[1][0], 2)]))
+    recs.append(Rec(dst=f[1][1], cm=3, terms=[T(a, cpd, 1, 2), T(b, cmd, 1, 2)], post=[(f[1][1], 2)]))
     return Op(name, [lin, recs])
 
 
@@ -396,8 +396,11 @@ def lines_dbl_op():
     line l = (Y^2 - 3b'Z^2) + (-3X^2 xP) w^2 + (2YZ yP) w^3:
       t0 = Y^2, t1 = Z^2, w = 12 xi t1 (= 3b' Z^2), u = t0 - 3w, v = t0 + 3w
       X4 = 2 XY u,  Y4 = v^2 - 12 w^2,  Z4 = 8 t0 YZ
-      l0 = t0 - w,  l2 = 3 X^2 (-xP),  l3 = 2 YZ yP"""
-    S1, S2, S3, S4, S5 = [], [], [], [], []
+      l0 = t0 - w,  l2 = 3 X^2 (-xP),  l3 = 2 YZ yP
+    Y4 = (v0 + v1)(v0 - v1) - (w0 + w1)(12w0 - 12w1) + (2 v0 v1 - 2 w0 12w1) u
+    over the sums of a LIN pass (S4b), so no lane of S5 needs more than two
+    products (the sub-op costs its busiest lane)."""
+    S1, S2, S3, S4, S4b, S5 = [], [], [], [], [], []
     for p in range(2):
         X, Y, Z = fp2(_pb(p, 0)), fp2(_pb(p, 2)), fp2(_pb(p, 4))
         X2, XY, YZ = fp2(_pb(p, 10)), fp2(_pb(p, 12)), fp2(_pb(p, 14))
@@ -428,13 +431,18 @@ def lines_dbl_op():
         S4.append(Rec(exp=6 * p + 4, cm=2, terms=[T(YZ[0], yp)]))
         S4.append(Rec(exp=6 * p + 5, cm=2, terms=[T(YZ[1], yp)]))
         W12 = Y
+        # S4b (LIN): vp = v0 + v1, vm = v0 - v1 (X2's slots, dead after S2), wp = w0 + w1,
+        # w12m = 12 w0 - 12 w1 (22, 23)
+        VP, VM, WP, W12M = _pb(p, 10), _pb(p, 11), _pb(p, 22), _pb(p, 23)
+        S4b.append(Rec(dst=VP, post=[(V[0], 1), (V[1], 1)]))
+        S4b.append(Rec(dst=VM, post=[(V[0], 1), (V[1], -1)]))
+        S4b.append(Rec(dst=WP, post=[(W[0], 1), (W[1], 1)]))
+        S4b.append(Rec(dst=W12M, post=[(W12[0], 1), (W12[1], -1)]))
         # S5: X4 = 2 XY u -> X, Y4 = v^2 - w w12 -> Y, Z4 = 8 t0 YZ -> Z
         fp2_out(S5, X, *mul_terms(XY, U, coef=2))
-        a, b = sqr_terms(V)
-        c, d = mul_terms(W, W12, sign=-1)
-        fp2_out(S5, Y, a + c, b + d)
+        fp2_out(S5, Y, [T(VP, VM), T(WP, W12M, -1)], [T(V[0], V[1], 1, 2), T(W[0], W12[1], -1, 2)])
         fp2_out(S5, Z, *mul_terms(t0, YZ), cm=8)
-    return Op("LDBL", [S1, S2, S3, S4, S5])
+    return Op("LDBL", [S1, S2, S3, S4, S4b, S5])
 
 
 def lines_add_op():

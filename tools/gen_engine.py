@@ -715,9 +715,13 @@ def encode(ops):
                 h0 = dst | (exp << 8) | ((r.cm & 0xFF) << 16) | (len(r.post) << 24)
                 posts = [((s & 0xFF) | ((d & 0xFFFF) << 16)) for s, d in r.post] + [0] * (3 - len(r.post))
                 words += [h0] + posts
+                # plain products first: for the leading term positions no lane
+                # of a sub-op negates or doubles its operand (engine.cuh skips
+                # that transform wave-uniformly)
+                terms = sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2))
                 for t in range(nt):
-                    if t < len(r.terms):
-                        a, b, sg, cf = r.terms[t]
+                    if t < len(terms):
+                        a, b, sg, cf = terms[t]
                         assert cf in (1, 2) and sg in (1, -1)
                         words.append((a & 0xFF) | ((b & 0xFF) << 8) | ((sg < 0) << 16) | ((cf == 2) << 17) | (1 << 31))
                     else:

@@ -48,6 +48,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (H2D-inclusive) pass")
+    ap.add_argument("--no-rlc", action="store_true",
+                    help="per-round mode: skip the RLC batch-verify pass over the same resident chain (configs[2])")
     ap.add_argument("--mode", choices=["per-round", "rlc", "recover"], default="per-round",
                     help="per-round: configs[1] / the metric; rlc: configs[2] (random linear combination + "
                          "bisection); recover: configs[4] (t-of-n threshold recovery, n=32, t=17)")
@@ -117,7 +119,7 @@ STAGE_KERNEL = {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_i
 def traffic_for(kern, items):
     """PMC FETCH_SIZE + WRITE_SIZE per item of this build (profiles/r02*_traffic.json)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r02*_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "r02*_traffic.json"), recursive=True), reverse=True):
         with open(path) as f:
             t = json.load(f)["kernels"]
         key = next((k for k in t if k.split("::")[-1].split("(")[0] == kern), None)
@@ -365,6 +367,28 @@ def main_verify(args, world, rank, local):
                "steps": e2e_steps, "api": "dgpu_verify_beacons (pageable host records: H2D, verify, D2H)",
                "verdicts_equal_device_path": bool(np.array_equal(host_ok, verdicts[lo:hi]))}
 
+    # configs[2] beside the metric: RLC batch verification (one multi-Miller
+    # loop + one final exponentiation per checked node, root first, exact
+    # per-round verdicts by bisection) over the same resident chain
+    rlc = None
+    if args.mode == "per-round" and not args.no_rlc and code in (_lib.SCHEME_CHAINED, _lib.SCHEME_UNCHAINED):
+        def step_rlc():
+            _lib.check(lib.dgpu_verify_beacons_device(
+                ctx.handle, code, _lib.ptr(pk), pk.size, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96,
+                d_sig_len.data_ptr(), d_prev.data_ptr(), 96, d_prev_len.data_ptr(), _lib.MODE_RLC, seed + 1,
+                d_bits.data_ptr(), None, ctypes.c_void_p(stream.cuda_stream)))
+
+        step_rlc()
+        rlc_ms = stage_times(lib, ctx, step_rlc)
+        rlc_steps = max(1, min(args.steps, 3))
+        t_rlc, v_rlc = timed(step_rlc, rlc_steps, world, dev,
+                             after=lambda: gather_verdict_bits(d_bits, n, n_total, world, rank))
+        rlc = {"value": n_total * rlc_steps / t_rlc, "unit": "rounds/s", "ms_per_step": t_rlc / rlc_steps * 1e3,
+               "steps": rlc_steps, "verdict_mismatches": int((v_rlc != expect).sum()), "stage_ms": rlc_ms,
+               "workload": "configs[2] on the same chain: RLC batch verify, root first, per-round verdicts by "
+                           "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)"}
+        log(f"rlc: {rlc['value']:.0f} rounds/s")
+
     if rank == 0:
         value = n_total * args.steps / elapsed
         roofline = roofline_for(stage_ms, n if args.mode == "per-round" else None)
@@ -403,6 +427,7 @@ def main_verify(args, world, rank, local):
             "corrupted_rounds_total": len(bad),
             "chain_gen_s": t_gen,
             "end_to_end": e2e,
+            "rlc": rlc,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

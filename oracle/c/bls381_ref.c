@@ -314,15 +314,17 @@ static void g2_affine(const g2* p, fp2* x, fp2* y) {
 
 /* ------------------------------------------------------------------ hash to G2 (RFC 9380) */
 static const char DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
-static void expand_xmd(uint8_t out[256], const uint8_t msg[32]) {
+static const char DST_G1[] = "BLS_SIG_BLS12381G1_XMD:SHA-256_SSWU_RO_NUL_";
+/* expand_message_xmd (RFC 9380 5.3.1): len_out = 32 ell bytes of a 32-byte msg under a 43-byte DST */
+static void expand_xmd_dst(uint8_t* out, int ell, const uint8_t msg[32], const char* dst) {
   uint8_t zpad[64] = {0}, dstp[44], b0[32], bi[32], tmp[32];
-  memcpy(dstp, DST, 43); dstp[43] = 43;
-  uint8_t lib0[3] = {1, 0, 0};
+  memcpy(dstp, dst, 43); dstp[43] = 43;
+  uint8_t lib0[3] = {(uint8_t)((32 * ell) >> 8), (uint8_t)(32 * ell), 0};
   const uint8_t* s0[4] = {zpad, msg, lib0, dstp};
   size_t l0[4] = {64, 32, 3, 44};
   sha256_segs(b0, s0, l0, 4);
   memset(bi, 0, 32);
-  for (int i = 1; i <= 8; ++i) {
+  for (int i = 1; i <= ell; ++i) {
     for (int k = 0; k < 32; ++k) tmp[k] = b0[k] ^ bi[k];
     uint8_t idx = (uint8_t)i;
     const uint8_t* s[3] = {tmp, &idx, dstp};
@@ -331,6 +333,7 @@ static void expand_xmd(uint8_t out[256], const uint8_t msg[32]) {
     memcpy(out + 32 * (i - 1), bi, 32);
   }
 }
+static void expand_xmd(uint8_t out[256], const uint8_t msg[32]) { expand_xmd_dst(out, 8, msg, DST); }
 static fp fp_from_be64(const uint8_t* b) { /* 64-byte BE mod p in Montgomery form */
   uint8_t hi[48] = {0};
   memcpy(hi + 32, b, 16);
@@ -414,6 +417,140 @@ static int g1_decode(fp* x, fp* y, const uint8_t* in) {
   if (fp_gt_half(*y) != !!(in[0] & 0x20)) *y = fp_neg(*y);
   return R_OK; /* subgroup of the (trusted, decoded-once) group key is checked by the callers' tests */
 }
+
+/* ------------------------------------------------------------------ G1 (Jacobian), hash to G1, G1 signatures */
+typedef struct { fp x, y, z; } g1;
+static int g1_inf(const g1* p) { return fp_is_zero(p->z); }
+static g1 g1_infinity(void) { g1 r = {fp_one(), fp_one(), {{0}}}; return r; }
+static g1 g1_dbl(g1 p) {
+  fp A = fp_sqr(p.x), B = fp_sqr(p.y), C = fp_sqr(B);
+  fp D = fp_sub(fp_sqr(fp_add(p.x, B)), fp_add(A, C));
+  D = fp_add(D, D);
+  fp E = fp_add(fp_add(A, A), A), F = fp_sqr(E);
+  g1 r;
+  r.x = fp_sub(F, fp_add(D, D));
+  fp C8 = fp_add(C, C); C8 = fp_add(C8, C8); C8 = fp_add(C8, C8);
+  r.y = fp_sub(fp_mul(E, fp_sub(D, r.x)), C8);
+  r.z = fp_mul(fp_add(p.y, p.y), p.z);
+  return r;
+}
+static g1 g1_add(g1 p, g1 q) {
+  if (g1_inf(&p)) return q;
+  if (g1_inf(&q)) return p;
+  fp z1z1 = fp_sqr(p.z), z2z2 = fp_sqr(q.z);
+  fp u1 = fp_mul(p.x, z2z2), u2 = fp_mul(q.x, z1z1);
+  fp s1 = fp_mul(fp_mul(p.y, q.z), z2z2), s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  fp h = fp_sub(u2, u1), rr = fp_sub(s2, s1);
+  rr = fp_add(rr, rr);
+  if (fp_is_zero(h)) return fp_is_zero(rr) ? g1_dbl(p) : g1_infinity();
+  fp i = fp_sqr(fp_add(h, h)), j = fp_mul(h, i), v = fp_mul(u1, i);
+  g1 r;
+  r.x = fp_sub(fp_sub(fp_sqr(rr), j), fp_add(v, v));
+  fp s1j = fp_mul(s1, j);
+  r.y = fp_sub(fp_mul(rr, fp_sub(v, r.x)), fp_add(s1j, s1j));
+  r.z = fp_mul(fp_sub(fp_sqr(fp_add(p.z, q.z)), fp_add(z1z1, z2z2)), h);
+  return r;
+}
+static g1 g1_mul_u64s(g1 p, const u64* k, int nbits) {
+  g1 r = g1_infinity();
+  for (int i = nbits - 1; i >= 0; --i) { r = g1_dbl(r); if ((k[i >> 6] >> (i & 63)) & 1) r = g1_add(r, p); }
+  return r;
+}
+static void g1_affine(const g1* p, fp* x, fp* y) {
+  fp zi = fp_inv(p->z), zi2 = fp_sqr(zi);
+  *x = fp_mul(p->x, zi2); *y = fp_mul(p->y, fp_mul(zi2, zi));
+}
+/* simplified SWU on E1' (RFC 9380 6.6.2), then the 11-isogeny to E1 */
+static void sswu1(fp* ox, fp* oy, fp u) {
+  fp A = fpc(SSWU1_A), B = fpc(SSWU1_B), Z = fpc(SSWU1_Z);
+  fp zu2 = fp_mul(Z, fp_sqr(u)), den = fp_add(fp_sqr(zu2), zu2), x1;
+  if (fp_is_zero(den)) x1 = fpc(SSWU1_BZA);
+  else x1 = fp_mul(fpc(SSWU1_MBA), fp_add(fp_one(), fp_inv(den)));
+  fp gx1 = fp_add(fp_mul(fp_add(fp_sqr(x1), A), x1), B);
+  fp x2 = fp_mul(zu2, x1), gx2 = fp_add(fp_mul(fp_add(fp_sqr(x2), A), x2), B), y;
+  if (fp_is_square(gx1)) { *ox = x1; y = fp_sqrt_cand(gx1); }
+  else { *ox = x2; y = fp_sqrt_cand(gx2); }
+  if (fp_sgn0(u) != fp_sgn0(y)) y = fp_neg(y);
+  *oy = y;
+}
+static fp fpoly(const u64 (*k)[6], int n, fp x) {
+  fp acc = fpc(k[n - 1]);
+  for (int i = n - 2; i >= 0; --i) acc = fp_add(fp_mul(acc, x), fpc(k[i]));
+  return acc;
+}
+static g1 iso11(fp x, fp y) {
+  fp xd = fpoly(ISO11_XDEN, 11, x), yd = fpoly(ISO11_YDEN, 16, x);
+  if (fp_is_zero(xd) || fp_is_zero(yd)) return g1_infinity();
+  g1 r = {fp_mul(fpoly(ISO11_XNUM, 12, x), fp_inv(xd)), fp_mul(y, fp_mul(fpoly(ISO11_YNUM, 16, x), fp_inv(yd))), fp_one()};
+  return r;
+}
+/* RFC 9380 BLS12381G1_XMD:SHA-256_SSWU_RO_ of a 32-byte digest; h_eff = 1 - x */
+static g1 hash_to_g1(const uint8_t msg[32], const char* dst) {
+  uint8_t u[128];
+  expand_xmd_dst(u, 4, msg, dst);
+  fp x, y;
+  sswu1(&x, &y, fp_from_be64(u));
+  g1 q0 = iso11(x, y);
+  sswu1(&x, &y, fp_from_be64(u + 64));
+  g1 q1 = iso11(x, y);
+  static const u64 HEFF1 = 0xd201000000010001ULL;
+  return g1_mul_u64s(g1_add(q0, q1), &HEFF1, 64);
+}
+/* 48-byte compressed G1 signature, kilic FromCompressed semantics (R): flags,
+   x < p, on the curve, [r]P == O */
+static int g1_decode_sig(fp* x, fp* y, const uint8_t* in, size_t len) {
+  if (len != 48) return R_DECODE;
+  if (!(in[0] & 0x80)) return R_DECODE;
+  if (in[0] & 0x40) {
+    int nz = in[0] & 0x3f;
+    for (int i = 1; i < 48; ++i) nz |= in[i];
+    return nz ? R_DECODE : R_INFINITY;
+  }
+  int rc = g1_decode(x, y, in);
+  if (rc != R_OK) return rc;
+  g1 q = {*x, *y, fp_one()};
+  g1 t = g1_mul_u64s(q, R_ORDER, 256);
+  return g1_inf(&t) ? R_OK : R_SUBGROUP;
+}
+
+/* ------------------------------------------------------------------ Fr (4 x 64-bit Montgomery, R = 2^256) */
+typedef struct { u64 v[4]; } fr;
+static int fr_geq(const fr* a) {
+  for (int i = 3; i >= 0; --i) { if (a->v[i] > FR_[i]) return 1; if (a->v[i] < FR_[i]) return 0; }
+  return 1;
+}
+static void fr_subr(fr* a) {
+  u128 b = 0;
+  for (int i = 0; i < 4; ++i) { u128 d = (u128)a->v[i] - FR_[i] - b; a->v[i] = (u64)d; b = (d >> 64) & 1; }
+}
+static fr fr_mul(fr a, fr b) { /* CIOS */
+  u64 t[6] = {0};
+  for (int i = 0; i < 4; ++i) {
+    u128 c = 0;
+    for (int j = 0; j < 4; ++j) { c += (u128)a.v[j] * b.v[i] + t[j]; t[j] = (u64)c; c >>= 64; }
+    c += t[4]; t[4] = (u64)c; t[5] = (u64)(c >> 64);
+    u64 m = t[0] * FR_INV;
+    c = (u128)m * FR_[0] + t[0]; c >>= 64;
+    for (int j = 1; j < 4; ++j) { c += (u128)m * FR_[j] + t[j]; t[j - 1] = (u64)c; c >>= 64; }
+    c += t[4]; t[3] = (u64)c; t[4] = t[5] + (u64)(c >> 64);
+  }
+  fr r; memcpy(r.v, t, 32);
+  if (t[4] || fr_geq(&r)) fr_subr(&r);
+  return r;
+}
+static fr fr_from_u64(u64 x) { fr a = {{x, 0, 0, 0}}, r2; memcpy(r2.v, FR_R2, 32); return fr_mul(a, r2); }
+static fr fr_sub(fr a, fr b) {
+  u128 br = 0; fr r;
+  for (int i = 0; i < 4; ++i) { u128 d = (u128)a.v[i] - b.v[i] - br; r.v[i] = (u64)d; br = (d >> 64) & 1; }
+  if (br) { u128 c = 0; for (int i = 0; i < 4; ++i) { c += (u128)r.v[i] + FR_[i]; r.v[i] = (u64)c; c >>= 64; } }
+  return r;
+}
+static fr fr_inv(fr a) {
+  fr r = fr_from_u64(1);
+  for (int i = 254; i >= 0; --i) { r = fr_mul(r, r); if ((FR_EM2[i >> 6] >> (i & 63)) & 1) r = fr_mul(r, a); }
+  return r;
+}
+static void fr_to_u64s(fr a, u64 out[4]) { fr one = {{1, 0, 0, 0}}; fr s = fr_mul(a, one); memcpy(out, s.v, 32); }
 
 /* ------------------------------------------------------------------ pairing check */
 typedef struct { fp2 x, y, z; } g2p;
@@ -536,5 +673,157 @@ int ref_verify_batch(int chained, const uint8_t* pk48, size_t n, const u64* roun
     pthread_create(&tid[t], NULL, worker, &jobs[t]);
   }
   for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ signatures on G1 (bls-unchained-on-g1 and its RFC DST) */
+/* VerifyBeacon for the G1-signature schemes: msg = SHA-256(BE64(round)) hashed
+   to G1 (legacy: the G2 suite's DST; rfc: the G1 suite's), signature 48-byte
+   G1, key 96-byte G2: e(H, pk) e(-sig, g2) == 1.  Reason codes as above;
+   100 = bad key. */
+int ref_verify_beacon_g1(int rfc_dst, const uint8_t* pk96, u64 round, const uint8_t* sig, size_t sig_len) {
+  fp2 kx, ky;
+  if (g2_decode(&kx, &ky, pk96, 96) != R_OK) return 100;
+  fp sx, sy;
+  int rc = g1_decode_sig(&sx, &sy, sig, sig_len);
+  if (rc != R_OK) return rc;
+  uint8_t m[32];
+  ref_digest(0, NULL, 0, round, m);
+  g1 h = hash_to_g1(m, rfc_dst ? DST_G1 : DST);
+  fp hx, hy;
+  g1_affine(&h, &hx, &hy);
+  fp12 f = miller2(kx, ky, hx, hy, f2c(G2X), f2c(G2Y), sx, fp_neg(sy));
+  return f12_is_one(final_exp(f)) ? R_OK : R_PAIRING;
+}
+
+void ref_hash_to_g1(int rfc_dst, const uint8_t* msg32, uint8_t* out48) {
+  g1 h = hash_to_g1(msg32, rfc_dst ? DST_G1 : DST);
+  fp x, y;
+  g1_affine(&h, &x, &y);
+  fp_to_be48(x, out48);
+  out48[0] |= 0x80;
+  if (fp_gt_half(y)) out48[0] |= 0x20;
+}
+
+typedef struct { int rfc; const uint8_t* pk; size_t lo, hi; const u64* rounds; const uint8_t* sigs; size_t sig_stride;
+                 const uint32_t* sig_len; uint8_t* reason; } job_g1_t;
+static void* worker_g1(void* arg) {
+  job_g1_t* j = (job_g1_t*)arg;
+  for (size_t i = j->lo; i < j->hi; ++i)
+    j->reason[i] = (uint8_t)ref_verify_beacon_g1(j->rfc, j->pk, j->rounds[i], j->sigs + i * j->sig_stride, j->sig_len[i]);
+  return NULL;
+}
+int ref_verify_batch_g1(int rfc_dst, const uint8_t* pk96, size_t n, const u64* rounds, const uint8_t* sigs,
+                        size_t sig_stride, const uint32_t* sig_len, int threads, uint8_t* reason) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  job_g1_t jobs[256];
+  for (int t = 0; t < threads; ++t) {
+    jobs[t] = (job_g1_t){rfc_dst, pk96, n * t / threads, n * (t + 1) / threads, rounds, sigs, sig_stride, sig_len, reason};
+    pthread_create(&tid[t], NULL, worker_g1, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  return 0;
+}
+
+/* ------------------------------------------------------------------ threshold recovery (kyber tbls.Recover (R)) */
+/* Restates oracle/drand_ref.recover: walk the partials in order, keep those
+   whose index is readable and that pass VerifyPartial against
+   PubPoly.Eval(index) = sum_j C_j (index + 1)^j, stop at t; sort by index,
+   first t distinct; Lagrange at 0 over x = index + 1 (Fr); G2 MSM; then
+   VerifyRecovered under C_0.  Returns 1 and the 96-byte signature, or 0. */
+static int verify_pt(fp px, fp py, const uint8_t* msg32, const uint8_t* sig, size_t len, fp2* sx, fp2* sy) {
+  int rc = g2_decode(sx, sy, sig, len);
+  if (rc != R_OK) return rc;
+  g2 h = hash_to_g2(msg32);
+  fp2 hx, hy;
+  g2_affine(&h, &hx, &hy);
+  fp12 f = miller2(hx, hy, px, py, *sx, *sy, fpc(G1X), fp_neg(fpc(G1Y)));
+  return f12_is_one(final_exp(f)) ? R_OK : R_PAIRING;
+}
+int ref_recover(const uint8_t* commits48, int t, const uint8_t* msg32, const uint8_t* partials, size_t pstride,
+                const uint32_t* plen, int m, uint8_t* out96) {
+  if (t < 1 || t > 64) return 0;
+  g1 C[64];
+  for (int j = 0; j < t; ++j) {
+    fp x, y;
+    if (g1_decode(&x, &y, commits48 + 48 * j) != R_OK) return 0;
+    C[j] = (g1){x, y, fp_one()};
+  }
+  int idx[64], cnt = 0;
+  fp2 sx[64], sy[64];
+  for (int k = 0; k < m && cnt < t; ++k) {
+    const uint8_t* pp = partials + (size_t)k * pstride;
+    if (plen[k] < 2) continue;
+    int i = (pp[0] << 8) | pp[1];
+    u64 xv = (u64)i + 1;
+    g1 e = C[t - 1];
+    for (int j = t - 2; j >= 0; --j) e = g1_add(g1_mul_u64s(e, &xv, 17), C[j]);
+    if (g1_inf(&e)) continue;
+    fp ex, ey;
+    g1_affine(&e, &ex, &ey);
+    if (verify_pt(ex, ey, msg32, pp + 2, plen[k] - 2, &sx[cnt], &sy[cnt]) != R_OK) continue;
+    idx[cnt++] = i;
+  }
+  /* sort by index (stable), first t distinct */
+  for (int a = 1; a < cnt; ++a)
+    for (int b = a; b > 0 && idx[b - 1] > idx[b]; --b) {
+      int ti = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = ti;
+      fp2 tx = sx[b]; sx[b] = sx[b - 1]; sx[b - 1] = tx;
+      fp2 ty = sy[b]; sy[b] = sy[b - 1]; sy[b - 1] = ty;
+    }
+  int sel[64], ns = 0;
+  for (int a = 0; a < cnt && ns < t; ++a)
+    if (ns == 0 || idx[sel[ns - 1]] != idx[a]) sel[ns++] = a;
+  if (ns < t) return 0;
+  g2 acc = g2_infinity();
+  for (int a = 0; a < ns; ++a) {
+    fr xa = fr_from_u64((u64)idx[sel[a]] + 1), num = fr_from_u64(1), den = fr_from_u64(1);
+    for (int b = 0; b < ns; ++b) {
+      if (b == a) continue;
+      fr xb = fr_from_u64((u64)idx[sel[b]] + 1);
+      num = fr_mul(num, xb);
+      den = fr_mul(den, fr_sub(xb, xa));
+    }
+    u64 lam[4];
+    fr_to_u64s(fr_mul(num, fr_inv(den)), lam);
+    g2 q = {sx[sel[a]], sy[sel[a]], f2_one()};
+    acc = g2_add(acc, g2_mul_u64s(q, lam, 256));
+  }
+  if (g2_inf(&acc)) return 0;
+  fp2 x, y;
+  g2_affine(&acc, &x, &y);
+  fp_to_be48(x.c1, out96);
+  fp_to_be48(x.c0, out96 + 48);
+  out96[0] |= 0x80;
+  if (f2_lexi(y)) out96[0] |= 0x20;
+  fp cx, cy;
+  g1_affine(&C[0], &cx, &cy);
+  fp2 rx, ry;
+  return verify_pt(cx, cy, msg32, out96, 96, &rx, &ry) == R_OK;
+}
+
+typedef struct { const uint8_t* commits; int t; const uint8_t* msgs; const uint8_t* parts; size_t pstride;
+                 const uint32_t* plen; int m; size_t lo, hi; uint8_t* out; uint8_t* ok; } job_rec_t;
+static void* worker_rec(void* arg) {
+  job_rec_t* j = (job_rec_t*)arg;
+  for (size_t r = j->lo; r < j->hi; ++r)
+    j->ok[r] = (uint8_t)ref_recover(j->commits, j->t, j->msgs + 32 * r, j->parts + r * j->m * j->pstride, j->pstride,
+                                    j->plen + r * j->m, j->m, j->out + 96 * r);
+  return NULL;
+}
+int ref_recover_batch(const uint8_t* commits48, int t, size_t n_rounds, const uint8_t* msgs32, const uint8_t* partials,
+                      size_t pstride, const uint32_t* plen, int m, int threads, uint8_t* out96, uint8_t* ok) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  job_rec_t jobs[256];
+  for (int k = 0; k < threads; ++k) {
+    jobs[k] = (job_rec_t){commits48, t, msgs32, partials, pstride, plen, m, n_rounds * k / threads,
+                          n_rounds * (k + 1) / threads, out96, ok};
+    pthread_create(&tid[k], NULL, worker_rec, &jobs[k]);
+  }
+  for (int k = 0; k < threads; ++k) pthread_join(tid[k], NULL);
   return 0;
 }

@@ -19,24 +19,30 @@ SCHEME_BY_CODE = {0: "pedersen-bls-chained", 1: "pedersen-bls-unchained", 2: "bl
 def run(chain, seconds, cores, expect_valid=None):
     n = len(chain)
     chained = chain.scheme_code == 0
-    if chain.scheme_code >= 2:  # the C restatement covers G2 signatures only
-        return _run_py(chain, seconds, cores, "signatures on G1", expect_valid)
+    on_g1 = chain.scheme_code >= 2
     try:
         from oracle import c_ref
         c_ref.load()
-        impl = "oracle/c/bls381_ref.c (C restatement, 6x64-bit limbs, [r]Q subgroup test as kilic (R))"
+        if on_g1:  # bls-unchained-on-g1 (G2 suite's DST) / bls-unchained-g1-rfc9380 (G1 DST)
+            rfc = chain.scheme_code == 3
+            impl = ("oracle/c/bls381_ref.c (C restatement, 6x64-bit limbs: RFC 9380 hash to G1, [r]P subgroup test, "
+                    "e(H, pk) e(-sig, g2))")
+            verify = lambda sub, thr: c_ref.verify_batch_g1(rfc, chain.pk, sub[0], sub[1], sub[2], thr)  # noqa: E731
+        else:
+            impl = "oracle/c/bls381_ref.c (C restatement, 6x64-bit limbs, [r]Q subgroup test as kilic (R))"
+            verify = lambda sub, thr: c_ref.verify_batch(chained, chain.pk, *sub, thr)  # noqa: E731
+        cols = (chain.rounds, chain.sigs, chain.sig_len, chain.prev, chain.prev_len)
         # calibrate on a few rounds single-threaded
         idx0 = np.arange(min(4, n))
         t = time.perf_counter()
-        c_ref.verify_batch(chained, chain.pk, chain.rounds[idx0], chain.sigs[idx0], chain.sig_len[idx0],
-                           chain.prev[idx0], chain.prev_len[idx0], 1)
+        verify([np.ascontiguousarray(a[idx0]) for a in cols], 1)
         per = (time.perf_counter() - t) / len(idx0)
         sample = int(max(cores, min(n, seconds * cores / max(per, 1e-6))))
         rng = np.random.default_rng(12345)
         idx = np.sort(rng.choice(n, size=sample, replace=False))
-        sub = [np.ascontiguousarray(a[idx]) for a in (chain.rounds, chain.sigs, chain.sig_len, chain.prev, chain.prev_len)]
+        sub = [np.ascontiguousarray(a[idx]) for a in cols]
         t = time.perf_counter()
-        reason = c_ref.verify_batch(chained, chain.pk, *sub, cores)
+        reason = verify(sub, cores)
         wall = time.perf_counter() - t
     except Exception as e:  # C build unavailable: pure-Python oracle
         return _run_py(chain, seconds, cores, repr(e))
@@ -116,10 +122,36 @@ def _rec_round(args):
 
 
 def run_recover(commits, t, n, msgs, parts, expect_sigs, seconds, cores):
-    """Bounded sample of the bench's recovery batch on `cores` processes:
-    C restatement pairings (t VerifyPartial + 1 VerifyRecovered per round),
-    Lagrange + G2 MSM in the Python oracle.  Checks against the expected
-    recovered signatures (None = failure)."""
+    """Bounded sample of the bench's recovery batch on `cores` threads of the
+    C restatement (oracle/c ref_recover: t VerifyPartial pairings, Lagrange in
+    Fr, G2 MSM, VerifyRecovered), checked against the expected recovered
+    signatures (None = failure).  Falls back to the Python Lagrange/MSM with
+    C pairings if the C recovery is unavailable."""
+    nr = len(msgs)
+    try:
+        from oracle import c_ref
+        c_ref.load()
+        t0 = time.perf_counter()
+        c_ref.recover_batch(commits, t, msgs[:1], parts[:1], 1)
+        per = time.perf_counter() - t0
+        sample = int(max(cores, min(nr, seconds * cores / max(per, 1e-6))))
+        idx = np.sort(np.random.default_rng(12345).choice(nr, size=sample, replace=False))
+        t0 = time.perf_counter()
+        sigs, ok = c_ref.recover_batch(commits, t, np.ascontiguousarray(msgs[idx]), np.ascontiguousarray(parts[idx]),
+                                       cores)
+        wall = time.perf_counter() - t0
+        mism = sum(1 for k, i in enumerate(idx) if (bytes(sigs[k]) if ok[k] else None) != expect_sigs[i])
+        return {"value": sample / wall, "unit": "rounds/s", "cores": cores, "kind": "port",
+                "impl": "oracle/c/bls381_ref.c ref_recover (C restatement of kyber tbls.Recover (R): VerifyPartial x t, "
+                        "Lagrange in Fr, G2 MSM, VerifyRecovered)",
+                "sample": f"{sample} uniformly sampled rounds of the bench batch", "wall_s": wall,
+                "single_core_ms_per_round": per * 1e3, "sample_mismatches": mism}
+    except (OSError, AttributeError):
+        return _run_recover_py(commits, t, n, msgs, parts, expect_sigs, seconds, cores)
+
+
+def _run_recover_py(commits, t, n, msgs, parts, expect_sigs, seconds, cores):
+    """Python selection / Lagrange / MSM with C pairings (fallback)."""
     from concurrent.futures import ProcessPoolExecutor
     nr = len(msgs)
     _rec_init(commits, t, n)

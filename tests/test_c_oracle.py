@@ -54,3 +54,35 @@ def test_batch_threads(cref):
     sigs[3, 0] ^= 0x20
     reason = cref.verify_batch(True, bytes.fromhex(g["pk"]), rounds, sigs, np.full(n, 96, dtype=np.uint32), prev, plen, 4)
     assert reason.tolist() == [0, 0, 0, 3, 0, 0, 0, 0]
+
+
+def test_hash_to_g1_golden(cref):
+    """The C hash to G1 (both DSTs of the G1-signature schemes) == the oracle's fixture."""
+    for c in load_golden("hash_to_g1.json")["cases"]:
+        if not c["msg"] or "QUUX" in c["dst"]:
+            continue
+        rfc = "BLS12381G1_XMD" in c["dst"]
+        assert cref.hash_to_g1(rfc, bytes.fromhex(c["msg"])).hex() == c["h"]
+
+
+@pytest.mark.parametrize("name", ["chain_on_g1_s1.json", "chain_g1_rfc9380_s2.json"])
+def test_g1_chain_verdicts_and_reasons(cref, name):
+    """VerifyBeacon for signatures on G1 in C == the oracle's fixture reasons
+    (the C cpu_baseline of configs[3]'s on-G1 chain)."""
+    g = load_golden(name)
+    rfc = g["scheme"] == "bls-unchained-g1-rfc9380"
+    pk = bytes.fromhex(g["pk"])
+    for r in g["rounds"][:4]:
+        assert cref.verify_beacon_g1(rfc, pk, r["round"], bytes.fromhex(r["sig"])) == 0
+    for c in g["corrupted"]:
+        assert cref.verify_beacon_g1(rfc, pk, c["round"], bytes.fromhex(c["sig"])) == c["reason"], c["kind"]
+
+
+def test_recover_golden(cref):
+    """Threshold recovery in C (Lagrange in Fr, G2 MSM, VerifyPartial /
+    VerifyRecovered pairings) == the oracle's recover fixtures."""
+    g = load_golden("recover_t3_n8.json")
+    commits = [bytes.fromhex(c) for c in g["commits"]]
+    for case in g["cases"]:
+        got = cref.recover(commits, g["t"], bytes.fromhex(case["msg"]), [bytes.fromhex(p) for p in case["partials"]])
+        assert (got.hex() if got else None) == case["recovered"], case["kind"]

@@ -233,3 +233,41 @@ def test_verify_multi_one_device_equals_single_context(mode, gpu_ctx):
     expect[list(bad.keys())] = False
     assert np.array_equal(got == 0, expect)
     assert not clean.any()
+
+
+def test_async_calls_on_two_streams_are_ordered(gpu_ctx):
+    """Two dgpu_verify_beacons_device calls on different streams share the
+    context's scratch; the second is ordered after the first on the device
+    (ADVICE r01), so both verdict sets are right."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    dev = torch.device("cuda", 0)
+    chains = [make_chain(71 + k, 40000, _lib.SCHEME_CHAINED, seg_len=64) for k in range(2)]
+    bads = [corrupt(c, 71 + k, rate=1e-3) for k, c in enumerate(chains)]
+    from drand_amd.chain import Verifier
+    v = Verifier(_sch("pedersen-bls-chained"))
+    for c in chains:  # both keys cached first: the async calls below never synchronize on a key decode
+        v.verify_reasons([c.beacon(0)], c.pk)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    outs = []
+    keep = []
+    for c, st in zip(chains, streams):
+        t = [torch.from_numpy(a).to(dev) for a in (c.rounds.view(np.int64), c.sigs, c.sig_len.view(np.int32), c.prev,
+                                                  c.prev_len.view(np.int32))]
+        torch.cuda.synchronize()
+        bits = torch.zeros((len(c) + 7) // 8, dtype=torch.uint8, device=dev)
+        pk = np.frombuffer(c.pk, dtype=np.uint8).copy()
+        keep.append((t, pk))
+        _lib.check(gpu_ctx.lib.dgpu_verify_beacons_device(
+            gpu_ctx.handle, _lib.SCHEME_CHAINED, _lib.ptr(pk), pk.size, len(c), t[0].data_ptr(), t[1].data_ptr(), 96,
+            t[2].data_ptr(), t[3].data_ptr(), 96, t[4].data_ptr(), _lib.MODE_PER_ROUND, 0, bits.data_ptr(), None,
+            ctypes.c_void_p(st.cuda_stream)))
+        outs.append(bits)
+    torch.cuda.synchronize()
+    for c, bad, bits in zip(chains, bads, outs):
+        got = np.unpackbits(bits.cpu().numpy(), bitorder="little")[: len(c)].astype(bool)
+        expect = np.ones(len(c), dtype=bool)
+        expect[list(bad.keys())] = False
+        assert np.array_equal(got, expect)

@@ -97,7 +97,13 @@ struct eng_io {
 // The program interpreter (one inlined copy of the op interpreter per kernel).
 // FIXED: LDLINE reads the per-key line table and scales it by the lane's P
 // coordinate (the on-G1 lines, computed in place of k_eng_lines_fixed).
-template <bool FIXED = false>
+// CYC: E_CYC runs straight-line (engine.cuh eng_cyc_fast), the FE kernel only.
+#ifndef DG_ENG_NO_CYC_FAST
+constexpr bool ENG_CYC_FAST = true;
+#else
+constexpr bool ENG_CYC_FAST = false;
+#endif
+template <bool FIXED = false, bool CYC = false>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
@@ -111,7 +117,8 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     const uint32_t ins = prog[pc];
     const uint32_t opc = ins >> 24, a = ins & 0xFFu, b = (ins >> 8) & 0xFFu;
     if (opc == ENG_OPC_RUN) {
-      eng_run((int)a, g, c, L.k, sink);
+      if (CYC && a == OP_E_CYC) eng_cyc_fast(g, L.k);
+      else eng_run((int)a, g, c, L.k, sink);
     } else if (opc == ENG_OPC_STEP) {
       ++step;
     } else if (opc == ENG_OPC_LDLINE) {
@@ -258,7 +265,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, 
   eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(2, 0, L.g, L.k)));
   if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
   asm volatile("" ::: "memory");
-  eng_exec(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});
+  eng_exec<false, ENG_CYC_FAST>(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});
   const fp v = eng_ld(g + (ENG_E_R + L.k) * ENG_SLOT_WORDS);
   const bool ok = eng_eq_canon(v, L.k == 0 ? fp_one() : fp_zero());
   const uint64_t m = __ballot(ok);

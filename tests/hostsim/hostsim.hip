@@ -254,7 +254,22 @@ struct HostGroup {
   void set(int slot, const fp& v) { eng_st(s + slot * ENG_SLOT_WORDS, v); }
 };
 
+bool g_cyc_fast = false;
+
+// eng_cyc_fast's two sub-ops for the 12 lanes (read all, then write all)
+void host_cyc_fast(HostGroup& G) {
+  fp outs[ENG_LANES];
+  for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_cyc_lin(G.s, ENG_CYC_PAR[k]);
+  for (int k = 0; k < ENG_LANES; ++k) eng_st(G.s + (ENG_CYC_PAR[k][0] & 0xFFFFu), outs[k]);
+  for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_cyc_prod(G.s, ENG_CYC_PAR[k]);
+  for (int k = 0; k < ENG_LANES; ++k) eng_st(G.s + (ENG_CYC_PAR[k][5] >> 16), outs[k]);
+}
+
 void host_run_op(HostGroup& G, int op) {
+  if (g_cyc_fast && op == OP_E_CYC) {
+    host_cyc_fast(G);
+    return;
+  }
   const uint32_t s0 = ENG_OP_TAB[op][0], ns = ENG_OP_TAB[op][1];
   for (uint32_t sb = s0; sb < s0 + ns; ++sb) {
     const uint32_t off = ENG_SUB_TAB[sb][0], nt = ENG_SUB_TAB[sb][1];
@@ -317,6 +332,32 @@ bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 // fused test (k_eng_lines status, tools/gen_engine.py lines_subgroup_op):
 // the point is pair 1's Q (pair 0 a dummy copy).  Returns 1 in G2, 0 not,
 // -1 undecodable.
+extern "C" void hs_eng_set_cyc_fast(int on) { g_cyc_fast = on != 0; }
+
+// E_CYC interpreted vs straight-line on the same random group slots (values
+// < p, normalized limbs), `reps` squarings in a row: 0 iff every slot word is
+// identical after every squaring.
+extern "C" int hs_eng_cyc_compare(uint64_t seed, int reps) {
+  HostGroup A, B;
+  uint64_t x = seed | 1;
+  for (int i = 0; i < 64 * ENG_SLOT_WORDS; ++i) {
+    x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+    const int limb = i % ENG_SLOT_WORDS;
+    A.s[i] = limb == FP_LIMBS - 1 ? (uint32_t)(x % FP_P[FP_LIMBS - 1]) : (uint32_t)(x & FP_MASK);
+  }
+  memset(A.c, 0, sizeof A.c);
+  B = A;
+  for (int r = 0; r < reps; ++r) {
+    g_cyc_fast = false;
+    host_run_op(A, OP_E_CYC);
+    g_cyc_fast = true;
+    host_run_op(B, OP_E_CYC);
+    g_cyc_fast = false;
+    if (memcmp(A.s, B.s, sizeof A.s) != 0) return r + 1;
+  }
+  return 0;
+}
+
 extern "C" int hs_eng_subgroup(const uint8_t* sig96) {
   g2a s;
   if (g2_decompress(&s, sig96, false) != DEC_OK) return -1;

@@ -170,6 +170,27 @@ def test_engine_pairing_host_emulation(hostsim):
         assert got == [c % P for pair in w for c in pair]
 
 
+def test_engine_fast_cyc_bit_identical(hostsim):
+    """The straight-line cyclotomic squaring (engine.cuh eng_cyc_fast) leaves
+    every slot word identical to the interpreted E_CYC op, over chains of
+    squarings from random slot contents, and the full pairing check through
+    the FE program gives the same GT value with it."""
+    for seed in (1, 2, 3, 0xDEADBEEF):
+        assert hostsim.hs_eng_cyc_compare(ctypes.c_uint64(seed), 40) == 0
+    sk = D.derive_secret(12)
+    pk48 = B.g1_compress(B.g1_mul(B.G1_GEN, sk))
+    msg = b"\x09" * 32
+    sig = B.g2_compress(B.g2_mul(B.hash_to_g2(msg), sk))
+    outs = []
+    for fast in (0, 1):
+        hostsim.hs_eng_set_cyc_fast(fast)
+        out = buf(576)
+        assert hostsim.hs_eng_pairing(pk48, msg, sig, out) == 1
+        outs.append(out.raw)
+    hostsim.hs_eng_set_cyc_fast(0)
+    assert outs[0] == outs[1]
+
+
 def test_hash_to_g1_golden(hostsim):
     """Kernel hash-to-G1 (inversion-free SSWU + 11-isogeny, both DSTs) vs the
     oracle's fixture, including drand digests under the legacy and RFC DSTs."""

@@ -33,6 +33,7 @@ import sys
 LANES = 12
 MAX_GROUP_SLOTS = 64
 MAX_TERMS = 12        # engine.cuh prefetches a lane's term words into a 12-entry FIFO
+SLOT_WORDS = 14       # 14 limbs of 28 bits, one 32-bit word each
 
 # ---------------------------------------------------------------- block constant slots (>= 64)
 C_ONE = 64
@@ -731,6 +732,52 @@ def encode(ops):
     return op_tab, sub_tab, words
 
 
+def cyc_fast_params(ops, name="E_CYC"):
+    """Per-lane parameters of the straight-line cyclotomic squaring
+    (engine.cuh eng_cyc_fast): the op's two sub-ops, decoded once here.
+    Sub-op 0 (LIN): out = x + y or x - y; sub-op 1: out = cm * redc(sum of <= 3
+    products) + d * post, with cm = ENG_CYC_CM and |d| = ENG_CYC_ABSD the same
+    for every lane.  Offsets are group-relative word offsets (slot * 14).
+    Word layout per lane (8 words):
+      0: lin dst | lin x << 16      1: lin y | (lin y negated) << 16
+      2..4: term t operands a | b << 16 (unused terms: 0, 0)
+      5: post | dst << 16
+      6: flags: bit 2t = term t negated, bit 2t+1 = term t doubled,
+         bits 8..9 = term count, bits 16..23 = cm (int8), 24..31 = d (int8)
+      7: 0"""
+    op = {o.name: o for o in ops}[name]
+    assert len(op.subs) == 2
+    lin, prod = op.subs
+    assert len(lin) == LANES and len(prod) == LANES
+    slot = SLOT_WORDS
+    rows = []
+    assert len({r.cm for r in prod}) == 1 and len({abs(r.post[0][1]) for r in prod}) == 1
+    for k in range(LANES):
+        lr, pr = lin[k], prod[k]
+        assert not lr.terms and len(lr.post) == 2 and lr.post[0][1] == 1 and abs(lr.post[1][1]) == 1
+        assert lr.dst is not None and lr.exp is None and pr.dst is not None and pr.exp is None
+        assert 2 <= len(pr.terms) <= 3 and len(pr.post) == 1 and -128 <= pr.cm < 128
+        (x, _), (y, dy) = lr.post
+        terms = sorted(pr.terms, key=lambda t: (t[2] < 0) + (t[3] == 2))
+        w = [lr.dst * slot | (x * slot) << 16, y * slot | (1 if dy < 0 else 0) << 16]
+        flags = 0
+        for t in range(3):
+            if t < len(terms):
+                a, b, sg, cf = terms[t]
+                assert a < 64 and b < 64
+                w.append(a * slot | (b * slot) << 16)
+                flags |= (sg < 0) << (2 * t) | (cf == 2) << (2 * t + 1)
+            else:
+                w.append(0)
+        (ps, d), = pr.post
+        assert ps < 64 and -128 <= d < 128
+        w.append(ps * slot | (pr.dst * slot) << 16)
+        flags |= len(terms) << 8 | (pr.cm & 0xFF) << 16 | (d & 0xFF) << 24
+        w += [flags, 0]
+        rows.append(w)
+    return rows
+
+
 def check_bounds(ops):
     """Static bounds the device arithmetic relies on (see engine.cuh):
     slot values < 2.01p; product sum < 2048 p^2 so redc < 1.8p; the post
@@ -806,6 +853,14 @@ def emit(path):
     lines.append(f"alignas(16) ENG_TABLE_QUAL uint32_t ENG_WORDS[{len(words)}] = {{")
     for i in range(0, len(words), 12):
         lines.append("  " + ", ".join(f"0x{w:08x}u" for w in words[i:i + 12]) + ",")
+    lines.append("};")
+    rows = cyc_fast_params(ops)
+    cyc = {o.name: o for o in ops}["E_CYC"].subs[1]
+    lines.append("// eng_cyc_fast: per-lane parameters of E_CYC (tools/gen_engine.py cyc_fast_params)")
+    lines.append(f"constexpr int ENG_CYC_CM = {cyc[0].cm}, ENG_CYC_ABSD = {abs(cyc[0].post[0][1])};")
+    lines.append(f"alignas(16) ENG_TABLE_QUAL uint32_t ENG_CYC_PAR[{LANES}][8] = {{")
+    for w in rows:
+        lines.append("  {" + ", ".join(f"0x{x:08x}u" for x in w) + "},")
     lines.append("};")
     op_index = {op.name: i for i, op in enumerate(ops)}
     lines.append(f"constexpr uint32_t ENG_OPC_RUN = {OPC['run']}, ENG_OPC_STEP = {OPC['step']}, ENG_OPC_LDLINE = {OPC['ldline']}, "

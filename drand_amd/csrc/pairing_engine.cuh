@@ -107,6 +107,7 @@ template <bool FIXED = false, bool CYC = false>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
+  bool cyc_lin_ready = false;  // the previous op was an E_CYC: its epilogue wrote E_CYC's LIN outputs
   auto sink = [&](uint32_t e, const fp& v) {
     if (!L.valid) return;
     if (e < 12) st_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, (int)e), v);
@@ -117,8 +118,13 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     const uint32_t ins = prog[pc];
     const uint32_t opc = ins >> 24, a = ins & 0xFFu, b = (ins >> 8) & 0xFFu;
     if (opc == ENG_OPC_RUN) {
-      if (CYC && a == OP_E_CYC) eng_cyc_fast(g, L.k);
-      else eng_run((int)a, g, c, L.k, sink);
+      if (CYC && a == OP_E_CYC) {
+        if (cyc_lin_ready) eng_cyc_fast<false>(g, L.k);
+        else eng_cyc_fast<true>(g, L.k);
+        cyc_lin_ready = true;
+        continue;
+      }
+      eng_run((int)a, g, c, L.k, sink);
     } else if (opc == ENG_OPC_STEP) {
       ++step;
     } else if (opc == ENG_OPC_LDLINE) {
@@ -135,6 +141,7 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     } else if (opc == ENG_OPC_ST12) {
       if (L.valid) st_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
     }
+    cyc_lin_ready = false;
     asm volatile("" ::: "memory");
   }
 }

@@ -250,26 +250,36 @@ struct HostGroup {
   fp fbuf[24];
   fp n1;
   int step = 0;
+  bool cyc_ready = false;   // eng_exec's cyc_lin_ready
   fp get(int slot) const { return eng_ld(s + slot * ENG_SLOT_WORDS); }
   void set(int slot, const fp& v) { eng_st(s + slot * ENG_SLOT_WORDS, v); }
 };
 
 bool g_cyc_fast = false;
 
-// eng_cyc_fast's two sub-ops for the 12 lanes (read all, then write all)
-void host_cyc_fast(HostGroup& G) {
-  fp outs[ENG_LANES];
-  for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_cyc_lin(G.s, ENG_CYC_PAR[k]);
-  for (int k = 0; k < ENG_LANES; ++k) eng_st(G.s + (ENG_CYC_PAR[k][0] & 0xFFFFu), outs[k]);
+// eng_cyc_fast for the 12 lanes (read all, then write all); `lin`: run the
+// LIN sub-op (else the previous E_CYC's fused epilogue wrote its outputs)
+void host_cyc_fast(HostGroup& G, bool lin) {
+  fp outs[ENG_LANES], fused[ENG_LANES];
+  if (lin) {
+    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_cyc_lin(G.s, ENG_CYC_PAR[k]);
+    for (int k = 0; k < ENG_LANES; ++k) eng_st(G.s + (ENG_CYC_PAR[k][0] & 0xFFFFu), outs[k]);
+  }
   for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_cyc_prod(G.s, ENG_CYC_PAR[k]);
-  for (int k = 0; k < ENG_LANES; ++k) eng_st(G.s + (ENG_CYC_PAR[k][5] >> 16), outs[k]);
+  for (int k = 0; k < ENG_LANES; ++k) fused[k] = eng_cyc_fused_lin(outs[k], outs[k ^ 1], k);
+  for (int k = 0; k < ENG_LANES; ++k) {
+    eng_st(G.s + (ENG_CYC_PAR[k][5] >> 16), outs[k]);
+    eng_st(G.s + ENG_CYC_PAR[k][7], fused[k]);
+  }
 }
 
 void host_run_op(HostGroup& G, int op) {
   if (g_cyc_fast && op == OP_E_CYC) {
-    host_cyc_fast(G);
+    host_cyc_fast(G, !G.cyc_ready);
+    G.cyc_ready = true;
     return;
   }
+  G.cyc_ready = false;
   const uint32_t s0 = ENG_OP_TAB[op][0], ns = ENG_OP_TAB[op][1];
   for (uint32_t sb = s0; sb < s0 + ns; ++sb) {
     const uint32_t off = ENG_SUB_TAB[sb][0], nt = ENG_SUB_TAB[sb][1];
@@ -290,6 +300,7 @@ void host_run_op(HostGroup& G, int op) {
 void host_exec(HostGroup& G, const uint32_t* prog, int len) {
   for (int pc = 0; pc < len; ++pc) {
     const uint32_t ins = prog[pc], opc = ins >> 24, a = ins & 0xFF, b = (ins >> 8) & 0xFF;
+    if (opc != ENG_OPC_RUN) G.cyc_ready = false;
     if (opc == ENG_OPC_RUN) host_run_op(G, (int)a);
     else if (opc == ENG_OPC_STEP) G.step++;
     else if (opc == ENG_OPC_LDLINE) {
@@ -334,9 +345,16 @@ bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 // -1 undecodable.
 extern "C" void hs_eng_set_cyc_fast(int on) { g_cyc_fast = on != 0; }
 
-// E_CYC interpreted vs straight-line on the same random group slots (values
-// < p, normalized limbs), `reps` squarings in a row: 0 iff every slot word is
-// identical after every squaring.
+// canonical residue of a normalized value < 2^392
+static fp host_canon(fp a) {
+  for (int i = 0; i < 12; ++i) a = fp_csub_p(a);
+  return a;
+}
+
+// E_CYC interpreted vs straight-line (fused LIN epilogue from the second
+// squaring on) on the same random group slots (values < p, normalized limbs),
+// `reps` squarings in a row: 0 iff the state (R) and LIN (TMP) slots hold the
+// same residues after every squaring.
 extern "C" int hs_eng_cyc_compare(uint64_t seed, int reps) {
   HostGroup A, B;
   uint64_t x = seed | 1;
@@ -353,7 +371,16 @@ extern "C" int hs_eng_cyc_compare(uint64_t seed, int reps) {
     g_cyc_fast = true;
     host_run_op(B, OP_E_CYC);
     g_cyc_fast = false;
-    if (memcmp(A.s, B.s, sizeof A.s) != 0) return r + 1;
+    for (int sl = 0; sl < 12; ++sl) {
+      const fp x = host_canon(A.get(sl)), y = host_canon(B.get(sl));
+      if (memcmp(&x, &y, sizeof x) != 0) return 1000 * (r + 1) + sl;
+    }
+    // the fused epilogue's LIN slots == the LIN sub-op over the new state
+    for (int k = 0; k < ENG_LANES; ++k) {
+      const fp x = host_canon(eng_cyc_lin(B.s, ENG_CYC_PAR[k]));
+      const fp y = host_canon(eng_ld(B.s + (ENG_CYC_PAR[k][0] & 0xFFFFu)));
+      if (memcmp(&x, &y, sizeof x) != 0) return 1000 * (r + 1) + 100 + k;
+    }
   }
   return 0;
 }

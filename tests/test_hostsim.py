@@ -170,11 +170,12 @@ def test_engine_pairing_host_emulation(hostsim):
         assert got == [c % P for pair in w for c in pair]
 
 
-def test_engine_fast_cyc_bit_identical(hostsim):
-    """The straight-line cyclotomic squaring (engine.cuh eng_cyc_fast) leaves
-    every slot word identical to the interpreted E_CYC op, over chains of
-    squarings from random slot contents, and the full pairing check through
-    the FE program gives the same GT value with it."""
+def test_engine_fast_cyc_matches_interpreter(hostsim):
+    """The straight-line cyclotomic squaring (engine.cuh eng_cyc_fast, with
+    the fused LIN epilogue) leaves every state and LIN slot with the same
+    residue as the interpreted E_CYC op, over chains of squarings from random
+    slot contents, and the full pairing check through the FE program gives
+    the same GT value with it."""
     for seed in (1, 2, 3, 0xDEADBEEF):
         assert hostsim.hs_eng_cyc_compare(ctypes.c_uint64(seed), 40) == 0
     sk = D.derive_secret(12)

@@ -58,8 +58,12 @@ __global__ void __launch_bounds__(64, 3) k_bench(int op, int reps, const uint32_
   uint32_t sink_acc = 0;
 #pragma unroll 1
   for (int r = 0; r < reps; ++r) {
-    if (op < 0) {
-      eng_cyc_fast(g, k);
+    if (op == -1) {  // E_CYC with its LIN sub-op
+      eng_cyc_fast<true>(g, k);
+      continue;
+    }
+    if (op == -2) {  // E_CYC after an E_CYC (fused LIN epilogue)
+      eng_cyc_fast<false>(g, k);
       continue;
     }
 #ifdef ENGBENCH_LDS_RECORDS
@@ -111,7 +115,7 @@ int main(int argc, char** argv) {
       {"LDBL", OP_LDBL, 0},       {"LADD", OP_LADD, 0},       {"M_XIF", OP_M_XIF, 1},     {"M_SQR", OP_M_SQR, 1},
       {"M_XIL", OP_M_XIL, 1},     {"M_LM1", OP_M_LM1, 1},     {"E_CYC", OP_E_CYC, 2},     {"E_MUL", OP_E_MUL, 2},
       {"E_MULCJ", OP_E_MULCJ, 2}, {"E_XIA", OP_E_XIA, 2},     {"E_FROB1", OP_E_FROB1, 2},
-      {"E_CYC_lin", OP_E_CYC, 2, 0, 1}, {"E_CYC_prod", OP_E_CYC, 2, 1, 1}, {"E_CYC_fast", -1, 2},
+      {"E_CYC_lin", OP_E_CYC, 2, 0, 1}, {"E_CYC_prod", OP_E_CYC, 2, 1, 1}, {"E_CYC_fast", -1, 2}, {"E_CYC_chain", -2, 2},
   };
   constexpr int WMAX = (ENG_NCONST + ENG_GROUPS_PER_WAVE * 64) * ENG_SLOT_WORDS;
   std::vector<uint32_t> h((size_t)64 * WMAX);

@@ -744,7 +744,12 @@ def cyc_fast_params(ops, name="E_CYC"):
       5: post | dst << 16
       6: flags: bit 2t = term t negated, bit 2t+1 = term t doubled,
          bits 8..9 = term count, bits 16..23 = cm (int8), 24..31 = d (int8)
-      7: 0"""
+      7: fused LIN destination: the next E_CYC's sub-op 0 output that this
+         lane forms from its own output and its partner lane's (k ^ 1: the
+         other half of the same Fp2 coefficient): re + im on the re lane,
+         re - im on the im lane.
+    The LIN outputs are left unreduced (normalized limbs, value < 10.02p):
+    their only readers are this op's product terms, bounded below."""
     op = {o.name: o for o in ops}[name]
     assert len(op.subs) == 2
     lin, prod = op.subs
@@ -773,8 +778,26 @@ def cyc_fast_params(ops, name="E_CYC"):
         assert ps < 64 and -128 <= d < 128
         w.append(ps * slot | (pr.dst * slot) << 16)
         flags |= len(terms) << 8 | (pr.cm & 0xFF) << 16 | (d & 0xFF) << 24
-        w += [flags, 0]
+        # fused LIN: this lane holds coefficient half pr.dst; partner k ^ 1 the other half
+        assert prod[k ^ 1].dst == pr.dst ^ 1
+        re, im = pr.dst & ~1, pr.dst | 1
+        want = [(re, 1), (im, 1 if pr.dst == re else -1)]
+        fused = [r.dst for r in lin if r.post == want]
+        assert len(fused) == 1, (k, want)
+        w += [flags, fused[0] * slot]
         rows.append(w)
+    # bounds: LIN outputs x + y < 4.02p, x - y + 8p < 10.02p (normalized, unreduced);
+    # every product sum < 2048 p^2 (redc output < 1.06p), <= 4 terms (no column normalization)
+    tmp = {}
+    for r in lin:
+        tmp[r.dst] = 4.02 if r.post[1][1] > 0 else 10.02
+    for r in prod:
+        tot = 0.0
+        for a, b, sg, cf in r.terms:
+            ba, bb = tmp.get(a, 2.01), tmp.get(b, 2.01)
+            assert not (sg < 0 and bb >= 7.99)   # 8p - b needs b < 7.99p
+            tot += cf * ba * (8.0 if sg < 0 else bb)
+        assert tot < 2048 and len(r.terms) <= 4, (r.dst, tot)
     return rows
 
 

@@ -282,9 +282,9 @@ void host_run_op(HostGroup& G, int op) {
   G.cyc_ready = false;
   const uint32_t s0 = ENG_OP_TAB[op][0], ns = ENG_OP_TAB[op][1];
   for (uint32_t sb = s0; sb < s0 + ns; ++sb) {
-    const uint32_t off = ENG_SUB_TAB[sb][0], nt = ENG_SUB_TAB[sb][1];
+    const uint32_t off = ENG_SUB_TAB[sb][0], ntw = ENG_SUB_TAB[sb][1], nt = ntw & 0xFFu;
     fp outs[ENG_LANES];
-    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_compute(G.s, G.c, ENG_WORDS + off + k * eng_rec_words(nt), nt);
+    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_compute(G.s, G.c, ENG_WORDS + off + k * eng_rec_words(nt), ntw);
     for (int k = 0; k < ENG_LANES; ++k) {
       const uint32_t* rec = ENG_WORDS + off + k * eng_rec_words(nt);
       if (eng_dst(rec) != 0xFF) G.set(eng_dst(rec), outs[k]);

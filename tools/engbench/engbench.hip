@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(64, 3) k_bench(int op, int reps, const uint32_
   __shared__ __attribute__((aligned(16))) uint32_t rec[528];  // largest op's record span
   const uint32_t s0 = ENG_OP_TAB[op][0], sl = s0 + ENG_OP_TAB[op][1] - 1;
   const uint32_t w0 = ENG_SUB_TAB[s0][0];
-  const uint32_t w1 = ENG_SUB_TAB[sl][0] + 12 * eng_rec_words(ENG_SUB_TAB[sl][1]);
+  const uint32_t w1 = ENG_SUB_TAB[sl][0] + 12 * eng_rec_words(ENG_SUB_TAB[sl][1] & 0xFFu);
   for (uint32_t t = threadIdx.x; t < w1 - w0; t += blockDim.x) rec[t] = ENG_WORDS[w0 + t];
 #define ENGBENCH_RUN_ARGS , rec, w0
 #elif defined(ENGBENCH_LDS_PAD)   // same LDS footprint, records from global memory

@@ -694,6 +694,71 @@ class ProgramRunner:
 
 
 # ---------------------------------------------------------------- table emission
+# ---------------------------------------------------------------- column normalization schedule
+# engine.cuh accumulates each lane's products in 27 64-bit columns and carries
+# them (normalizes) only where this schedule says: a greedy pass over the
+# sub-op's terms (in encoded order) with exact per-column bounds of every lane,
+# normalizing before a term whenever some lane's column could reach 2^64, and
+# after the last term when the reduction's headroom (2^64 - 2^60: it adds up to
+# 14 (2^28)^2 and a carry) would be exceeded.
+def _p_limbs():
+    from fractions import Fraction  # noqa: F401  (exact integers only)
+    p = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+    return p
+
+
+_P = _p_limbs()
+_SUBK = [(8 * _P >> (28 * i)) & 0xFFFFFFF for i in range(14)]
+
+
+def _subk_limbs():
+    # FP_SUBK (constants.h): 8p with every non-top limb raised by 2^28 (borrowed from the next)
+    v = 8 * _P
+    limbs = [(v >> (28 * i)) & 0xFFFFFFF for i in range(14)]
+    limbs[13] = v >> (28 * 13)
+    out = []
+    for i in range(14):
+        x = limbs[i] + ((1 << 28) if i < 13 else 0) - (1 if i > 0 else 0)
+        out.append(x)
+    return out
+
+
+def _slot_limb_max(bound_p=2.01):
+    top = int(bound_p * _P) >> (28 * 13)
+    return [(1 << 28) - 1] * 13 + [top]
+
+
+def norm_schedule(sub):
+    """Bit t set: normalize after term t (encoded term order)."""
+    amax = _slot_limb_max()
+    subk = _subk_limbs()
+    LIM, LIM_REDC = (1 << 64) - 1, (1 << 64) - (1 << 60)
+    lanes = [sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2)) for r in sub]
+    nt = max([len(t) for t in lanes] + [0])
+    after_norm = [(1 << 28) - 1] * 27 + [1 << 40]
+    cur = [[0] * 28 for _ in lanes]
+    mask = 0
+    for t in range(nt):
+        grow = []
+        for terms in lanes:
+            g = [0] * 28
+            if t < len(terms):
+                _, _, sg, cf = terms[t]
+                bmax = [(subk[j] if sg < 0 else amax[j]) << (cf - 1) for j in range(14)]
+                for i in range(14):
+                    for j in range(14):
+                        g[i + j] += amax[i] * bmax[j]
+            grow.append(g)
+        if t and any(c[k] + g[k] > LIM for c, g in zip(cur, grow) for k in range(28)):
+            mask |= 1 << (t - 1)
+            cur = [list(after_norm) for _ in lanes]
+        cur = [[c[k] + g[k] for k in range(28)] for c, g in zip(cur, grow)]
+        assert all(max(c) <= LIM for c in cur)
+    if nt and any(max(c) > LIM_REDC for c in cur):
+        mask |= 1 << (nt - 1)
+    return mask
+
+
 def encode(ops):
     words = []
     op_tab = []
@@ -704,7 +769,7 @@ def encode(ops):
             nt = max([len(r.terms) for r in sub] + [0])
             assert nt <= MAX_TERMS, (op.name, nt)
             ntp = (nt + 3) & ~3   # records are 16-byte aligned: header + terms padded to 4 words
-            sub_tab.append((len(words), nt))
+            sub_tab.append((len(words), nt | norm_schedule(sub) << 8))
             for k in range(LANES):
                 r = sub[k] if k < len(sub) else None
                 if r is None:

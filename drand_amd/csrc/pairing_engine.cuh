@@ -214,6 +214,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
 }
 
 // ---------------------------------------------------------------- k_eng_miller
+// (4 waves/SIMD measured slower, r02m: the 128-VGPR cap spills)
 __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller(size_t cnt, const uint32_t* __restrict__ consts,
                                                           uint32_t* __restrict__ lines,
                                                           uint32_t* __restrict__ fbuf, uint32_t* __restrict__ n1) {

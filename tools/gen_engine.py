@@ -759,6 +759,12 @@ def norm_schedule(sub):
     return mask
 
 
+def slot_ref(s):
+    """An operand in a term or post word: its word offset (bits 0..9) from the
+    group's slots, or (bit 10 set) from the block constant region."""
+    return (s * SLOT_WORDS) if s < 64 else (((s - 64) * SLOT_WORDS) | 0x400)
+
+
 def encode(ops):
     words = []
     op_tab = []
@@ -769,7 +775,8 @@ def encode(ops):
             nt = max([len(r.terms) for r in sub] + [0])
             assert nt <= MAX_TERMS, (op.name, nt)
             ntp = (nt + 3) & ~3   # records are 16-byte aligned: header + terms padded to 4 words
-            sub_tab.append((len(words), nt | norm_schedule(sub) << 8))
+            uses_c = any(x >= 64 for r in sub for t in r.terms for x in t[:2]) or any(x >= 64 for r in sub for x, _ in r.post)
+            sub_tab.append((len(words), nt | norm_schedule(sub) << 8 | uses_c << 20))
             for k in range(LANES):
                 r = sub[k] if k < len(sub) else None
                 if r is None:
@@ -779,7 +786,7 @@ def encode(ops):
                 dst = 0xFF if r.dst is None else r.dst
                 exp = 0xFF if r.exp is None else r.exp
                 h0 = dst | (exp << 8) | ((r.cm & 0xFF) << 16) | (len(r.post) << 24)
-                posts = [((s & 0xFF) | ((d & 0xFFFF) << 16)) for s, d in r.post] + [0] * (3 - len(r.post))
+                posts = [(slot_ref(s) | ((d & 0xFFFF) << 16)) for s, d in r.post] + [0] * (3 - len(r.post))
                 words += [h0] + posts
                 # plain products first: for the leading term positions no lane
                 # of a sub-op negates or doubles its operand (engine.cuh skips
@@ -789,7 +796,7 @@ def encode(ops):
                     if t < len(terms):
                         a, b, sg, cf = terms[t]
                         assert cf in (1, 2) and sg in (1, -1)
-                        words.append((a & 0xFF) | ((b & 0xFF) << 8) | ((sg < 0) << 16) | ((cf == 2) << 17) | (1 << 31))
+                        words.append(slot_ref(a) | (slot_ref(b) << 11) | ((sg < 0) << 22) | ((cf == 2) << 23) | (1 << 31))
                     else:
                         words.append(0)
                 words += [0] * (ntp - nt)

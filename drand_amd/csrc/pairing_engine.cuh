@@ -98,12 +98,19 @@ struct eng_io {
 // FIXED: LDLINE reads the per-key line table and scales it by the lane's P
 // coordinate (the on-G1 lines, computed in place of k_eng_lines_fixed).
 // CYC: E_CYC runs straight-line (engine.cuh eng_cyc_fast), the FE kernel only.
+// FAM: the kernel's family of compiled ops (engine_compiled.h eng_run_c<FAM>:
+// 0 lines, 1 Miller, 2 FE), -1 none.
 #ifndef DG_ENG_NO_CYC_FAST
 constexpr bool ENG_CYC_FAST = true;
 #else
 constexpr bool ENG_CYC_FAST = false;
 #endif
-template <bool FIXED = false, bool CYC = false>
+#ifndef DG_ENG_NO_COMPILED
+constexpr bool ENG_COMPILED = true;
+#else
+constexpr bool ENG_COMPILED = false;
+#endif
+template <bool FIXED = false, bool CYC = false, int FAM = -1>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
@@ -124,7 +131,11 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
         cyc_lin_ready = true;
         continue;
       }
-      eng_run((int)a, g, c, L.k, sink);
+      bool done = false;
+      if constexpr (ENG_COMPILED && FAM == 0) done = eng_run_c0((int)a, g, c, L.k, sink);
+      if constexpr (ENG_COMPILED && FAM == 1) done = eng_run_c1((int)a, g, c, L.k, sink);
+      if constexpr (ENG_COMPILED && FAM == 2) done = eng_run_c2((int)a, g, c, L.k, sink);
+      if (!done) eng_run((int)a, g, c, L.k, sink);
     } else if (opc == ENG_OPC_STEP) {
       ++step;
     } else if (opc == ENG_OPC_LDLINE) {
@@ -202,7 +213,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
     eng_st(g + (ENG_L_NXP0 + L.k) * ENG_SLOT_WORDS, v);
   }
   asm volatile("" ::: "memory");
-  eng_exec(ENG_PROG_LINES, ENG_PROG_LINES_LEN, g, c, L, eng_io{lines, nullptr, nullptr, cnt});
+  eng_exec<false, false, 0>(ENG_PROG_LINES, ENG_PROG_LINES_LEN, g, c, L, eng_io{lines, nullptr, nullptr, cnt});
   if (status) {
     // lanes 0..3 test D1, D2 == 0, lanes 4, 5 test Z (re, im) == 0
     const int sl = L.k < 2 ? ENG_L_SUB_D1 + L.k : L.k < 4 ? ENG_L_SUB_D2 + L.k - 2 : ENG_L_SUB_Z + (L.k & 1);
@@ -225,7 +236,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller(size_t cnt, const u
   uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS;
   eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
   asm volatile("" ::: "memory");
-  eng_exec(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
+  eng_exec<false, false, 1>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
   if (L.valid) st_blk(fbuf, eng_blk_off(2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 
@@ -273,7 +284,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, 
   eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(2, 0, L.g, L.k)));
   if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
   asm volatile("" ::: "memory");
-  eng_exec<false, ENG_CYC_FAST>(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});
+  eng_exec<false, ENG_CYC_FAST, 2>(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});
   const fp v = eng_ld(g + (ENG_E_R + L.k) * ENG_SLOT_WORDS);
   const bool ok = eng_eq_canon(v, L.k == 0 ? fp_one() : fp_zero());
   const uint64_t m = __ballot(ok);
@@ -341,7 +352,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller_fixed(size_t n, siz
   }
   eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
   asm volatile("" ::: "memory");
-  eng_exec<true>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, io);
+  eng_exec<true, false, 1>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, io);
   if (L.valid) st_blk(fbuf, eng_blk_off(2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 

@@ -256,6 +256,7 @@ struct HostGroup {
 };
 
 bool g_cyc_fast = false;
+bool g_compiled = false;   // compiled ops (engine_compiled.h) instead of the interpreter
 
 // eng_cyc_fast for the 12 lanes (read all, then write all); `lin`: run the
 // LIN sub-op (else the previous E_CYC's fused epilogue wrote its outputs)
@@ -284,7 +285,10 @@ void host_run_op(HostGroup& G, int op) {
   for (uint32_t sb = s0; sb < s0 + ns; ++sb) {
     const uint32_t off = ENG_SUB_TAB[sb][0], ntw = ENG_SUB_TAB[sb][1], nt = ntw & 0xFFu;
     fp outs[ENG_LANES];
-    for (int k = 0; k < ENG_LANES; ++k) outs[k] = eng_compute(G.s, G.c, ENG_WORDS + off + k * eng_rec_words(nt), ntw);
+    for (int k = 0; k < ENG_LANES; ++k) {
+      const uint32_t* rec = ENG_WORDS + off + k * eng_rec_words(nt);
+      if (!(g_compiled && eng_sub_c_host(op, (int)(sb - s0), G.s, G.c, rec, outs[k]))) outs[k] = eng_compute(G.s, G.c, rec, ntw);
+    }
     for (int k = 0; k < ENG_LANES; ++k) {
       const uint32_t* rec = ENG_WORDS + off + k * eng_rec_words(nt);
       if (eng_dst(rec) != 0xFF) G.set(eng_dst(rec), outs[k]);
@@ -344,6 +348,39 @@ bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 // the point is pair 1's Q (pair 0 a dummy copy).  Returns 1 in G2, 0 not,
 // -1 undecodable.
 extern "C" void hs_eng_set_cyc_fast(int on) { g_cyc_fast = on != 0; }
+extern "C" void hs_eng_set_compiled(int on) { g_compiled = on != 0; }
+
+// every compiled op vs the interpreter on the same random slots: 0 iff all
+// outputs (slots and exports) are identical words
+extern "C" int hs_eng_compiled_compare(uint64_t seed) {
+  static const int ops[] = {OP_LDBL, OP_LADD, OP_M_XIF, OP_M_SQR, OP_M_XIL, OP_E_MUL, OP_E_MULCJ, OP_E_XIA};
+  int n = 0;
+  for (int op : ops) {
+    HostGroup A;
+    uint64_t x = seed * 0x9E3779B97F4A7C15ull + (uint64_t)op + 1;
+    for (int i = 0; i < 64 * ENG_SLOT_WORDS; ++i) {
+      x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      const int limb = i % ENG_SLOT_WORDS;
+      A.s[i] = limb == FP_LIMBS - 1 ? (uint32_t)(x % FP_P[FP_LIMBS - 1]) : (uint32_t)(x & FP_MASK);
+    }
+    for (int i = 0; i < ENG_NCONST * ENG_SLOT_WORDS; ++i) {
+      x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      const int limb = i % ENG_SLOT_WORDS;
+      A.c[i] = limb == FP_LIMBS - 1 ? (uint32_t)(x % FP_P[FP_LIMBS - 1]) : (uint32_t)(x & FP_MASK);
+    }
+    HostGroup B = A;
+    g_compiled = false;
+    host_run_op(A, op);
+    g_compiled = true;
+    host_run_op(B, op);
+    g_compiled = false;
+    if (memcmp(A.s, B.s, sizeof A.s) != 0) return 100 + op;
+    for (size_t i = 0; i < A.lines.size(); ++i)
+      if (memcmp(&A.lines[i], &B.lines[i], sizeof(fp)) != 0) return 200 + op;
+    ++n;
+  }
+  return n == 8 ? 0 : -1;
+}
 
 // canonical residue of a normalized value < 2^392
 static fp host_canon(fp a) {

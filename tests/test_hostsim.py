@@ -192,6 +192,26 @@ def test_engine_fast_cyc_matches_interpreter(hostsim):
     assert outs[0] == outs[1]
 
 
+def test_engine_compiled_ops_match_interpreter(hostsim):
+    """The compiled (straight-line) hot ops (engine_compiled.h) give the same
+    output words as the interpreter on random slots, and the full pairing
+    check through all three programs gives the same GT value with them."""
+    for seed in (1, 7, 99):
+        assert hostsim.hs_eng_compiled_compare(ctypes.c_uint64(seed)) == 0
+    sk = D.derive_secret(13)
+    pk48 = B.g1_compress(B.g1_mul(B.G1_GEN, sk))
+    msg = b"\x0a" * 32
+    sig = B.g2_compress(B.g2_mul(B.hash_to_g2(msg), sk))
+    outs = []
+    for on in (0, 1):
+        hostsim.hs_eng_set_compiled(on)
+        out = buf(576)
+        assert hostsim.hs_eng_pairing(pk48, msg, sig, out) == 1
+        outs.append(out.raw)
+    hostsim.hs_eng_set_compiled(0)
+    assert outs[0] == outs[1]
+
+
 def test_hash_to_g1_golden(hostsim):
     """Kernel hash-to-G1 (inversion-free SSWU + 11-isogeny, both DSTs) vs the
     oracle's fixture, including drand digests under the legacy and RFC DSTs."""

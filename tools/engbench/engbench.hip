@@ -66,6 +66,13 @@ __global__ void __launch_bounds__(64, 3) k_bench(int op, int reps, const uint32_
       eng_cyc_fast<false>(g, k);
       continue;
     }
+    if (op >= 1000) {  // compiled form (engine_compiled.h)
+      auto snk = [&](uint32_t e, const fp& v) { sink_acc += v.l[0] ^ e; };
+      if (!(eng_run_c0(op - 1000, g, c, k, snk) || eng_run_c1(op - 1000, g, c, k, snk) ||
+            eng_run_c2(op - 1000, g, c, k, snk)))
+        sink_acc += 1;
+      continue;
+    }
 #ifdef ENGBENCH_LDS_RECORDS
     eng_run(op, g, c, k, [&](uint32_t e, const fp& v) { sink_acc += v.l[0] ^ e; } ENGBENCH_RUN_ARGS);
 #else
@@ -116,6 +123,8 @@ int main(int argc, char** argv) {
       {"M_XIL", OP_M_XIL, 1},     {"M_LM1", OP_M_LM1, 1},     {"E_CYC", OP_E_CYC, 2},     {"E_MUL", OP_E_MUL, 2},
       {"E_MULCJ", OP_E_MULCJ, 2}, {"E_XIA", OP_E_XIA, 2},     {"E_FROB1", OP_E_FROB1, 2},
       {"E_CYC_lin", OP_E_CYC, 2, 0, 1}, {"E_CYC_prod", OP_E_CYC, 2, 1, 1}, {"E_CYC_fast", -1, 2}, {"E_CYC_chain", -2, 2},
+      {"LDBL_c", 1000 + OP_LDBL, 0}, {"LADD_c", 1000 + OP_LADD, 0}, {"M_SQR_c", 1000 + OP_M_SQR, 1},
+      {"M_XIF_c", 1000 + OP_M_XIF, 1}, {"E_MUL_c", 1000 + OP_E_MUL, 2}, {"E_XIA_c", 1000 + OP_E_XIA, 2},
   };
   constexpr int WMAX = (ENG_NCONST + ENG_GROUPS_PER_WAVE * 64) * ENG_SLOT_WORDS;
   std::vector<uint32_t> h((size_t)64 * WMAX);

@@ -873,6 +873,97 @@ def cyc_fast_params(ops, name="E_CYC"):
     return rows
 
 
+# ---------------------------------------------------------------- compiled ops (engine_compiled.h)
+# Hot ops run as straight-line code (engine.cuh eng_sub_c): the generator
+# fixes each sub-op's shape at compile time.  Families: the kernel whose
+# eng_exec includes the op (0 lines, 1 miller, 2 fe).
+# (M_LM1 / M_LM2 stay interpreted: compiled, they push k_eng_miller to 142 spilled VGPRs)
+COMPILED = {"LDBL": 0, "LADD": 0, "M_XIF": 1, "M_SQR": 1, "M_XIL": 1,
+            "E_MUL": 2, "E_MULCJ": 2, "E_XIA": 2}
+
+
+def sub_shape(sub):
+    lanes = [sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2)) for r in sub] + [[]] * (LANES - len(sub))
+    nt = max(len(t) for t in lanes)
+    ntmin = min(len(t) for t in lanes)
+    xf = 0
+    for t in range(nt):
+        if any(t < len(ts) and (ts[t][2] < 0 or ts[t][3] == 2) for ts in lanes):
+            xf |= 1 << t
+    np_ = max(len(r.post) for r in sub)
+    plain = all(r.cm == 1 and not r.post for r in sub) and len(sub) == LANES
+    kind = "ENG_K_PLAIN" if plain else ("ENG_K_LIN" if nt == 0 else "ENG_K_MIXED")
+    lin32 = all(abs(r.cm) * (1 << (29 if r.cm < 0 else 28)) + sum(abs(d) * (1 << (29 if d < 0 else 28)) for _, d in r.post)
+                <= (1 << 31) for r in sub)
+    consts = any(x >= 64 for r in sub for t in r.terms for x in t[:2]) or any(x >= 64 for r in sub for x, _ in r.post)
+    has_dst = any(r.dst is not None for r in sub)
+    has_exp = any(r.exp is not None for r in sub)
+    return nt, ntmin, xf, np_, kind, lin32, consts, has_dst, has_exp
+
+
+def emit_compiled(ops, sub_tab, path):
+    idx = {op.name: i for i, op in enumerate(ops)}
+    out = ["// GENERATED by tools/gen_engine.py -- do not edit.",
+           "// Straight-line forms of the hot engine ops (engine.cuh eng_sub_c): each",
+           "// sub-op's shape fixed at compile time, the records and sums the interpreter's.",
+           "// Included by engine.cuh inside namespace dgpu.",
+           "#pragma once", ""]
+    s_index = 0
+    first_sub = {}
+    for op in ops:
+        first_sub[op.name] = s_index
+        s_index += len(op.subs)
+    for name, fam in COMPILED.items():
+        op = ops[idx[name]]
+        out.append("template <class Sink>")
+        out.append(f"__device__ __forceinline__ void eng_op_c_{name}(uint32_t* g, const uint32_t* c, int k, Sink&& sink) {{")
+        for si, sub in enumerate(op.subs):
+            nt, ntmin, xf, np_, kind, lin32, consts, has_dst, has_exp = sub_shape(sub)
+            off, ntw = sub_tab[first_sub[name] + si]
+            recw = 4 + ((nt + 3) & ~3)
+            out.append("  {")
+            out.append(f"    const uint32_t* rec = ENG_WORDS + {off}u + (uint32_t)k * {recw}u;")
+            out.append(f"    const fp o = eng_sub_c<{nt}, {ntmin}, 0x{xf:x}u, {np_}, {kind}, {str(lin32).lower()}, "
+                       f"{str(consts).lower()}>(g, c, rec);")
+            out.append("    const uint32_t h0 = rec[0];")
+            out.append("    asm volatile(\"\" ::: \"memory\");")
+            if has_dst:
+                out.append("    if ((h0 & 0xFFu) != 0xFFu) eng_st(g + (h0 & 0xFFu) * ENG_SLOT_WORDS, o);")
+            if has_exp:
+                out.append("    if (((h0 >> 8) & 0xFFu) != 0xFFu) sink((h0 >> 8) & 0xFFu, o);")
+            out.append("    asm volatile(\"\" ::: \"memory\");")
+            out.append("  }")
+        out.append("}")
+        out.append("")
+    for fam in range(3):
+        out.append("template <class Sink>")
+        out.append(f"__device__ __forceinline__ bool eng_run_c{fam}(int op, uint32_t* g, const uint32_t* c, int k, Sink&& sink) {{")
+        out.append("  switch (op) {")
+        for name, f in COMPILED.items():
+            if f == fam:
+                out.append(f"    case OP_{name}: eng_op_c_{name}(g, c, k, sink); return true;")
+        out.append("    default: return false;")
+        out.append("  }")
+        out.append("}")
+        out.append("")
+    # host emulation: one sub-op for one lane
+    out.append("// host emulation (tests/hostsim): sub-op si of compiled op `op` for the lane")
+    out.append("// whose record is `rec`; false if the op is not compiled")
+    out.append("DG_FN bool eng_sub_c_host(int op, int si, const uint32_t* g, const uint32_t* c, const uint32_t* rec, fp& o) {")
+    out.append("  switch (op * 16 + si) {")
+    for name in COMPILED:
+        op = ops[idx[name]]
+        for si, sub in enumerate(op.subs):
+            nt, ntmin, xf, np_, kind, lin32, consts, _, _ = sub_shape(sub)
+            out.append(f"    case OP_{name} * 16 + {si}: o = eng_sub_c<{nt}, {ntmin}, 0x{xf:x}u, {np_}, {kind}, "
+                       f"{str(lin32).lower()}, {str(consts).lower()}>(g, c, rec); return true;")
+    out.append("    default: return false;")
+    out.append("  }")
+    out.append("}")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+
+
 def check_bounds(ops):
     """Static bounds the device arithmetic relies on (see engine.cuh):
     slot values < 2.01p; product sum < 2048 p^2 so redc < 1.8p; the post
@@ -971,6 +1062,7 @@ def emit(path):
     lines.append("}  // namespace dgpu")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
+    emit_compiled(ops, sub_tab, os.path.join(os.path.dirname(path), "engine_compiled.h"))
     return ops, nsl
 
 

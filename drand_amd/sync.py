@@ -131,11 +131,20 @@ def check_past_beacons(store, verifier, pubkey, up_to, cb=None, window=1 << 16, 
         # fetch one window of rows, then verify every present beacon in one batch
         hi = min(n, i + window)
         rows = []
-        for r in range(i, hi):
-            try:
-                rows.append(store.get(r))
-            except (ErrNoBeaconSaved, ValueError):  # no row, or Unmarshal error: the round is faulty
-                rows.append(None)
+        if hasattr(store, "scan"):  # one ordered pass over the window's rows (drand_amd/boltstore.py)
+            got = dict(store.scan(i, hi))
+            for r in range(i, hi):
+                v = got.get(r)
+                try:
+                    rows.append(None if v is None else beacon_unmarshal(v))
+                except ValueError:  # Unmarshal error: the round is faulty
+                    rows.append(None)
+        else:
+            for r in range(i, hi):
+                try:
+                    rows.append(store.get(r))
+                except (ErrNoBeaconSaved, ValueError):  # no row, or Unmarshal error: the round is faulty
+                    rows.append(None)
         present = [b for b in rows if b is not None]
         reasons = verifier.verify_reasons(present, pubkey, mode) if present else []
         ok = iter(r == 0 for r in reasons)

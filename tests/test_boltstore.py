@@ -1,0 +1,142 @@
+"""Read-only bolt beacon store (drand_amd/boltstore.py) for check-chain ingest:
+the read side of chain/boltdb/store.go (Len / Last / Get) over bbolt files,
+and CheckPastBeacons fed from it.  The files come from tests/bolt_writer.py
+(Go and bbolt are absent, so parity with bbolt-written files is unpinned);
+the semantics are checked against the in-memory store and the oracle's
+restatement of the loop."""
+import random
+import struct
+
+import pytest
+
+from bolt_writer import write_bolt
+from drand_amd.boltstore import BoltFormatError, BoltStore, fnv1a64
+from drand_amd.chain import Beacon
+from drand_amd.sync import ErrNoBeaconSaved, MemoryStore, beacon_marshal, check_past_beacons
+from oracle import drand_ref as D
+from test_sync import MarkerVerifier
+
+
+def _kv(st: MemoryStore):
+    return dict(st._kv)
+
+
+def _random_store(rng, n, big=None):
+    st = MemoryStore()
+    table = {0: (0, b"", b"genesis")}
+    st.put(Beacon(b"", 0, b"genesis"))
+    for r in range(1, n + 1):
+        if rng.random() < 0.04:
+            continue  # missing row
+        if rng.random() < 0.01:
+            st.put_raw(r, b"not json")  # unmarshal error: faulty, like the reference's Get
+            table[r] = None
+            continue
+        rr = r if rng.random() > 0.02 else r + 7  # stored beacon with a different Round field
+        sig = (b"BAD" if rng.random() < 0.1 else b"ok") + r.to_bytes(4, "big")
+        prev = bytes(rng.randrange(256) for _ in range(big if big and r % 97 == 0 else 96))
+        st.put_raw(r, beacon_marshal(Beacon(prev, rr, sig)))
+        table[r] = (rr, prev, sig)
+    return st, table
+
+
+def test_reference_store_test_semantics(tmp_path):
+    """chain/boltdb/store_test.go TestStoreBolt / TestStoreBoltOrder: Len counts
+    keys, Last is the highest round whatever the insertion order, Get returns
+    the stored beacon, a missing round is ErrNoBeaconSaved."""
+    b1 = Beacon(bytes([1, 2, 3]), 145, bytes([2, 3, 4]))
+    b2 = Beacon(bytes([2, 3, 4]), 146, bytes([1, 2, 3]))
+    for order in ((b2, b1), (b1, b2)):
+        st = MemoryStore()
+        for b in order:
+            st.put(b)
+        p = tmp_path / "drand.db"
+        write_bolt(p, _kv(st))
+        bs = BoltStore(p)
+        assert bs.len() == 2 and bs.last() == b2
+        assert bs.get(145) == b1 and bs.get(146) == b2
+        with pytest.raises(ErrNoBeaconSaved):
+            bs.get(147)
+        bs.close()
+
+
+@pytest.mark.parametrize("n,inline,big", [(3, True, None), (40, False, None), (3000, False, None), (600, False, 9000)])
+def test_bolt_store_equals_memory_store(tmp_path, n, inline, big):
+    """Inline bucket, one leaf, a three-level tree, and leaves with overflow
+    pages (a 9,000-byte PreviousSig): Len / Last / Get / scan agree with the
+    in-memory store row for row."""
+    st, _ = _random_store(random.Random(n), n, big)
+    p = tmp_path / "drand.db"
+    write_bolt(p, _kv(st), inline=inline)
+    bs = BoltStore(p)
+    assert bs.len() == st.len()
+    assert bs.last() == st.last()
+    for r in range(0, n + 3):
+        try:
+            want = st.get(r)
+        except (ErrNoBeaconSaved, ValueError) as e:
+            want = type(e)
+        try:
+            got = bs.get(r)
+        except (ErrNoBeaconSaved, ValueError) as e:
+            got = type(e)
+        assert got == want, r
+    lo, hi = n // 3, 2 * n // 3 + 1
+    assert list(bs.scan(lo, hi)) == [(r, v) for r, v in sorted(
+        (struct.unpack(">Q", k)[0], v) for k, v in _kv(st).items()) if lo <= r < hi]
+    bs.close()
+
+
+@pytest.mark.parametrize("window", [1, 5, 64, 1 << 16])
+def test_check_past_beacons_from_bolt(tmp_path, window):
+    """CheckPastBeacons over the bolt file (windowed ordered scans) gives the
+    same faulty list and progress callbacks as over the in-memory store and
+    as the oracle's restatement of chain/beacon/sync_manager.go:171-232."""
+    rng = random.Random(window)
+    st, table = _random_store(rng, 700)
+    p = tmp_path / "drand.db"
+    write_bolt(p, _kv(st))
+    bs = BoltStore(p)
+    for up_to in (1, 350, 10 ** 9):
+        c1, c2 = [], []
+        got = check_past_beacons(bs, MarkerVerifier(), b"pk", up_to, cb=lambda i, u: c1.append((i, u)), window=window)
+        mem = check_past_beacons(st, MarkerVerifier(), b"pk", up_to, cb=lambda i, u: c2.append((i, u)), window=window)
+        tab = {r: v for r, v in table.items() if v is not None}
+        for r in (r for r, v in table.items() if v is None):
+            tab[r] = (r, b"", b"BAD-unmarshal")  # the oracle's table has no raw rows: faulty either way
+        exp, progress = D.check_past_beacons(tab, up_to, lambda b: not b[2].startswith(b"BAD"))
+        assert got == mem == exp
+        assert c1 == c2 == progress
+    bs.close()
+
+
+def test_meta_selection_and_errors(tmp_path):
+    """The valid meta page with the larger txid is current; a bad checksum on
+    it falls back to the other; no valid meta, a missing bucket or an empty
+    bucket are reported like bbolt / the store do."""
+    st, _ = _random_store(random.Random(1), 50)
+    p = tmp_path / "drand.db"
+    write_bolt(p, _kv(st))
+    raw = bytearray(p.read_bytes())
+    assert BoltStore(p).txid == 1
+    raw[4096 + 16 + 40] ^= 1  # page 1's txid: checksum no longer matches
+    p.write_bytes(bytes(raw))
+    bs = BoltStore(p)
+    assert bs.txid == 0 and bs.last() == st.last()
+    bs.close()
+    raw[16 + 40] ^= 1
+    p.write_bytes(bytes(raw))
+    with pytest.raises(BoltFormatError):
+        BoltStore(p)
+    q = tmp_path / "other.db"
+    write_bolt(q, _kv(st), bucket=b"other")
+    with pytest.raises(BoltFormatError):
+        BoltStore(q)
+    e = tmp_path / "empty.db"
+    write_bolt(e, {})
+    be = BoltStore(e)
+    assert be.len() == 0
+    with pytest.raises(ErrNoBeaconSaved):
+        be.last()
+    be.close()
+    assert fnv1a64(b"") == 0xCBF29CE484222325 and fnv1a64(b"a") == 0xAF63DC4C8601EC8C  # FNV-1a-64 test vectors

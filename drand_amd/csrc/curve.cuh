@@ -34,19 +34,25 @@ DG_FN g2j g2_cmov(const g2j& a, const g2j& b, bool take_b) {
 // dbl-2009-l (a = 0): 2M + 5S.  Infinity stays infinity (Z3 = 2YZ).
 // (*_body: the same code force-inlined, for loops that keep the point in
 // registers instead of passing it through the stack to an out-of-line call)
+// Lazy linear steps (bounds in units of p; CI = normalized, < 2.01p):
+//   X + B carried (< 4.02p) into fp2_sqr; D/2 = (X+B)^2 - A - C reduced;
+//   E = 3A carried (< 6.03p); X3 = F - 4(D/2) (4(D/2) carried, < 8.04p);
+//   D - X3 = 2(D/2) + 8p - X3 carried (< 12.02p) into fp2_mul with E
+//   (sum products 12.06p x 24.04p); 8C carried (< 16.08p);
+//   Z3 = (2Y) Z with 2Y lazy (limbs < 2^29, fp2_mul's sum < 2^30).
 DG_FN g2j g2_dbl_body(const g2j& p) {
-  fp2 A = fp2_sqr(p.x);
-  fp2 B = fp2_sqr(p.y);
-  fp2 C = fp2_sqr(B);
-  fp2 D = fp2_sub(fp2_sqr(fp2_add(p.x, B)), fp2_add(A, C));
-  D = fp2_dbl(D);
-  fp2 E = fp2_add(fp2_dbl(A), A);
-  fp2 F = fp2_sqr(E);
+  const fp2 A = fp2_sqr(p.x);
+  const fp2 B = fp2_sqr(p.y);
+  const fp2 C = fp2_sqr(B);
+  const fp2 Dh = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(p.x, B))), fp2_add_lz(A, C));
+  const fp2 E = fp2_carry(fp2_add_lz(fp2_add_lz(A, A), A));
+  const fp2 F = fp2_sqr(E);
   g2j r;
-  r.x = fp2_sub(F, fp2_dbl(D));
-  fp2 C8 = fp2_dbl(fp2_dbl(fp2_dbl(C)));
-  r.y = fp2_sub(fp2_mul(E, fp2_sub(D, r.x)), C8);
-  r.z = fp2_dbl(fp2_mul(p.y, p.z));
+  r.x = fp2_sub32(F, fp2_carry(fp2_mulk_lz(Dh, 4)));
+  const fp2 D2 = fp2_add_lz(Dh, Dh);
+  const fp2 DX = fp2_carry(fp2{fp_sub_lz(D2.c0, r.x.c0), fp_sub_lz(D2.c1, r.x.c1)});
+  r.y = fp2_sub32(fp2_mul(E, DX), fp2_carry(fp2_mulk_lz(C, 8)));
+  r.z = fp2_mul(fp2_add_lz(p.y, p.y), p.z);
   return r;
 }
 
@@ -54,24 +60,30 @@ DG_NOINL g2j g2_dbl(const g2j& p) { return g2_dbl_body(p); }
 
 // add-2007-bl with the exceptional cases resolved (P == Q -> dbl,
 // P == -Q -> infinity, either operand infinity -> the other).
+// Lazy linear steps: rr = 2(s2 - s1) and 2h carried (< 4.02p); X3 = rr^2 -
+// (J + 2V), the sum carried (< 6.03p); V - X3 = V + 8p - X3 carried (< 10.02p)
+// into fp2_mul with rr (sum products 8.04p x 20.04p); 2 s1 J = (2 s1) J with
+// 2 s1 lazy; Z1 + Z2 carried into fp2_sqr, minus the lazy z1z1 + z2z2.
 DG_FN g2j g2_add_body(const g2j& p, const g2j& q) {
-  fp2 z1z1 = fp2_sqr(p.z);
-  fp2 z2z2 = fp2_sqr(q.z);
-  fp2 u1 = fp2_mul(p.x, z2z2);
-  fp2 u2 = fp2_mul(q.x, z1z1);
-  fp2 s1 = fp2_mul(fp2_mul(p.y, q.z), z2z2);
-  fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
-  fp2 h = fp2_sub(u2, u1);
-  fp2 rr = fp2_dbl(fp2_sub(s2, s1));
-  bool p_inf = g2_is_inf(p), q_inf = g2_is_inf(q);
-  bool h0 = fp2_is_zero(h), r0 = fp2_is_zero(rr);
-  fp2 i = fp2_sqr(fp2_dbl(h));
-  fp2 j = fp2_mul(h, i);
-  fp2 v = fp2_mul(u1, i);
+  const fp2 z1z1 = fp2_sqr(p.z);
+  const fp2 z2z2 = fp2_sqr(q.z);
+  const fp2 u1 = fp2_mul(p.x, z2z2);
+  const fp2 u2 = fp2_mul(q.x, z1z1);
+  const fp2 s1 = fp2_mul(fp2_mul(p.y, q.z), z2z2);
+  const fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
+  const fp2 h = fp2_sub(u2, u1);
+  const fp2 rh = fp2_sub(s2, s1);
+  const bool p_inf = g2_is_inf(p), q_inf = g2_is_inf(q);
+  const bool h0 = fp2_is_zero(h), r0 = fp2_is_zero(rh);
+  const fp2 rr = fp2_carry(fp2_add_lz(rh, rh));
+  const fp2 i = fp2_sqr(fp2_carry(fp2_add_lz(h, h)));
+  const fp2 j = fp2_mul(h, i);
+  const fp2 v = fp2_mul(u1, i);
   g2j r;
-  r.x = fp2_sub(fp2_sub(fp2_sqr(rr), j), fp2_dbl(v));
-  r.y = fp2_sub(fp2_mul(rr, fp2_sub(v, r.x)), fp2_dbl(fp2_mul(s1, j)));
-  r.z = fp2_mul(fp2_sub(fp2_sqr(fp2_add(p.z, q.z)), fp2_add(z1z1, z2z2)), h);
+  r.x = fp2_sub32(fp2_sqr(rr), fp2_carry(fp2_add_lz(fp2_add_lz(j, v), v)));
+  const fp2 VX = fp2_carry(fp2{fp_sub_lz(v.c0, r.x.c0), fp_sub_lz(v.c1, r.x.c1)});
+  r.y = fp2_sub(fp2_mul(rr, VX), fp2_mul(fp2_add_lz(s1, s1), j));
+  r.z = fp2_mul(fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(p.z, q.z))), fp2_add_lz(z1z1, z2z2)), h);
   if (h0 && !p_inf && !q_inf) r = r0 ? g2_dbl(p) : g2_infinity();
   if (p_inf) r = q;
   if (q_inf) r = p;
@@ -83,21 +95,24 @@ DG_NOINL g2j g2_add(const g2j& p, const g2j& q) { return g2_add_body(p, q); }
 // Mixed addition p + q with q affine (madd-2007-bl: 7M + 4S), exceptional
 // cases resolved (p == q -> dbl, p == -q -> infinity, p infinity -> q).
 DG_FN g2j g2_add_affine_body(const g2j& p, const g2a& q) {
-  fp2 z1z1 = fp2_sqr(p.z);
-  fp2 u2 = fp2_mul(q.x, z1z1);
-  fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
-  fp2 h = fp2_sub(u2, p.x);
-  fp2 rr = fp2_dbl(fp2_sub(s2, p.y));
-  bool p_inf = g2_is_inf(p);
-  bool h0 = fp2_is_zero(h), r0 = fp2_is_zero(rr);
-  fp2 hh = fp2_sqr(h);
-  fp2 i = fp2_dbl(fp2_dbl(hh));
-  fp2 j = fp2_mul(h, i);
-  fp2 v = fp2_mul(p.x, i);
+  // lazy linear steps as g2_add_body; I = 4 HH carried (< 8.04p)
+  const fp2 z1z1 = fp2_sqr(p.z);
+  const fp2 u2 = fp2_mul(q.x, z1z1);
+  const fp2 s2 = fp2_mul(fp2_mul(q.y, p.z), z1z1);
+  const fp2 h = fp2_sub(u2, p.x);
+  const fp2 rh = fp2_sub(s2, p.y);
+  const bool p_inf = g2_is_inf(p);
+  const bool h0 = fp2_is_zero(h), r0 = fp2_is_zero(rh);
+  const fp2 rr = fp2_carry(fp2_add_lz(rh, rh));
+  const fp2 hh = fp2_sqr(h);
+  const fp2 i = fp2_carry(fp2_mulk_lz(hh, 4));
+  const fp2 j = fp2_mul(h, i);
+  const fp2 v = fp2_mul(p.x, i);
   g2j r;
-  r.x = fp2_sub(fp2_sub(fp2_sqr(rr), j), fp2_dbl(v));
-  r.y = fp2_sub(fp2_mul(rr, fp2_sub(v, r.x)), fp2_dbl(fp2_mul(p.y, j)));
-  r.z = fp2_sub(fp2_sqr(fp2_add(p.z, h)), fp2_add(z1z1, hh));
+  r.x = fp2_sub32(fp2_sqr(rr), fp2_carry(fp2_add_lz(fp2_add_lz(j, v), v)));
+  const fp2 VX = fp2_carry(fp2{fp_sub_lz(v.c0, r.x.c0), fp_sub_lz(v.c1, r.x.c1)});
+  r.y = fp2_sub(fp2_mul(rr, VX), fp2_mul(fp2_add_lz(p.y, p.y), j));
+  r.z = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(p.z, h))), fp2_add_lz(z1z1, hh));
   if (h0 && !p_inf) r = r0 ? g2_dbl(g2_from_affine(q)) : g2_infinity();
   if (p_inf) r = g2_from_affine(q);
   return r;

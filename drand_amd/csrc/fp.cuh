@@ -62,8 +62,13 @@ DG_FN fp fp_zero() {
 DG_FN fp fp_one() { return FP_ONE_MONT; }
 
 // ---------------------------------------------------------------- Montgomery
-// Separated operand scanning in product-scanning order: full 28-limb product,
-// then the Montgomery reduction, both column-wise into a 64-bit accumulator.
+// Separated operand scanning in product-scanning order: the full product as
+// 27 unnormalized 64-bit columns (one v_mad_u64_u32 per partial product, no
+// carry handling), then the Montgomery reduction over the columns into a
+// running 64-bit accumulator.  Column bound: 14 products of limbs < 2^30 are
+// < 14 * 2^60, plus the reduction's 14 m * p terms (< 2^56 each) and carry:
+// < 2^64.  (Round 1 normalized the columns first: 540 VALU instructions per
+// multiplication and 484 per squaring, against 490 and 422 in this form.)
 #define DG_LIMB_PARAMS(x)                                                                                     \
   uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, uint32_t x##6,   \
       uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11, uint32_t x##12, uint32_t x##13
@@ -76,23 +81,12 @@ DG_FN fp fp_one() { return FP_ONE_MONT; }
 // calling convention passes a second 14-dword struct byval through scratch,
 // which would put a store/load round trip (and an exposed wait) in front of
 // every multiplication.  28 scalars travel in v0..v27.
-DG_FPK fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
-  const fp a = DG_LIMB_PACK(x), b = DG_LIMB_PACK(y);
-  DG_COUNT(dg_count_mul);
-  uint32_t t[2 * FP_LIMBS];
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * FP_LIMBS - 1; ++k) {
-#pragma unroll
-    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); i <= (k < FP_LIMBS ? k : FP_LIMBS - 1); ++i)
-      acc += (uint64_t)a.l[i] * b.l[k - i];
-    t[k] = (uint32_t)acc & FP_MASK;
-    acc >>= FP_BITS;
-  }
-  t[2 * FP_LIMBS - 1] = (uint32_t)acc;
-  uint32_t m[FP_LIMBS];
+// Montgomery reduction of unnormalized product columns t[k] (< 2^64 - 2^60):
+// T / R mod p, normalized limbs, < T/R + p.
+DG_FN fp fp_redc_cols(const uint64_t* t) {
   fp r;
-  acc = 0;
+  uint32_t m[FP_LIMBS];
+  uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < FP_LIMBS; ++k) {
 #pragma unroll
@@ -117,50 +111,40 @@ DG_FPK fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
   return r;
 }
 
-// Squaring: cross products computed once and doubled (98 instead of 196
-// partial products in the first half).
+// Product columns left unnormalized (each < 14 * 2^60 for limbs < 2^30)
+// and fed straight to the reduction.
+DG_FPK fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
+  const fp a = DG_LIMB_PACK(x), b = DG_LIMB_PACK(y);
+  DG_COUNT(dg_count_mul);
+  uint64_t t[2 * FP_LIMBS];
+#pragma unroll
+  for (int k = 0; k < 2 * FP_LIMBS - 1; ++k) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); i <= (k < FP_LIMBS ? k : FP_LIMBS - 1); ++i)
+      c += (uint64_t)a.l[i] * b.l[k - i];
+    t[k] = c;
+  }
+  t[2 * FP_LIMBS - 1] = 0;
+  return fp_redc_cols(t);
+}
+
+// Squaring: cross products once, doubled per column.
 DG_FPK fp fp_sqr_r(DG_LIMB_PARAMS(x)) {
   const fp a = DG_LIMB_PACK(x);
   DG_COUNT(dg_count_sqr);
-  uint32_t t[2 * FP_LIMBS];
-  uint64_t carry = 0;
+  uint64_t t[2 * FP_LIMBS];
 #pragma unroll
   for (int k = 0; k < 2 * FP_LIMBS - 1; ++k) {
-    uint64_t x = 0;
+    uint64_t c = 0;
 #pragma unroll
-    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); 2 * i < k; ++i) x += (uint64_t)a.l[i] * a.l[k - i];
-    x <<= 1;
-    if ((k & 1) == 0) x += (uint64_t)a.l[k / 2] * a.l[k / 2];
-    x += carry;
-    t[k] = (uint32_t)x & FP_MASK;
-    carry = x >> FP_BITS;
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); 2 * i < k; ++i) c += (uint64_t)a.l[i] * a.l[k - i];
+    c <<= 1;
+    if ((k & 1) == 0) c += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    t[k] = c;
   }
-  t[2 * FP_LIMBS - 1] = (uint32_t)carry;
-  uint32_t m[FP_LIMBS];
-  fp r;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < FP_LIMBS; ++k) {
-#pragma unroll
-    for (int i = 0; i < k; ++i) acc += (uint64_t)m[i] * FP_P[k - i];
-    acc += t[k];
-    m[k] = ((uint32_t)acc * FP_PINV) & FP_MASK;
-    acc += (uint64_t)m[k] * FP_P[0];
-    acc >>= FP_BITS;
-  }
-#pragma unroll
-  for (int k = FP_LIMBS; k < 2 * FP_LIMBS; ++k) {
-#pragma unroll
-    for (int i = k - FP_LIMBS + 1; i < FP_LIMBS; ++i) acc += (uint64_t)m[i] * FP_P[k - i];
-    acc += t[k];
-    if (k < 2 * FP_LIMBS - 1) {
-      r.l[k - FP_LIMBS] = (uint32_t)acc & FP_MASK;
-      acc >>= FP_BITS;
-    } else {
-      r.l[k - FP_LIMBS] = (uint32_t)acc;
-    }
-  }
-  return r;
+  t[2 * FP_LIMBS - 1] = 0;
+  return fp_redc_cols(t);
 }
 
 // ---------------------------------------------------------------- normalization

@@ -114,7 +114,6 @@ template <bool FIXED = false, bool CYC = false, int FAM = -1>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
-  bool cyc_lin_ready = false;  // the previous op was an E_CYC: its epilogue wrote E_CYC's LIN outputs
   auto sink = [&](uint32_t e, const fp& v) {
     if (!L.valid) return;
     if (e < 12) st_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, (int)e), v);
@@ -125,10 +124,11 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     const uint32_t ins = prog[pc];
     const uint32_t opc = ins >> 24, a = ins & 0xFFu, b = (ins >> 8) & 0xFFu;
     if (opc == ENG_OPC_RUN) {
-      if (CYC && a == OP_E_CYC) {
-        if (cyc_lin_ready) eng_cyc_fast<false>(g, L.k);
-        else eng_cyc_fast<true>(g, L.k);
-        cyc_lin_ready = true;
+      if (CYC && a == OP_E_CYC) {  // the run of E_CYC ops starting here, as one chain
+        int n = 1;
+        while (pc + n < len && prog[pc + n] == ins) ++n;
+        eng_cyc_chain(g, L.k, n);
+        pc += n - 1;
         continue;
       }
       bool done = false;
@@ -152,7 +152,6 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
     } else if (opc == ENG_OPC_ST12) {
       if (L.valid) st_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
     }
-    cyc_lin_ready = false;
     asm volatile("" ::: "memory");
   }
 }
@@ -191,11 +190,11 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
                                                          const uint32_t* __restrict__ consts,
                                                          uint32_t* __restrict__ lines,
                                                          uint8_t* __restrict__ status) {
-  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_LINES) * ENG_SLOT_WORDS];
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_LINES * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
   const eng_lane L = eng_lane_id(cnt);
-  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_LINES) * ENG_SLOT_WORDS;
+  uint32_t* g = lds + ENG_GBASE_LINES[L.g] * ENG_SLOT_WORDS;
   const size_t r = r0 + L.i;
   if (L.k < 8) {  // Q coordinates: X, Y of T and the affine copy (xQ, yQ)
     const int p = L.k >> 2, comp = L.k & 3;
@@ -229,11 +228,11 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
 __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller(size_t cnt, const uint32_t* __restrict__ consts,
                                                           uint32_t* __restrict__ lines,
                                                           uint32_t* __restrict__ fbuf, uint32_t* __restrict__ n1) {
-  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS];
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_MILLER * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
   const eng_lane L = eng_lane_id(cnt);
-  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS;
+  uint32_t* g = lds + ENG_GBASE_MILLER[L.g] * ENG_SLOT_WORDS;
   eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
   asm volatile("" ::: "memory");
   eng_exec<false, false, 1>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
@@ -276,11 +275,11 @@ __global__ void __launch_bounds__(256) k_eng_inv(size_t cnt, size_t r0, uint32_t
 __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
                                                       uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ n1inv,
                                                       uint8_t* __restrict__ status) {
-  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_FE) * ENG_SLOT_WORDS];
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_FE * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
   const eng_lane L = eng_lane_id(cnt);
-  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_FE) * ENG_SLOT_WORDS;
+  uint32_t* g = lds + ENG_GBASE_FE[L.g] * ENG_SLOT_WORDS;
   eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(2, 0, L.g, L.k)));
   if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
   asm volatile("" ::: "memory");
@@ -336,11 +335,11 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller_fixed(size_t n, siz
                                                                 const uint32_t* __restrict__ table,
                                                                 uint32_t* __restrict__ fbuf,
                                                                 uint32_t* __restrict__ n1) {
-  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS];
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_MILLER * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
   const eng_lane L = eng_lane_id(cnt);
-  uint32_t* g = lds + (ENG_NCONST + L.g * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS;
+  uint32_t* g = lds + ENG_GBASE_MILLER[L.g] * ENG_SLOT_WORDS;
   eng_io io{nullptr, fbuf, n1, cnt};
   io.table = table;
   const int pair = L.k / 6, k = L.k % 6;

@@ -54,6 +54,27 @@ DG_FN fp2 fp2_sqr(const fp2& a) {
 
 DG_FN fp2 fp2_mul_fp(const fp2& a, const fp& s) { return fp2{fp_mul(a.c0, s), fp_mul(a.c1, s)}; }
 
+// ---- lazy Fp2 steps for the group law: each caller states the bounds it
+// relies on (fp_mul / fp2_mul / fp2_sqr inputs: limbs < 2^30 after their own
+// internal lazy sums, value products < ~2600 p^2; fp2_sqr's second coefficient
+// normalized < 7.99p).  An fp2_add + fp2_dbl chain of CI ops costs a carry
+// pass and a reduction per coefficient per step; these defer both.
+DG_FN fp2 fp2_add_lz(const fp2& a, const fp2& b) { return fp2{fp_add_lz(a.c0, b.c0), fp_add_lz(a.c1, b.c1)}; }
+// carry propagation only (input limbs < 2^31): normalized, value unchanged
+DG_FN fp2 fp2_carry(const fp2& a) { return fp2{fp_norm(a.c0), fp_norm(a.c1)}; }
+// k a limb-wise (k a < 2^31 per limb), unnormalized
+DG_FN fp2 fp2_mulk_lz(const fp2& a, uint32_t k) {
+  fp2 r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.c0.l[i] = k * a.c0.l[i], r.c1.l[i] = k * a.c1.l[i];
+  return r;
+}
+// a - b reduced (CI): a CI, b normalized with value < 31.9p or an unnormalized
+// sum of two normalized values (fp_sub2_lz's precondition)
+DG_FN fp2 fp2_sub32(const fp2& a, const fp2& b) {
+  return fp2{fp_reduce(fp_norm(fp_sub2_lz(a.c0, b.c0))), fp_reduce(fp_norm(fp_sub2_lz(a.c1, b.c1)))};
+}
+
 // multiply by xi = 1 + u: (a0 - a1) + (a0 + a1) u
 DG_FN fp2 fp2_mul_xi(const fp2& a) { return fp2{fp_sub(a.c0, a.c1), fp_add(a.c0, a.c1)}; }
 

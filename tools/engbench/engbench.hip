@@ -27,10 +27,18 @@ using namespace dgpu;
 #ifndef ENGBENCH_PAD_WORDS
 #define ENGBENCH_PAD_WORDS 0   // extra LDS per block: occupancy sweep
 #endif
-template <int NSLOTS>
+// the production kernels' LDS layout per family (0 lines, 1 Miller, 2 FE)
+constexpr int bench_lds_slots(int fam) {
+  return fam == 0 ? ENG_LDS_SLOTS_LINES : fam == 1 ? ENG_LDS_SLOTS_MILLER : ENG_LDS_SLOTS_FE;
+}
+__device__ __forceinline__ int bench_gbase(int fam, int g) {
+  return fam == 0 ? ENG_GBASE_LINES[g] : fam == 1 ? ENG_GBASE_MILLER[g] : ENG_GBASE_FE[g];
+}
+template <int FAM>
 __global__ void __launch_bounds__(64, 3) k_bench(int op, int reps, const uint32_t* __restrict__ init,
                                                  uint32_t* __restrict__ out, int sub_first, int sub_count) {
-  __shared__ uint32_t lds[(ENG_NCONST + ENG_GROUPS_PER_WAVE * NSLOTS) * ENG_SLOT_WORDS + ENGBENCH_PAD_WORDS];
+  constexpr int NSLOTS = FAM == 0 ? ENG_SLOTS_LINES : FAM == 1 ? ENG_SLOTS_MILLER : ENG_SLOTS_FE;
+  __shared__ uint32_t lds[bench_lds_slots(FAM) * ENG_SLOT_WORDS + ENGBENCH_PAD_WORDS];
 #ifdef ENGBENCH_LDS_RECORDS   // the op's records staged in LDS instead of read from global memory
   __shared__ __attribute__((aligned(16))) uint32_t rec[528];  // largest op's record span
   const uint32_t s0 = ENG_OP_TAB[op][0], sl = s0 + ENG_OP_TAB[op][1] - 1;
@@ -46,7 +54,7 @@ __global__ void __launch_bounds__(64, 3) k_bench(int op, int reps, const uint32_
 #else
 #define ENGBENCH_RUN_ARGS
 #endif
-  constexpr int W = (ENG_NCONST + ENG_GROUPS_PER_WAVE * NSLOTS) * ENG_SLOT_WORDS;
+  constexpr int W = bench_lds_slots(FAM) * ENG_SLOT_WORDS;
   const uint32_t* src = init + (size_t)(blockIdx.x & 63) * W;
   for (int t = threadIdx.x; t < W; t += blockDim.x) lds[t] = src[t];
   __syncthreads();
@@ -54,17 +62,17 @@ __global__ void __launch_bounds__(64, 3) k_bench(int op, int reps, const uint32_
   const int gi = lane < 60 ? lane / 12 : 4;
   const int k = lane < 60 ? lane % 12 : lane - 60;
   uint32_t* c = lds;
-  uint32_t* g = lds + (ENG_NCONST + gi * NSLOTS) * ENG_SLOT_WORDS;
+  uint32_t* g = lds + bench_gbase(FAM, gi) * ENG_SLOT_WORDS;
   uint32_t sink_acc = 0;
 #pragma unroll 1
   for (int r = 0; r < reps; ++r) {
     if (op == -1) {  // E_CYC with its LIN sub-op
-      eng_cyc_fast<true>(g, k);
+      eng_cyc_fast<true>(g, k, fp{});
       continue;
     }
-    if (op == -2) {  // E_CYC after an E_CYC (fused LIN epilogue)
-      eng_cyc_fast<false>(g, k);
-      continue;
+    if (op == -2) {  // one chain of reps E_CYC (fused LIN epilogue, post operand in registers)
+      eng_cyc_chain(g, k, reps);
+      break;
     }
     if (op >= 1000) {  // compiled form (engine_compiled.h)
       auto snk = [&](uint32_t e, const fp& v) { sink_acc += v.l[0] ^ e; };
@@ -166,9 +174,9 @@ int main(int argc, char** argv) {
   for (const OpDesc& o : ops) {
     if (only && !strstr(only, o.name)) continue;
     auto launch = [&](int r) {
-      if (o.fam == 0) hipLaunchKernelGGL(k_bench<ENG_SLOTS_LINES>, dim3(blocks), dim3(64), 0, 0, o.op, r, d_init, d_out, o.sub_first, o.sub_count);
-      else if (o.fam == 1) hipLaunchKernelGGL(k_bench<ENG_SLOTS_MILLER>, dim3(blocks), dim3(64), 0, 0, o.op, r, d_init, d_out, o.sub_first, o.sub_count);
-      else hipLaunchKernelGGL(k_bench<ENG_SLOTS_FE>, dim3(blocks), dim3(64), 0, 0, o.op, r, d_init, d_out, o.sub_first, o.sub_count);
+      if (o.fam == 0) hipLaunchKernelGGL(k_bench<0>, dim3(blocks), dim3(64), 0, 0, o.op, r, d_init, d_out, o.sub_first, o.sub_count);
+      else if (o.fam == 1) hipLaunchKernelGGL(k_bench<1>, dim3(blocks), dim3(64), 0, 0, o.op, r, d_init, d_out, o.sub_first, o.sub_count);
+      else hipLaunchKernelGGL(k_bench<2>, dim3(blocks), dim3(64), 0, 0, o.op, r, d_init, d_out, o.sub_first, o.sub_count);
     };
     launch(2);
     CK(hipDeviceSynchronize());

@@ -848,6 +848,7 @@ def cyc_fast_params(ops, name="E_CYC"):
                 w.append(0)
         (ps, d), = pr.post
         assert ps < 64 and -128 <= d < 128
+        assert ps == pr.dst   # the post operand is the lane's own slot (engine.cuh eng_cyc_chain keeps it in registers)
         w.append(ps * slot | (pr.dst * slot) << 16)
         flags |= len(terms) << 8 | (pr.cm & 0xFF) << 16 | (d & 0xFF) << 24
         # fused LIN: this lane holds coefficient half pr.dst; partner k ^ 1 the other half
@@ -886,10 +887,12 @@ def sub_shape(sub):
     lanes = [sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2)) for r in sub] + [[]] * (LANES - len(sub))
     nt = max(len(t) for t in lanes)
     ntmin = min(len(t) for t in lanes)
-    xf = 0
+    xf = 0   # bit t: some lane negates term t's b operand; bit 16 + t: some lane doubles it
     for t in range(nt):
-        if any(t < len(ts) and (ts[t][2] < 0 or ts[t][3] == 2) for ts in lanes):
+        if any(t < len(ts) and ts[t][2] < 0 for ts in lanes):
             xf |= 1 << t
+        if any(t < len(ts) and ts[t][3] == 2 for ts in lanes):
+            xf |= 1 << (16 + t)
     np_ = max(len(r.post) for r in sub)
     plain = all(r.cm == 1 and not r.post for r in sub) and len(sub) == LANES
     kind = "ENG_K_PLAIN" if plain else ("ENG_K_LIN" if nt == 0 else "ENG_K_MIXED")
@@ -983,6 +986,16 @@ def check_bounds(ops):
                     assert s < 64 + N_CONST
 
 
+# Group bases in LDS (slots from the start of the block's LDS; the constant
+# region takes slots 0 .. N_CONST-1): consecutive groups, no padding.  The
+# bank model (tools/lds_banks.py search_bases) predicted 10-45% fewer
+# operand-load LDS cycles for padded bases (lines 24 + 51 g, Miller
+# [24, 65, 113, 161, 202], FE [24, 71, 117, 164, 210] with the hard part's
+# blocks reordered), but those measured slower (profiles/r02/r02s_group_bases_ab.json:
+# lines +3%, Miller +2%), so the layout stays packed.
+GROUP_BASES = {k: [N_CONST + g * n for g in range(5)] for k, n in (("LINES", 50), ("MILLER", 34), ("FE", 46))}
+
+
 def emit(path):
     ops = build_ops()
     check_bounds(ops)
@@ -1025,7 +1038,12 @@ def emit(path):
         "FE": max(v for k, v in nslots.items() if k.startswith("E_")),
     }
     for k, v in nsl.items():
+        b = GROUP_BASES[k]
+        assert b[0] >= N_CONST and all(b[g + 1] - b[g] >= v for g in range(4)), (k, v, b)
         lines.append(f"constexpr int ENG_SLOTS_{k} = {v};")
+        # group g's slots start at LDS slot ENG_GBASE_k[g]; the block's LDS is ENG_LDS_SLOTS_k slots
+        lines.append(f"constexpr int ENG_GBASE_{k}[5] = {{{', '.join(map(str, b))}}};")
+        lines.append(f"constexpr int ENG_LDS_SLOTS_{k} = {b[4] + v};")
     lines.append("")
     lines.append("#ifndef ENG_TABLE_QUAL")
     lines.append("#define ENG_TABLE_QUAL static const")
@@ -1044,6 +1062,11 @@ def emit(path):
     cyc = {o.name: o for o in ops}["E_CYC"].subs[1]
     lines.append("// eng_cyc_fast: per-lane parameters of E_CYC (tools/gen_engine.py cyc_fast_params)")
     lines.append(f"constexpr int ENG_CYC_CM = {cyc[0].cm}, ENG_CYC_ABSD = {abs(cyc[0].post[0][1])};")
+    xf = 0   # product term t: bit t some lane negates, bit 16 + t some lane doubles (eng_cyc_term)
+    for r in cyc:
+        for t, (_, _, sg, cf) in enumerate(sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2))):
+            xf |= (sg < 0) << t | (cf == 2) << (16 + t)
+    lines.append(f"constexpr uint32_t ENG_CYC_XF = 0x{xf:x}u;")
     lines.append(f"alignas(16) ENG_TABLE_QUAL uint32_t ENG_CYC_PAR[{LANES}][8] = {{")
     for w in rows:
         lines.append("  {" + ", ".join(f"0x{x:08x}u" for x in w) + "},")

@@ -35,9 +35,12 @@ LANES = lane_map()
 
 
 def word(g, s, S):
+    """S: the group stride (group g at NCONST + g S), or a list of the five
+    group bases (slots from the start of LDS)."""
     if s >= 64:
         return (s - 64) * SW
-    return (ge.N_CONST + g * S + s) * SW
+    base = S[g] if isinstance(S, (list, tuple)) else ge.N_CONST + g * S
+    return (base + s) * SW
 
 
 def cycles_b64(slot_of_k, S):
@@ -74,7 +77,7 @@ def sub_loads(sub):
 
 
 def op_cycles(op, S, cache={}):
-    key = (op.name, S)
+    key = (op.name, tuple(S) if isinstance(S, list) else S)
     if key not in cache:
         c = 0
         for sub in op.subs:
@@ -91,6 +94,33 @@ def min_cycles(op):
 
 def program_ops(prog):
     return Counter(ins[1] for ins in prog if ins[0] == "run")
+
+
+def search_bases(ops, cnt, used, max_slots, rounds=3):
+    """Group bases NCONST + g used + c_g with 0 = c_0 <= c_1 <= ... <= c_4 and
+    the wave's LDS within max_slots, by coordinate descent on the gaps
+    (conflicts depend on the bases mod 32 only, so gaps < 32)."""
+    spare = max_slots - ge.N_CONST - 5 * used
+
+    def cost(gaps):
+        cs = [0]
+        for x in gaps:
+            cs.append(cs[-1] + x)
+        bases = [ge.N_CONST + g * used + cs[g] for g in range(5)]
+        return sum(n * op_cycles(ops[o], bases) for o, n in cnt.items()), bases
+
+    gaps = [0, 0, 0, 0]
+    best = cost(gaps)
+    for _ in range(rounds):
+        for j in range(4):
+            for x in range(min(31, spare) + 1):
+                trial = gaps[:j] + [x] + gaps[j + 1:]
+                if sum(trial) > spare:
+                    break
+                c = cost(trial)
+                if c[0] < best[0]:
+                    best, gaps = c, trial
+    return best
 
 
 def main():

@@ -40,19 +40,21 @@ DG_FN g2j g2_cmov(const g2j& a, const g2j& b, bool take_b) {
 //   D - X3 = 2(D/2) + 8p - X3 carried (< 12.02p) into fp2_mul with E
 //   (sum products 12.06p x 24.04p); 8C carried (< 16.08p);
 //   Z3 = (2Y) Z with 2Y lazy (limbs < 2^29, fp2_mul's sum < 2^30).
+// Evaluation order keeps at most five Fp2 values live across the
+// out-of-line Fp calls (Z3 first frees Z, B frees Y, X + B frees X, ...).
 DG_FN g2j g2_dbl_body(const g2j& p) {
-  const fp2 A = fp2_sqr(p.x);
-  const fp2 B = fp2_sqr(p.y);
-  const fp2 C = fp2_sqr(B);
-  const fp2 Dh = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(p.x, B))), fp2_add_lz(A, C));
-  const fp2 E = fp2_carry(fp2_add_lz(fp2_add_lz(A, A), A));
-  const fp2 F = fp2_sqr(E);
   g2j r;
-  r.x = fp2_sub32(F, fp2_carry(fp2_mulk_lz(Dh, 4)));
+  r.z = fp2_mul(fp2_add_lz(p.y, p.y), p.z);
+  const fp2 B = fp2_sqr(p.y);
+  const fp2 A = fp2_sqr(p.x);
+  const fp2 XB = fp2_carry(fp2_add_lz(p.x, B));
+  const fp2 C = fp2_sqr(B);
+  const fp2 Dh = fp2_sub32(fp2_sqr(XB), fp2_add_lz(A, C));
+  const fp2 E = fp2_carry(fp2_add_lz(fp2_add_lz(A, A), A));
+  r.x = fp2_sub32(fp2_sqr(E), fp2_carry(fp2_mulk_lz(Dh, 4)));
   const fp2 D2 = fp2_add_lz(Dh, Dh);
   const fp2 DX = fp2_carry(fp2{fp_sub_lz(D2.c0, r.x.c0), fp_sub_lz(D2.c1, r.x.c1)});
   r.y = fp2_sub32(fp2_mul(E, DX), fp2_carry(fp2_mulk_lz(C, 8)));
-  r.z = fp2_mul(fp2_add_lz(p.y, p.y), p.z);
   return r;
 }
 

@@ -111,6 +111,7 @@ DG_FN fp fp_redc_cols(const uint64_t* t) {
   return r;
 }
 
+#if defined(DG_FP_SOS)
 // Product columns left unnormalized (each < 14 * 2^60 for limbs < 2^30)
 // and fed straight to the reduction.
 DG_FPK fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
@@ -146,6 +147,76 @@ DG_FPK fp fp_sqr_r(DG_LIMB_PARAMS(x)) {
   t[2 * FP_LIMBS - 1] = 0;
   return fp_redc_cols(t);
 }
+#else
+// Finely integrated product scanning (FIPS): column k of the product and of
+// the reduction's m * p go into one running 64-bit accumulator (same bound
+// as above: < 14 * 2^60 + 14 * 2^56 + carry < 2^64), so no 27-column array
+// is held: ~50 VGPRs instead of 81 for the separated form.  These functions
+// are called out of line from loops whose live state must survive the calls
+// in the registers a call does not clobber, so their register footprint
+// matters as much as their instruction count.
+DG_FPK fp fp_mul_r(DG_LIMB_PARAMS(x), DG_LIMB_PARAMS(y)) {
+  const fp a = DG_LIMB_PACK(x), b = DG_LIMB_PACK(y);
+  DG_COUNT(dg_count_mul);
+  uint32_t m[FP_LIMBS];
+  fp r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * FP_LIMBS; ++k) {
+#pragma unroll
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); i <= (k < FP_LIMBS ? k : FP_LIMBS - 1); ++i)
+      if (k < 2 * FP_LIMBS - 1) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); i < (k < FP_LIMBS ? k : FP_LIMBS); ++i)
+      acc += (uint64_t)m[i] * FP_P[k - i];
+    if (k < FP_LIMBS) {
+      m[k] = ((uint32_t)acc * FP_PINV) & FP_MASK;
+      acc += (uint64_t)m[k] * FP_P[0];
+      acc >>= FP_BITS;
+    } else if (k < 2 * FP_LIMBS - 1) {
+      r.l[k - FP_LIMBS] = (uint32_t)acc & FP_MASK;
+      acc >>= FP_BITS;
+    } else {
+      r.l[k - FP_LIMBS] = (uint32_t)acc;
+    }
+  }
+  return r;
+}
+
+// Squaring: cross products once, doubled per column, then the column's
+// reduction terms (FIPS as fp_mul_r).
+DG_FPK fp fp_sqr_r(DG_LIMB_PARAMS(x)) {
+  const fp a = DG_LIMB_PACK(x);
+  DG_COUNT(dg_count_sqr);
+  uint32_t m[FP_LIMBS];
+  fp r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * FP_LIMBS; ++k) {
+    if (k < 2 * FP_LIMBS - 1) {
+      uint64_t c = 0;
+#pragma unroll
+      for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); 2 * i < k; ++i) c += (uint64_t)a.l[i] * a.l[k - i];
+      acc += c << 1;
+      if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    }
+#pragma unroll
+    for (int i = (k < FP_LIMBS ? 0 : k - FP_LIMBS + 1); i < (k < FP_LIMBS ? k : FP_LIMBS); ++i)
+      acc += (uint64_t)m[i] * FP_P[k - i];
+    if (k < FP_LIMBS) {
+      m[k] = ((uint32_t)acc * FP_PINV) & FP_MASK;
+      acc += (uint64_t)m[k] * FP_P[0];
+      acc >>= FP_BITS;
+    } else if (k < 2 * FP_LIMBS - 1) {
+      r.l[k - FP_LIMBS] = (uint32_t)acc & FP_MASK;
+      acc >>= FP_BITS;
+    } else {
+      r.l[k - FP_LIMBS] = (uint32_t)acc;
+    }
+  }
+  return r;
+}
+#endif
 
 // ---------------------------------------------------------------- normalization
 // Carry-propagate: limbs < 2^28 except the top one.  Input limbs < 2^31.

@@ -132,7 +132,7 @@ int main(int argc, char** argv) {
       {"E_MULCJ", OP_E_MULCJ, 2}, {"E_XIA", OP_E_XIA, 2},     {"E_FROB1", OP_E_FROB1, 2},
       {"E_CYC_lin", OP_E_CYC, 2, 0, 1}, {"E_CYC_prod", OP_E_CYC, 2, 1, 1}, {"E_CYC_fast", -1, 2}, {"E_CYC_chain", -2, 2},
       {"LDBL_c", 1000 + OP_LDBL, 0}, {"LADD_c", 1000 + OP_LADD, 0}, {"M_SQR_c", 1000 + OP_M_SQR, 1},
-      {"M_XIF_c", 1000 + OP_M_XIF, 1}, {"E_MUL_c", 1000 + OP_E_MUL, 2}, {"E_XIA_c", 1000 + OP_E_XIA, 2},
+      {"M_XIF_c", 1000 + OP_M_XIF, 1}, {"M_LM1_c", 1000 + OP_M_LM1, 1}, {"E_MUL_c", 1000 + OP_E_MUL, 2}, {"E_XIA_c", 1000 + OP_E_XIA, 2},
   };
   constexpr int WMAX = (ENG_NCONST + ENG_GROUPS_PER_WAVE * 64) * ENG_SLOT_WORDS;
   std::vector<uint32_t> h((size_t)64 * WMAX);

@@ -878,8 +878,9 @@ def cyc_fast_params(ops, name="E_CYC"):
 # Hot ops run as straight-line code (engine.cuh eng_sub_c): the generator
 # fixes each sub-op's shape at compile time.  Families: the kernel whose
 # eng_exec includes the op (0 lines, 1 miller, 2 fe).
-# (M_LM1 / M_LM2 stay interpreted: compiled, they push k_eng_miller to 142 spilled VGPRs)
-COMPILED = {"LDBL": 0, "LADD": 0, "M_XIF": 1, "M_SQR": 1, "M_XIL": 1,
+# (M_LM1 / M_LM2 compile without spills since eng_sub_c fences each term's
+# products; without the fence k_eng_miller spilled 179 VGPRs)
+COMPILED = {"LDBL": 0, "LADD": 0, "M_XIF": 1, "M_SQR": 1, "M_XIL": 1, "M_LM1": 1, "M_LM2": 1,
             "E_MUL": 2, "E_MULCJ": 2, "E_XIA": 2}
 
 

@@ -8,6 +8,12 @@ TAG=${TAG:-r02u}
 O=gpurun_out/$TAG
 mkdir -p $O
 step() { echo "== $1 $(date +%T)"; }
+if [ -n "$TEST" ]; then
+step pytest
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log
+[ $rc -ne 0 ] && exit $rc
+fi
 step bench
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?
 head -c 700 $O/bench.json; echo

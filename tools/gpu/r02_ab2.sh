@@ -26,7 +26,7 @@ for pass in 1 2; do
     name=$(basename $v .so)
     step "bench $name pass $pass"
     DRAND_GPU_LIB=$PWD/$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-e2e ${RLC:---no-rlc} --rounds ${ROUNDS:-2000000} --steps 3 > $O/${name}_$pass.json 2> $O/${name}_$pass.err || exit $?
-    python3 -c "import json; d=json.load(open('$O/${name}_$pass.json')); print('$name', round(d['value']), d['verdict_mismatches'], {k: round(v,1) for k,v in d['stage_ms'].items()}, 'rlc', round(d['rlc']['value']) if 'rlc' in d else None)"
+    python3 -c "import json; d=json.load(open('$O/${name}_$pass.json')); print('$name', round(d['value']), d['verdict_mismatches'], {k: round(v,1) for k,v in d['stage_ms'].items()}, 'rlc', round(d['rlc']['value']) if d.get('rlc') else None)"
   done
 done
 echo done

@@ -51,7 +51,7 @@ DG_FN g1j map_to_curve_sswu_iso11_body(const fp& u) {
   const fp D2 = fp_sqr(D);
   const fp D3 = fp_mul(D2, D);
   const fp U = fp_add(fp_mul(N, fp_add(fp_sqr(N), fp_mul(C_SSWU1_A, D2))), fp_mul(C_SSWU1_B, D3));
-  const fp t = fp_pow(fp_mul(U, fp_mul(fp_sqr(D3), D3)), EXP_P_MINUS_3_DIV_4, EXP_P_MINUS_3_DIV_4_BITS);
+  const fp t = DG_POW(fp_mul(U, fp_mul(fp_sqr(D3), D3)), EXP_P_MINUS_3_DIV_4);
   fp y = fp_mul(fp_mul(U, D3), t);
   if (!fp_eq(fp_mul(fp_sqr(y), D3), U)) {  // gx1 not square: x2 = Z u^2 x1
     y = fp_mul(fp_mul(C_SSWU1_Z_SQRT_MZ, fp_mul(fp_sqr(u), u)), y);

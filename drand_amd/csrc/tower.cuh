@@ -105,7 +105,7 @@ DG_NOINL fp2 fp2_sqrt_scaled(const fp2& w, const fp& g, const fp& m) {
   d = fp_cmov(d, fp_half(fp_sub(w.c0, g)), fp_is_zero(d));
   const fp m2 = fp_sqr(m);
   const fp dm4 = fp_mul(d, fp_sqr(m2));
-  const fp t = fp_pow(dm4, EXP_P_MINUS_3_DIV_4, EXP_P_MINUS_3_DIV_4_BITS);
+  const fp t = DG_POW(dm4, EXP_P_MINUS_3_DIV_4);
   const bool sq = fp_eq(fp_mul(dm4, fp_sqr(t)), fp_one());
   const fp dt = fp_mul(d, t);
   const fp wt = fp_half(fp_mul(w.c1, t));

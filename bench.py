@@ -100,9 +100,9 @@ def engine_work():
 
 
 def hash_work():
-    """Per-item v_mad_u64_u32 counts of the hash / decode kernels
-    (tools/count_ops.py -> profiles/op_counts.json, counted by the host build
-    of the same device functions)."""
+    """Per-round v_mad_u64_u32 counts of the hash / decode kernels of the
+    chained per-round pipeline (tools/count_ops.py -> profiles/op_counts.json,
+    counted by the host build of the same device functions)."""
     p = os.path.join(ROOT, "profiles", "op_counts.json")
     if not os.path.exists(p):
         return {}
@@ -151,6 +151,10 @@ def roofline_for(stage_ms, items):
         achieved = items * per_item / (ms * 1e-3)
         out.update(achieved=achieved / 1e12, frac=achieved / PEAK_MAD_U64_PER_S, work_per_item_mads=per_item,
                    work_source="profiles/engine_work.json" if kern in engine_work() else "profiles/op_counts.json")
+    # the same fraction for every stage that has a work figure (hash and decode
+    # from profiles/op_counts.json, the engine from profiles/engine_work.json)
+    out["stage_frac"] = {s: items * work[STAGE_KERNEL.get(s, s)]["mads"] / (t * 1e-3) / PEAK_MAD_U64_PER_S
+                         for s, t in stage_ms.items() if STAGE_KERNEL.get(s, s) in work and t > 0}
     traffic, src = traffic_for(kern, items)
     if traffic is not None:
         out["traffic"] = traffic

@@ -48,6 +48,35 @@ int hs_count_stages(const uint8_t* pk48, const uint8_t* prev, uint32_t prev_len,
 #endif
 }
 
+// Per-kernel Fp mul/sqr counts of the per-round pipeline as the device runs
+// it (DG_COUNT_OPS builds): out[0..7] = mul,sqr of k_h2c_field, k_h2c_sswu
+// (both of a round's items), k_h2c_finish, k_decode_g2_sigs (membership left
+// to k_eng_lines, check_subgroup = 0).
+int hs_count_kernels(const uint8_t* prev, uint32_t prev_len, uint64_t round, const uint8_t* sig96,
+                     unsigned long long* out) {
+#ifdef DG_COUNT_OPS
+  uint32_t m[8];
+  drand_digest(m, prev, prev_len, round);
+  fp2 u0, u1;
+  dg_count_mul = dg_count_sqr = 0;
+  hash_to_field_g2(u0, u1, m);
+  out[0] = dg_count_mul; out[1] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  const g2j q0 = map_to_curve_sswu_iso3_body(u0), q1 = map_to_curve_sswu_iso3_body(u1);
+  out[2] = dg_count_mul; out[3] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  const g2j h = g2_clear_cofactor_inl(g2_add_body(q0, q1));
+  out[4] = dg_count_mul; out[5] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  g2a s;
+  const int rc = g2_decompress(&s, sig96, false);
+  out[6] = dg_count_mul; out[7] = dg_count_sqr;
+  return rc == DEC_OK && !g2_is_inf(h) ? 0 : -1;
+#else
+  return -100;
+#endif
+}
+
 // a*b, a+b, a-b, a^2 on canonical 48-byte big-endian inputs
 int hs_fp_ops(const uint8_t* a48, const uint8_t* b48, uint8_t* mul, uint8_t* add, uint8_t* sub, uint8_t* sqr,
               uint8_t* inv) {

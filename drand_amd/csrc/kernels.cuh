@@ -130,7 +130,14 @@ __global__ void __launch_bounds__(256) k_h2c_field(size_t n, msg_src m, uint32_t
   for (int k = 0; k < 4; ++k) st_fp(u_out + (size_t)k * FP_WORDS * n, n, i, fp_from_be64_words(uni + 16 * k));
 }
 
-__global__ void __launch_bounds__(256, 2) k_h2c_sswu(size_t n, const uint32_t* __restrict__ u,
+// Minimum blocks per CU of the two heavy hash kernels (A/B knobs).
+#ifndef DG_SSWU_OCC
+#define DG_SSWU_OCC 2
+#endif
+#ifndef DG_FINISH_OCC
+#define DG_FINISH_OCC 2
+#endif
+__global__ void __launch_bounds__(256, DG_SSWU_OCC) k_h2c_sswu(size_t n, const uint32_t* __restrict__ u,
                                                    uint32_t* __restrict__ q_out) {
   size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= 2 * n) return;
@@ -140,7 +147,7 @@ __global__ void __launch_bounds__(256, 2) k_h2c_sswu(size_t n, const uint32_t* _
   st_g2j(q_out + which * G2J_WORDS * n, n, i, map_to_curve_sswu_iso3_body(uu));
 }
 
-__global__ void __launch_bounds__(256, 2) k_h2c_finish(size_t n, const uint32_t* __restrict__ q,
+__global__ void __launch_bounds__(256, DG_FINISH_OCC) k_h2c_finish(size_t n, const uint32_t* __restrict__ q,
                                                      uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -13,6 +13,9 @@ step pytest
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log
 [ $rc -ne 0 ] && exit $rc
+step smoke
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+tail -1 $O/smoke.log
 fi
 step bench
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || exit $?

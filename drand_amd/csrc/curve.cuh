@@ -243,6 +243,56 @@ DG_NOINL g2j g2_psi2(const g2j& p) {
   return g2j{fp2_mul_fp(p.x, fp2(C_PSI2_CX).c0), fp2_mul_fp(p.y, fp2(C_PSI2_CY).c0), p.z};
 }
 
+// Signed radix-16 digits of a 32-bit k: k = sum_j d_j 16^j with d_j in
+// [-8, 7] for j < 8 and d_8 in {0, 1}; digit j packed at bits 5j..5j+4 as
+// |d_j| (4 bits) and its sign (bit 4).
+DG_FN uint64_t win4_recode32(uint32_t k) {
+  uint64_t out = 0;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t w = ((k >> (4 * j)) & 15u) + c;
+    c = w >= 8u ? 1u : 0u;
+    const uint32_t mag = c ? 16u - w : w;
+    out |= (uint64_t)(mag | (c && mag ? 16u : 0u)) << (5 * j);
+  }
+  return out | ((uint64_t)c << 40);
+}
+
+// [a] q + [b] psi(q) for an affine q (not the identity) and 32-bit a, b with
+// the same operation sequence in every lane.  In k_rlc_leaves the lanes of a
+// wave hold unrelated coefficients, so a digit-driven ladder (the NAF form
+// above) runs the union of its lanes' additions -- about two per bit.  Here:
+// signed radix-16 windows of both scalars over the table T[m] = [m + 1] q
+// (Jacobian, private memory, built with 1 doubling + 6 mixed additions); 8
+// windows of 4 doublings + 2 additions (psi applied to b's entry), a zero
+// digit's addition computed and discarded: 33 doublings, 17 additions.
+DG_FN g2j g2_mul2_win4_affine(const g2a& q, uint32_t a, uint32_t b) {
+  const uint64_t da = win4_recode32(a), db = win4_recode32(b);
+  g2j T[8];
+  T[0] = g2_from_affine(q);
+  T[1] = g2_dbl_body(T[0]);
+#pragma unroll 1
+  for (int m = 2; m < 8; ++m) T[m] = g2_add_affine_body(T[m - 1], q);
+  // top digits (0 or 1): acc = [d_8(a)] q + [d_8(b)] psi(q)
+  g2j acc = g2_cmov(g2_infinity(), T[0], (da >> 40) & 1u);
+  acc = g2_cmov(acc, g2_add_body(acc, g2_psi(T[0])), (db >> 40) & 1u);
+#pragma unroll 1
+  for (int j = 7; j >= 0; --j) {
+#pragma unroll 1
+    for (int s = 0; s < 4; ++s) acc = g2_dbl_body(acc);
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t dg = (uint32_t)(((s ? db : da) >> (5 * j)) & 31u), mag = dg & 15u;
+      g2j t = T[(mag - 1u) & 7u];
+      if (s) t = g2_psi(t);
+      t.y = fp2_cmov(t.y, fp2_neg(t.y), (dg & 16u) != 0);
+      acc = g2_cmov(acc, g2_add_body(acc, t), mag != 0);
+    }
+  }
+  return acc;
+}
+
 DG_NOINL bool g2_eq(const g2j& p, const g2j& q) {
   bool pi = g2_is_inf(p), qi = g2_is_inf(q);
   if (pi || qi) return pi && qi;

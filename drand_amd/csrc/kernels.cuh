@@ -331,8 +331,9 @@ __device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t idx) {
 // same soundness as a uniform 64-bit r_i, at half the doublings.  R_i is affine
 // here (k_g2_batch_affine ran on the pre-cofactor hash points; (0, 0) marks
 // the identity).  2n threads: j < n computes P_j, j >= n computes S_{j-n}.
-// Two waves per SIMD with psi(q) recomputed at its digits measured fastest
-// (1 or 3 waves, or psi(q) held live: 120 vs 123-157 ms per 1M rounds).
+// The scalar multiplication is the window form (g2_mul2_win4_affine): every
+// lane runs the same sequence; the NAF ladder (DG_RLC_NAF) ran the union of
+// its lanes' digit-driven additions.
 __global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, uint64_t seed, const uint32_t* __restrict__ r_aff,
                                                             const uint32_t* __restrict__ sig_pts,
                                                             const uint8_t* __restrict__ status,
@@ -346,7 +347,11 @@ __global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, uint64_t seed, 
     const g2a q = ld_g2a(sig ? sig_pts : r_aff, n, i);
     if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) {
       const uint64_t z = rlc_coeff(seed, i);
+#if defined(DG_RLC_NAF)
       acc = g2_mul2_naf32_affine<true>(q, q, (uint32_t)z, (uint32_t)(z >> 32));
+#else
+      acc = g2_mul2_win4_affine(q, (uint32_t)z, (uint32_t)(z >> 32));
+#endif
     }
   }
   st_g2j(sig ? s_out : p_out, n, i, acc);

@@ -226,6 +226,23 @@ extern "C" int hs_cyclo_sqr_check(const uint8_t* p48, const uint8_t* q96) {
   return 0;
 }
 
+// The RLC leaves' window ladder against plain double-and-add on a hashed
+// point R (not in G2: psi is applied, not [x]) for the scalar pairs given.
+extern "C" int hs_g2_mul2_win4_check(const uint8_t* msg32, const uint32_t* ab, int n) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  fp2 u0, u1;
+  hash_to_field_g2(u0, u1, m);
+  const g2j R = g2_add(map_to_curve_sswu_iso3(u0), map_to_curve_sswu_iso3(u1));
+  const g2a Ra = g2_to_affine(R);
+  for (int i = 0; i < n; ++i) {
+    const uint32_t a = ab[2 * i], b = ab[2 * i + 1];
+    const g2j want = g2_add(g2_mul_words(R, &a, 1), g2_mul_words(g2_psi(R), &b, 1));
+    if (!g2_eq(g2_mul2_win4_affine(Ra, a, b), want)) return i + 1;
+  }
+  return 0;
+}
+
 // RLC collapse check over a whole batch (same device functions as k_rlc_*):
 // returns 0 if e(pk, h_eff * sum r_i R_i) * e(-g1, sum r_i sig_i) == 1.
 extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, const uint8_t* sigs96, int n,
@@ -253,10 +270,11 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
     g2j rR = g2_mul2_naf32_affine<true>(Ra, Ra, a, b);
     if (!g2_eq(rR, g2_add(g2_mul_words(R, &a, 1), g2_mul_words(g2_psi(R), &b, 1)))) return -3;
     if (!g2_eq(rR, g2_mul2_naf32_affine<false>(Ra, g2a_psi(Ra), a, b))) return -5;
+    if (!g2_eq(rR, g2_mul2_win4_affine(Ra, a, b))) return -6;
     const uint32_t kw[2] = {a, b};
     if (!g2_eq(g2_mul64_naf_affine(Ra, z), g2_mul_words(R, kw, 2))) return -4;
     P = g2_add(P, rR);
-    S = g2_add(S, g2_mul2_naf32_affine<true>(s, s, a, b));
+    S = g2_add(S, g2_mul2_win4_affine(s, a, b));
   }
   g2a Pa = g2_to_affine(g2_clear_cofactor(P)), Sa = g2_to_affine(S);
   fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);

@@ -151,6 +151,21 @@ def test_rlc_collapse_algebra(hostsim):
     assert hostsim.hs_rlc_batch_check(pk, msgs, bad, 5, ctypes.c_uint64(99), rounds) == 1
 
 
+def test_rlc_window_ladder_edge_scalars(hostsim):
+    """k_rlc_leaves' uniform ladder [a] q + [b] psi(q) (signed radix-16
+    windows, zero digits computed and discarded) equals plain double-and-add
+    on a point outside G2, for scalar halves at the recoding's edges: zero
+    halves, digits 7 / 8 / 9 (sign flips and carries), carry chains into the
+    top digit, and random pairs."""
+    import random
+    rnd = random.Random(7)
+    edge = [0, 1, 7, 8, 9, 15, 16, 0x88888888, 0x77777777, 0xFFFFFFFF, 0x80000000, 0x7FFFFFFF, 0xF8F8F8F8]
+    pairs = [(a, b) for a in edge[:7] for b in (0, 8, 0xFFFFFFFF)] + [(a, a ^ 0x5A5A5A5A) for a in edge]
+    pairs += [(rnd.getrandbits(32), rnd.getrandbits(32)) for _ in range(8)]
+    ab = (ctypes.c_uint32 * (2 * len(pairs)))(*[v for p in pairs for v in p])
+    assert hostsim.hs_g2_mul2_win4_check(bytes(range(32)), ab, len(pairs)) == 0
+
+
 def test_engine_pairing_host_emulation(hostsim):
     """The device engine's per-lane arithmetic (engine.cuh) run by the host
     emulation over the generated programs: verdict and the exact GT value

@@ -1324,8 +1324,18 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
                      (const uint8_t*)d_ok, (const uint32_t*)xs, dig);
   HIP_TRY(hipGetLastError());
   mark(c, s, "recover_msm");
+#if defined(DG_RECOVER_MSM_BITS)
   hipLaunchKernelGGL(k_recover_msm, dim3(grid_for(4 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t,
                      (const uint8_t*)d_ok, (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part);
+#else
+  {
+    // window tables sized to t (private memory: TMAX x 8 Jacobian points per thread)
+    auto msm = t <= 8 ? k_recover_msm_w4<8> : t <= 16 ? k_recover_msm_w4<16> : t <= 24 ? k_recover_msm_w4<24>
+                                                                                         : k_recover_msm_w4<32>;
+    hipLaunchKernelGGL(msm, dim3(grid_for(4 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t, (const uint8_t*)d_ok,
+                       (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part);
+  }
+#endif
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_recover_finish, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, (const uint8_t*)d_ok,
                      (const uint32_t*)part, d_out, rpts, rst);

@@ -249,6 +249,65 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm(size_t n_rounds, int t, 
   st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
 }
 
+// Signed radix-16 digit j (0..16) of a 64-bit k: d_j = w_j + b_{4j-1} - 16
+// b_{4j+3} (w_j the 4-bit window, b the bits of k), in [-8, 8];
+// k = sum_j d_j 16^j.
+DG_FN int win4_digit64(uint64_t k, int j) {
+  const int w = j < 16 ? (int)((k >> (4 * j)) & 15u) : 0;
+  const int cin = j ? (int)((k >> (4 * j - 1)) & 1u) : 0;
+  const int cout = j < 16 ? (int)((k >> (4 * j + 3)) & 1u) : 0;
+  return w + cin - 16 * cout;
+}
+
+// k_recover_msm with the same operation sequence in every lane.  The lanes
+// of a wave hold different rounds, whose signer sets (so Lagrange digits)
+// differ; the bit-driven loop above runs an addition whenever any lane's bit
+// is set, i.e. about 64 t per thread.  Here: per point j a table
+// [1..8] sig_j (Jacobian, private memory, 1 doubling + 6 mixed additions),
+// then 17 signed radix-16 windows of 4 doublings + t additions (a zero
+// digit's addition computed and discarded): 16 t + 7 t additions in all.
+// TMAX bounds t (private table TMAX x 8 points).
+template <int TMAX>
+__global__ void __launch_bounds__(256, 2) k_recover_msm_w4(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
+                                                         const uint32_t* __restrict__ sel,
+                                                         const uint64_t* __restrict__ digits,
+                                                         const uint32_t* __restrict__ sig_pts, size_t n_items,
+                                                         uint32_t* __restrict__ part) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 4 * n_rounds) return;
+  const size_t r = g >> 2;
+  const int i = (int)(g & 3);
+  if (!ok[r] || t > TMAX) return;
+  const uint64_t* d = digits + r * RECOVER_MAX_T * 4 + i;
+  const uint32_t* sl = sel + r * RECOVER_MAX_T;
+  g2j T[TMAX][8];
+#pragma unroll 1
+  for (int j = 0; j < t; ++j) {
+    const g2a q = ld_g2a(sig_pts, n_items, sl[j]);
+    T[j][0] = g2_from_affine(q);
+    T[j][1] = g2_dbl_body(T[j][0]);
+#pragma unroll 1
+    for (int m = 2; m < 8; ++m) T[j][m] = g2_add_affine_body(T[j][m - 1], q);
+  }
+  g2j acc = g2_infinity();
+#pragma unroll 1
+  for (int w = 16; w >= 0; --w) {
+    if (w < 16) {
+#pragma unroll 1
+      for (int s = 0; s < 4; ++s) acc = g2_dbl_body(acc);
+    }
+#pragma unroll 1
+    for (int j = 0; j < t; ++j) {
+      const int dg = win4_digit64(d[4 * j], w);
+      const int mag = dg < 0 ? -dg : dg;
+      g2j e = T[j][(mag - 1) & 7];
+      e.y = fp2_cmov(e.y, fp2_neg(e.y), dg < 0);
+      acc = g2_cmov(acc, g2_add_body(acc, e), mag != 0);
+    }
+  }
+  st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
+}
+
 __global__ void __launch_bounds__(64) k_recover_finish(size_t n_rounds, const uint8_t* __restrict__ ok,
                                                        const uint32_t* __restrict__ part, uint8_t* __restrict__ out96,
                                                        uint32_t* __restrict__ rec_pts, uint8_t* __restrict__ rec_st) {

@@ -179,23 +179,41 @@ class BoltStore:
             raise BoltFormatError(f"{path}: no bucket {bucket!r}")
         self._b = _Bucket(self, v)
 
+    def _read_meta(self, off):
+        """The meta at byte offset `off` (a page start), or None if it fails
+        bbolt's meta.validate (magic, version, checksum)."""
+        mm = self._mm
+        off += PAGE_HEADER
+        if off + 64 > len(mm):
+            return None
+        magic, ver, psize, flags, root, seq, freelist, hw, txid, chk = struct.unpack_from("<IIIIQQQQQQ", mm, off)
+        if magic != MAGIC or ver != VERSION or chk != fnv1a64(mm[off:off + 56]):
+            return None
+        return {"page_size": psize, "root": root, "sequence": seq, "freelist": freelist, "hw": hw, "txid": txid}
+
     def _meta(self):
+        """bbolt v1.3.4 DB.Open + DB.meta: the page size comes from meta 0 only
+        if meta 0 validates; otherwise bbolt assumes the OS page size (the
+        size the file was created with) and finds meta 1 one page later.
+        Then the valid meta with the larger txid is current.  Besides the OS
+        page size, other common page sizes are tried for meta 1 when meta 0
+        is torn (a file written on another machine)."""
         mm = self._mm
         if len(mm) < 2 * 1024:
             raise BoltFormatError("file shorter than two meta pages")
-        # page 0's meta gives the page size; page 1 sits one page later
-        ps = struct.unpack_from("<I", mm, PAGE_HEADER + 8)[0]
-        best = None
-        for pg in (0, 1):
-            off = pg * ps + PAGE_HEADER
-            if off + 64 > len(mm):
+        m0 = self._read_meta(0)
+        if m0 is not None:
+            sizes = [m0["page_size"]]
+        else:
+            sizes = [mmap.PAGESIZE] + [s for s in (4096, 8192, 16384, 65536) if s != mmap.PAGESIZE]
+        best = m0
+        for ps in sizes:
+            m1 = self._read_meta(ps)
+            if m1 is None or (m0 is None and m1["page_size"] != ps):
                 continue
-            magic, ver, psize, flags, root, seq, freelist, hw, txid, chk = struct.unpack_from("<IIIIQQQQQQ", mm, off)
-            if magic != MAGIC or ver != VERSION or chk != fnv1a64(mm[off:off + 56]):
-                continue
-            m = {"page_size": psize, "root": root, "sequence": seq, "freelist": freelist, "hw": hw, "txid": txid}
-            if best is None or txid > best["txid"]:
-                best = m
+            if best is None or m1["txid"] > best["txid"]:
+                best = m1
+            break
         if best is None:
             raise BoltFormatError("no valid meta page")
         return best

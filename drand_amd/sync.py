@@ -43,6 +43,19 @@ def beacon_marshal(b: Beacon) -> bytes:
     }, separators=(",", ":")).encode()
 
 
+_HEX_DIGITS = frozenset("0123456789abcdefABCDEF")
+
+
+def hex_decode_strict(s: str, name="field") -> bytes:
+    """Go's hex.DecodeString, which hexjson uses for []byte fields: an
+    even-length string of hex digits only.  Python's bytes.fromhex would
+    also accept whitespace between byte pairs ('ab cd'); Go rejects it
+    (InvalidByteError), so the round must come out faulty here too."""
+    if len(s) & 1 or not _HEX_DIGITS.issuperset(s):
+        raise ValueError(f"beacon: {name} is not valid hex")
+    return bytes.fromhex(s)
+
+
 def _json_field(d, name):
     """encoding/json field lookup: exact key first, then case-insensitive."""
     if name in d:
@@ -73,7 +86,7 @@ def beacon_unmarshal(buf: bytes) -> Beacon:
             return b""
         if not isinstance(v, str):
             raise ValueError(f"beacon: {name} is not a hex string")
-        return bytes.fromhex(v)
+        return hex_decode_strict(v, name)
 
     r = _json_field(d, "Round")
     if r is None:

@@ -214,6 +214,13 @@ def recover_cases(name, seed, t, n):
                 "cases": cases})
 
 
+def recover_extra():
+    """The threshold range's other MSM table sizes: t = 12 (the
+    9..16 bucket, typical production thresholds) and t = 32 (RECOVER_MAX_T)."""
+    recover_cases("recover_t12_n20.json", 7, 12, 20)
+    recover_cases("recover_t32_n40.json", 8, 32, 40)
+
+
 if __name__ == "__main__":
     if sys.argv[1:2] == ["--only"]:
         for fn in sys.argv[2:]:
@@ -231,3 +238,5 @@ if __name__ == "__main__":
     if "--recover" in sys.argv or not os.path.exists(os.path.join(HERE, "recover_t17_n32.json")):
         recover_cases("recover_t3_n8.json", 3, 3, 8)
         recover_cases("recover_t17_n32.json", 5, 17, 32)
+    if "--recover" in sys.argv or not os.path.exists(os.path.join(HERE, "recover_t32_n40.json")):
+        recover_extra()

@@ -77,6 +77,91 @@ int hs_count_kernels(const uint8_t* prev, uint32_t prev_len, uint64_t round, con
 #endif
 }
 
+static void msg_words(const uint8_t* msg32, uint32_t m[8]);
+
+// Per-item Fp mul/sqr counts of the RLC and on-G1 pipelines' kernels
+// (DG_COUNT_OPS builds), out[2k], out[2k+1] = mul, sqr of:
+//   k=0 rlc hash: k_h2c_field + k_h2c_sswu (both items) + k_h2c_sum
+//   k=1 k_decode_g2_sigs with the membership check (RLC needs it up front)
+//   k=2 one RLC leaf: g2_mul2_win4_affine (k_rlc_leaves; two per round)
+//   k=3 one tree node: g2_add_body (k_rlc_level; about two per round)
+//   k=4 k_g2_batch_affine per point (a 16-point group's share of the inversion)
+//   k=5 k_hash_to_g1_beacons (expand under the G2 suite's DST + SSWU/iso-11 + h_eff)
+//   k=6 k_decode_g1_sigs (decode + endomorphism membership)
+//   k=7 k_g1_batch_affine per point
+int hs_count_extra(const uint8_t* msg32, const uint8_t* sig96, const uint8_t* sig48, uint64_t coeff,
+                   unsigned long long* out) {
+#ifdef DG_COUNT_OPS
+  uint32_t m[8];
+  msg_words(msg32, m);
+  fp2 u0, u1;
+  dg_count_mul = dg_count_sqr = 0;
+  hash_to_field_g2(u0, u1, m);
+  const g2j R = g2_add_body(map_to_curve_sswu_iso3_body(u0), map_to_curve_sswu_iso3_body(u1));
+  out[0] = dg_count_mul; out[1] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  g2a s;
+  if (g2_decompress(&s, sig96, true) != DEC_OK) return -1;
+  out[2] = dg_count_mul; out[3] = dg_count_sqr;
+  const g2a Ra = g2_to_affine(R);
+  dg_count_mul = dg_count_sqr = 0;
+  const g2j leaf = g2_mul2_win4_affine(Ra, (uint32_t)coeff, (uint32_t)(coeff >> 32));
+  out[4] = dg_count_mul; out[5] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  (void)g2_add_body(leaf, leaf);
+  out[6] = dg_count_mul; out[7] = dg_count_sqr;
+  // k_g2_batch_affine over a 16-point group: prefix products, one inversion,
+  // the backward pass (the kernel's loop bodies)
+  {
+    const int G = 16;
+    fp2 zs[G];
+    for (int i = 0; i < G; ++i) zs[i] = fp2_add(R.z, fp2{fp_one(), fp_zero()});
+    dg_count_mul = dg_count_sqr = 0;
+    fp pre[G], acc = fp_one();
+    for (int i = 0; i < G; ++i) { acc = fp_mul(acc, fp2_norm(zs[i])); pre[i] = acc; }
+    fp inv = fp_inv(acc);
+    for (int i = G - 1; i >= 0; --i) {
+      const fp nz = fp2_norm(zs[i]);
+      const fp ninv = i ? fp_mul(inv, pre[i - 1]) : inv;
+      const fp2 zinv = fp2_mul_fp(fp2_conj(zs[i]), ninv);
+      const fp2 zinv2 = fp2_sqr(zinv);
+      (void)fp2_mul(Ra.x, zinv2);
+      (void)fp2_mul(Ra.y, fp2_mul(zinv2, zinv));
+      if (i) inv = fp_mul(inv, nz);
+    }
+    out[8] = (dg_count_mul + G / 2) / G; out[9] = (dg_count_sqr + G / 2) / G;
+  }
+  dg_count_mul = dg_count_sqr = 0;
+  uint32_t uni[32];
+  expand_xmd<false, 4>(uni, m);
+  const g1j h1 = hash_to_g1_from_uni<true>(uni);
+  out[10] = dg_count_mul; out[11] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  g1a s1;
+  if (g1_decompress_sig(&s1, sig48) != DEC_OK) return -2;
+  out[12] = dg_count_mul; out[13] = dg_count_sqr;
+  {
+    const int G = 16;
+    dg_count_mul = dg_count_sqr = 0;
+    fp pre[G], acc = fp_one();
+    for (int i = 0; i < G; ++i) { acc = fp_mul(acc, h1.z); pre[i] = acc; }
+    fp inv = fp_inv(acc);
+    for (int i = G - 1; i >= 0; --i) {
+      const fp zinv = i ? fp_mul(inv, pre[i - 1]) : inv;
+      const fp zinv2 = fp_sqr(zinv);
+      (void)fp_mul(h1.x, zinv2);
+      (void)fp_mul(h1.y, fp_mul(zinv2, zinv));
+      if (i) inv = fp_mul(inv, h1.z);
+    }
+    out[14] = (dg_count_mul + G / 2) / G; out[15] = (dg_count_sqr + G / 2) / G;
+  }
+  return 0;
+#else
+  (void)msg32; (void)sig96; (void)sig48; (void)coeff; (void)out;
+  return -100;
+#endif
+}
+
 // a*b, a+b, a-b, a^2 on canonical 48-byte big-endian inputs
 int hs_fp_ops(const uint8_t* a48, const uint8_t* b48, uint8_t* mul, uint8_t* add, uint8_t* sub, uint8_t* sqr,
               uint8_t* inv) {

@@ -140,3 +140,33 @@ def test_meta_selection_and_errors(tmp_path):
         be.last()
     be.close()
     assert fnv1a64(b"") == 0xCBF29CE484222325 and fnv1a64(b"a") == 0xAF63DC4C8601EC8C  # FNV-1a-64 test vectors
+
+
+def test_torn_meta0_opens_from_meta1(tmp_path):
+    """bbolt v1.3.4 Open: when meta 0 fails validation its page size is not
+    trusted (the OS page size is assumed) and the file opens from meta 1
+    (ADVICE r02).  Page 0's checksum broken, then its page-size field
+    garbage as well: both open from page 1 (txid 1)."""
+    st, _ = _random_store(random.Random(2), 80)
+    p = tmp_path / "drand.db"
+    write_bolt(p, _kv(st))
+    raw = bytearray(p.read_bytes())
+    raw[16 + 40] ^= 1  # page 0's txid: checksum mismatch
+    p.write_bytes(bytes(raw))
+    bs = BoltStore(p)
+    assert bs.txid == 1 and bs.page_size == 4096 and bs.last() == st.last() and bs.len() == st.len()
+    bs.close()
+    raw[16 + 8:16 + 12] = struct.pack("<I", 123457)  # page 0's pageSize: garbage
+    p.write_bytes(bytes(raw))
+    bs = BoltStore(p)
+    assert bs.txid == 1 and bs.last() == st.last() and bs.len() == st.len()
+    bs.close()
+    # a 16 KiB-page file whose meta 0 is torn still opens (meta 1 at 16384)
+    q = tmp_path / "big.db"
+    write_bolt(q, _kv(st), page_size=16384)
+    raw = bytearray(q.read_bytes())
+    raw[16 + 40] ^= 1
+    q.write_bytes(bytes(raw))
+    bq = BoltStore(q)
+    assert bq.txid == 1 and bq.page_size == 16384 and bq.last() == st.last()
+    bq.close()

@@ -14,7 +14,8 @@ from conftest import load_golden
 from oracle import bls12381 as B
 from oracle import drand_ref as D
 
-FIXTURES = ["recover_t3_n8.json", "recover_t17_n32.json"]
+# t = 3, 12, 17, 32: every MSM table bucket of k_recover_msm_w4 (TMAX 8 / 16 / 24 / 32)
+FIXTURES = ["recover_t3_n8.json", "recover_t12_n20.json", "recover_t17_n32.json", "recover_t32_n40.json"]
 
 
 @pytest.mark.parametrize("name", FIXTURES)

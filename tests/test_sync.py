@@ -49,6 +49,18 @@ def test_hexjson_roundtrip():
     assert beacon_unmarshal(b'{"Round":7}') == Beacon(b"", 7, b"")
 
 
+@pytest.mark.parametrize("bad", ["ab cd", " abcd", "abcd ", "abc", "zz", "0xab", "ab\ncd", "١٢", "ab\tcd"])
+def test_hexjson_rejects_what_go_hex_rejects(bad):
+    """hexjson decodes []byte fields with Go's hex.DecodeString, which refuses
+    odd lengths and any non-hex byte (whitespace included) -- the row is an
+    Unmarshal error, so CheckPastBeacons counts it faulty."""
+    import json
+    for field in ("Signature", "PreviousSig"):
+        with pytest.raises(ValueError):
+            beacon_unmarshal(json.dumps({"Round": 3, field: bad}).encode())
+    assert beacon_unmarshal(b'{"Round":3,"Signature":"ABcd"}') == Beacon(b"", 3, b"\xab\xcd")
+
+
 @pytest.mark.parametrize("window", [1, 3, 16, 1 << 16])
 def test_check_past_beacons_matches_oracle(window):
     rng = random.Random(window)

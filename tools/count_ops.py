@@ -47,6 +47,31 @@ def main():
     h = [kernels[k] for k in ("k_h2c_field", "k_h2c_sswu", "k_h2c_finish")]
     # bench.py's stage "hash_to_g2" = the three hash kernels' launches summed
     kernels["hash_to_g2"] = {k: sum(x[k] for x in h) for k in ("fp_mul", "fp_sqr", "mads")}
+    # RLC mode (configs[2]) and the on-G1 schemes (configs[3]): per-round work
+    # of their stages (bench.py stage names), same host build of the device code
+    import hashlib
+    g1 = json.load(open(os.path.join(ROOT, "tests", "golden", "chain_on_g1_s1.json")))
+    msg = hashlib.sha256(bytes.fromhex(r["prev"]) + r["round"].to_bytes(8, "big")).digest()
+    xo = (ctypes.c_ulonglong * 16)()
+    rc = L.hs_count_extra(msg, bytes.fromhex(r["sig"]), bytes.fromhex(g1["rounds"][0]["sig"]),
+                          ctypes.c_uint64(0x9E3779B97F4A7C15), xo)
+    assert rc == 0, rc
+    part = {name: (xo[2 * i], xo[2 * i + 1]) for i, name in enumerate(
+        ["rlc_hash", "decode_sub", "leaf", "node", "g2_affine", "hash_g1", "decode_g1", "g1_affine"])}
+
+    def ent(*terms):
+        mul = sum(c * part[p][0] for c, p in terms)
+        sqr = sum(c * part[p][1] for c, p in terms)
+        return {"fp_mul": mul, "fp_sqr": sqr, "mads": MADS_MUL * mul + MADS_SQR * sqr}
+    # per round: the raw hash (no cofactor); decode with membership; two
+    # leaves (P and S trees) + the affine conversion of R + two tree nodes
+    kernels["rlc_hash_to_g2_raw"] = ent((1, "rlc_hash"))
+    kernels["k_decode_g2_sigs+subgroup"] = ent((1, "decode_sub"))
+    kernels["rlc_leaves_tree"] = ent((2, "leaf"), (1, "g2_affine"), (2, "node"))
+    kernels["k_hash_to_g1_beacons"] = ent((1, "hash_g1"))
+    kernels["k_g1_batch_affine"] = ent((1, "g1_affine"))
+    kernels["k_g2_batch_affine"] = ent((1, "g2_affine"))
+    kernels["k_decode_g1_sigs"] = ent((1, "decode_g1"))
     res = {"per_round_verify": {"fp_mul": tot_mul, "fp_sqr": tot_sqr, "stages": stages},
            "kernels": kernels,
            "unit": "per round; mads = v_mad_u64_u32 issued by the Fp multiplications (%d per mul, %d per sqr)"

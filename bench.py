@@ -11,7 +11,17 @@ SURVEY.md 8(e)); each rank verifies its shard, and the per-rank verdict
 bitmaps are all-gathered over RCCL (the one exchange step) inside the timed
 region, then checked against the construction.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rounds R]
+The default run also measures every other BASELINE.json configuration at its
+stated size, each with its own verdict check, roofline and CPU baseline:
+  rlc            configs[2]: RLC batch verify of the same resident chain
+  configs3       configs[3]: 10M-round pedersen-bls-unchained and
+                 bls-unchained-on-g1 chains, per-round verify
+  recover        configs[4]: threshold recovery, n=32, t=17, 100k rounds
+  multi_abi      the product multi-GPU boundary (dgpu_verify_multi: one
+                 process drives all N GPUs, host records, RCCL gathers), run
+                 in a child process while the ranks wait
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rounds R] [--no-legs]
+    python bench.py --driver abi [--gpus N]   # the value through dgpu_verify_multi
 
 With --gpus N > 1 and no torch.distributed environment, bench.py starts the
 N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) before
@@ -19,6 +29,7 @@ anything touches the GPU; under torch.distributed.run it is one rank.
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import subprocess
@@ -50,6 +61,9 @@ def parse(argv=None):
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (H2D-inclusive) pass")
     ap.add_argument("--no-rlc", action="store_true",
                     help="per-round mode: skip the RLC batch-verify pass over the same resident chain (configs[2])")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the configs[3] / configs[4] / multi_abi legs of the default run")
+    ap.add_argument("--leg-steps", type=int, default=2, help="timed steps of each extra leg")
     ap.add_argument("--mode", choices=["per-round", "rlc", "recover"], default="per-round",
                     help="per-round: configs[1] / the metric; rlc: configs[2] (random linear combination + "
                          "bisection); recover: configs[4] (t-of-n threshold recovery, n=32, t=17)")
@@ -61,6 +75,13 @@ def parse(argv=None):
                     choices=["pedersen-bls-chained", "pedersen-bls-unchained", "bls-unchained-on-g1",
                              "bls-unchained-g1-rfc9380"],
                     help="per-round/rlc modes: the chain's scheme (configs[3]: unchained and on-g1)")
+    ap.add_argument("--driver", choices=["dist", "abi"], default="dist",
+                    help="dist: one process per GPU over torch.distributed (RCCL); abi: one process, "
+                         "dgpu_verify_multi / dgpu_recover_multi over all GPUs (the Go caller's boundary)")
+    ap.add_argument("--abi-devices", default=None,
+                    help="abi driver: comma-separated device list (default 0..N-1; a repeated device needs "
+                         "DGPU_MULTI_ALLOW_SAME_DEVICE=1)")
+    ap.add_argument("--abi-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -88,38 +109,54 @@ def launch_ranks(args):
     return rc
 
 
+def _load_json(*parts):
+    p = os.path.join(ROOT, *parts)
+    if not os.path.exists(p):
+        return {}
+    with open(p) as f:
+        return json.load(f)
+
+
 def engine_work():
     """Exact per-item work of the pairing-engine kernels (tools/engine_work.py
     -> profiles/engine_work.json: product terms + reductions of the generated
     programs, x 196 v_mad_u64_u32 each)."""
-    p = os.path.join(ROOT, "profiles", "engine_work.json")
-    if not os.path.exists(p):
-        return {}
-    with open(p) as f:
-        return json.load(f)["kernels"]
+    return _load_json("profiles", "engine_work.json").get("kernels", {})
 
 
 def hash_work():
-    """Per-round v_mad_u64_u32 counts of the hash / decode kernels of the
-    chained per-round pipeline (tools/count_ops.py -> profiles/op_counts.json,
-    counted by the host build of the same device functions)."""
-    p = os.path.join(ROOT, "profiles", "op_counts.json")
-    if not os.path.exists(p):
-        return {}
-    with open(p) as f:
-        return json.load(f).get("kernels", {})
+    """Per-round v_mad_u64_u32 counts of the hash / decode / RLC / on-G1
+    kernels (tools/count_ops.py -> profiles/op_counts.json, counted by the host
+    build of the same device functions)."""
+    return _load_json("profiles", "op_counts.json").get("kernels", {})
 
 
-# stage name (dgpu_stage_times) -> kernel symbol
+# stage name (dgpu_stage_times) -> work key (profiles/*.json), per pipeline
+STAGE_WORK = {
+    "g2": {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
+           "hash_to_g2": "hash_to_g2", "decode_g2": "k_decode_g2_sigs", "h_affine": "k_g2_batch_affine"},
+    "g1": {"eng_miller": "k_eng_miller_fixed", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
+           "eng_lines_fixed": "k_eng_lines_fixed", "hash_to_g1": "k_hash_to_g1_beacons",
+           "decode_g1": "k_decode_g1_sigs", "h_affine": "k_g1_batch_affine"},
+    # RLC: the per-round stages only (node checks are data-dependent: 1 at 0% corruption)
+    "rlc": {"rlc_hash_to_g2_raw": "rlc_hash_to_g2_raw", "decode_g2": "k_decode_g2_sigs+subgroup",
+            "rlc_leaves_tree": "rlc_leaves_tree"},
+    # recovery: items = partials + rounds of engine checks
+    "recover": {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv",
+                "eng_fe": "k_eng_fe"},
+}
+# stage -> kernel symbol for the traffic lookup
 STAGE_KERNEL = {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
                 "eng_lines_fixed": "k_eng_lines_fixed", "hash_to_g2": "hash_to_g2", "decode_g2": "k_decode_g2_sigs",
-                "hash_to_g1": "k_hash_to_g1_beacons", "decode_g1": "k_decode_g1_sigs"}
+                "hash_to_g1": "k_hash_to_g1_beacons", "decode_g1": "k_decode_g1_sigs",
+                "rlc_leaves_tree": "k_rlc_leaves"}
 
 
 def traffic_for(kern, items):
-    """PMC FETCH_SIZE + WRITE_SIZE per item of this build (profiles/r02*_traffic.json)."""
+    """PMC FETCH_SIZE + WRITE_SIZE per item of this build (latest profiles/**/r0*_traffic.json)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "r02*_traffic.json"), recursive=True), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "r0*_traffic.json"), recursive=True),
+                       key=os.path.basename, reverse=True):
         with open(path) as f:
             t = json.load(f)["kernels"]
         key = next((k for k in t if k.split("::")[-1].split("(")[0] == kern), None)
@@ -129,33 +166,35 @@ def traffic_for(kern, items):
     return None, None
 
 
-def roofline_for(stage_ms, items):
-    """Roofline of the dominant kernel (largest summed launch time; chunked
-    stages are summed over their launches): achieved = algorithmic
-    v_mad_u64_u32 products over the launches / measured time (HIP events on
-    the launch stream) vs the measured int32 mad peak; traffic = PMC bytes of
-    this build over the same launches.  items = pairing checks per pass
-    (None when data-dependent, as in RLC)."""
-    if not stage_ms:
+def roofline_for(stage_ms, items, pipeline="g2", stage_items=None):
+    """Roofline of the dominant stage (largest summed launch time among the
+    stages with a work figure; chunked stages are summed over their
+    launches): achieved = algorithmic v_mad_u64_u32 products over the launches
+    / measured time (HIP events on the launch stream) vs the measured int32
+    mad peak; traffic = PMC bytes of this build over the same launches.
+    items = work items per pass (rounds, or pairing checks); stage_items
+    overrides it per stage."""
+    if not stage_ms or not items:
         return None
-    name = max(stage_ms, key=stage_ms.get)
-    ms = stage_ms[name]
-    kern = STAGE_KERNEL.get(name, name)
-    out = {"bound": "valu-int32", "unit": "T mad_u64_u32/s", "kernel": kern, "launch_ms_total": ms,
-           "items": items, "peak": PEAK_MAD_U64_PER_S / 1e12, "achieved": None, "frac": None, "traffic": None}
-    if not items:
-        return out
+    wmap = STAGE_WORK[pipeline]
     work = dict(hash_work(), **engine_work())
-    if kern in work:
-        per_item = work[kern]["mads"]
-        achieved = items * per_item / (ms * 1e-3)
-        out.update(achieved=achieved / 1e12, frac=achieved / PEAK_MAD_U64_PER_S, work_per_item_mads=per_item,
-                   work_source="profiles/engine_work.json" if kern in engine_work() else "profiles/op_counts.json")
-    # the same fraction for every stage that has a work figure (hash and decode
-    # from profiles/op_counts.json, the engine from profiles/engine_work.json)
-    out["stage_frac"] = {s: items * work[STAGE_KERNEL.get(s, s)]["mads"] / (t * 1e-3) / PEAK_MAD_U64_PER_S
-                         for s, t in stage_ms.items() if STAGE_KERNEL.get(s, s) in work and t > 0}
-    traffic, src = traffic_for(kern, items)
+    have = {s: t for s, t in stage_ms.items() if s in wmap and wmap[s] in work and t > 0}
+    if not have:
+        return None
+    stage_items = stage_items or {}
+    name = max(have, key=have.get)
+    ms = have[name]
+    key = wmap[name]
+    it = stage_items.get(name, items)
+    per_item = work[key]["mads"]
+    achieved = it * per_item / (ms * 1e-3)
+    out = {"bound": "valu-int32", "unit": "T mad_u64_u32/s", "kernel": key, "stage": name, "launch_ms_total": ms,
+           "items": it, "peak": PEAK_MAD_U64_PER_S / 1e12, "achieved": achieved / 1e12,
+           "frac": achieved / PEAK_MAD_U64_PER_S, "traffic": None, "work_per_item_mads": per_item,
+           "work_source": "profiles/engine_work.json" if key in engine_work() else "profiles/op_counts.json"}
+    out["stage_frac"] = {s: stage_items.get(s, items) * work[wmap[s]]["mads"] / (t * 1e-3) / PEAK_MAD_U64_PER_S
+                         for s, t in have.items()}
+    traffic, src = traffic_for(STAGE_KERNEL.get(name, key), it)
     if traffic is not None:
         out["traffic"] = traffic
         out["traffic_unit"] = "bytes over the launches (PMC FETCH_SIZE+WRITE_SIZE, %s)" % src
@@ -198,29 +237,34 @@ def timed(step, steps, world, dev, after=None):
     return float(t.item()), res
 
 
-def shard_chain(args, code, n_total, lo, hi, device):
+def shard_chain(seed, seg, code, lo, hi, device):
     """This rank's rounds [lo + 1, hi] of the global chain: whole seg_len
     segments are generated (segment s covers rounds s*seg_len + 1 ..; its seed
     depends only on s), so every rank sees the same chain whatever N is."""
     from drand_amd.synth import make_chain
-    seg = args.seg_len
     s0 = lo // seg
     s1 = (hi + seg - 1) // seg
-    ch = make_chain(args.seed, (s1 - s0) * seg, code, seg_len=seg, device=device, start_round=s0 * seg + 1)
+    ch = make_chain(seed, (s1 - s0) * seg, code, seg_len=seg, device=device, start_round=s0 * seg + 1)
     a, b = lo - s0 * seg, hi - s0 * seg
     for name in ("rounds", "sigs", "sig_len", "prev", "prev_len"):
         setattr(ch, name, np.ascontiguousarray(getattr(ch, name)[a:b]))
     return ch
 
 
-def main_recover(args, world, rank, local):
+def cpu_threads():
+    """cpu_baseline threads: every core this process may run on (GOMAXPROCS =
+    the host's cores, as north_star asks; host and cgroup views are reported)."""
+    return len(os.sched_getaffinity(0))
+
+
+# ---------------------------------------------------------------- configs[4]
+def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
     """configs[4]: batch threshold recovery (kyber tbls.Recover as the
     aggregator calls it, chain/beacon/chain.go:158-168): per round t partials
-    (one invalid in --bad-rate of the rounds), VerifyPartial of each on the
-    pairing engine, selection + Lagrange + G2 MSM, VerifyRecovered.  Inputs
-    resident in HBM (dgpu_recover_batch_device).  The --rounds batch is split
-    into contiguous round shards (strong scaling); each rank checks its own
-    outputs."""
+    (one invalid in --bad-rate of the rounds), VerifyPartial, selection +
+    Lagrange + G2 MSM, VerifyRecovered.  Inputs resident in HBM
+    (dgpu_recover_batch_device).  The batch is split into contiguous round
+    shards (strong scaling); each rank checks its own outputs."""
     import torch
     import torch.distributed as dist
     from drand_amd import _lib
@@ -228,7 +272,6 @@ def main_recover(args, world, rank, local):
     from drand_amd.dist import shard_range
     from drand_amd.synth import group_signatures, make_group, make_recovery_batch
 
-    n_total = args.rounds or 100_000
     lo, hi = shard_range(n_total, world, rank)
     n = hi - lo
     dev = torch.device("cuda", local)
@@ -238,6 +281,7 @@ def main_recover(args, world, rank, local):
                                                  first_round=lo + 1, device=local)
     expect = group_signatures(grp, msgs, device=local)
     t_gen = time.time() - t_gen
+    log(f"recover: {n} rounds generated in {t_gen:.1f} s")
     ctx = get_context(local)
     lib = ctx.lib
     cbuf = np.frombuffer(b"".join(grp.commits), dtype=np.uint8).copy()
@@ -255,11 +299,11 @@ def main_recover(args, world, rank, local):
                                                  d_plen.data_ptr(), d_out.data_ptr(), d_ok.data_ptr(), None,
                                                  ctypes.c_void_p(stream.cuda_stream)))
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     stage_ms = stage_times(lib, ctx, step)
-    elapsed, _ = timed(step, args.steps, world, dev)
+    elapsed, _ = timed(step, steps, world, dev)
 
     ok = d_ok.cpu().numpy().astype(bool)
     out = d_out.cpu().numpy()
@@ -267,49 +311,54 @@ def main_recover(args, world, rank, local):
     mism_t = torch.tensor([mism], device=dev)
     if world > 1:
         dist.all_reduce(mism_t)
+    res = {"metric": "recovered beacon rounds/sec, t-of-n threshold recovery (VerifyPartial x t, Lagrange, "
+                     "G2 MSM, VerifyRecovered)",
+           "value": n_total * steps / elapsed, "unit": "rounds/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+           "ms_per_step": elapsed / steps * 1e3, "higher_is_better": True, "scaling": "strong",
+           "dtype": "u32 (14x28-bit limb Fp, 10x28-bit limb Fr, int32 VALU)",
+           "data": f"synthetic {args.t}-of-{args.n} group and partials generated on GPU (seeded), "
+                   f"{args.bad_rate:.0%} of rounds with one invalid partial",
+           "config": {"workload": "configs[4]: threshold recovery, n=%d, t=%d" % (args.n, args.t),
+                      "rounds_total": n_total, "rounds_per_gpu": n, "partials_per_round": m, "mode": "recover",
+                      "parallelism": f"shard{world}"},
+           "stage_ms": stage_ms, "verdict_mismatches": int(mism_t.item()),
+           "unrecoverable_rounds_rank0": int((~expect_ok).sum()), "gen_s": t_gen}
     if rank == 0:
-        items = n * m
-        roof = roofline_for({k: v for k, v in stage_ms.items() if k.startswith("eng_")}, items + n)
+        res["roofline"] = roofline_for(stage_ms, n * (m + 1), "recover")
+        if res["roofline"]:
+            res["roofline"]["items_note"] = "pairing checks per pass (engine items)"
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
                 from oracle import cpu_baseline as cb
                 exp_sigs = [bytes(expect[i]) if expect_ok[i] else None for i in range(n)]
-                cpu = cb.run_recover(grp.commits, grp.t, grp.n, msgs, parts, exp_sigs, args.cpu_seconds,
-                                     min(16, os.cpu_count() or 1))
+                cpu = cb.run_recover(grp.commits, grp.t, grp.n, msgs, parts, exp_sigs, cpu_seconds, cpu_threads())
             except Exception as e:  # reported, never fatal
                 cpu = {"error": repr(e)}
-        print(json.dumps({
-            "metric": "recovered beacon rounds/sec, t-of-n threshold recovery (VerifyPartial x t, Lagrange, "
-                      "G2 MSM, VerifyRecovered)",
-            "value": n_total * args.steps / elapsed, "unit": "rounds/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u32 (14x28-bit limb Fp, 10x28-bit limb Fr, int32 VALU)",
-            "data": f"synthetic {args.t}-of-{args.n} group and partials generated on GPU (seeded), "
-                    f"{args.bad_rate:.0%} of rounds with one invalid partial",
-            "config": {"workload": "configs[4]: threshold recovery, n=%d, t=%d" % (args.n, args.t),
-                       "rounds_total": n_total, "rounds_per_gpu": n, "partials_per_round": m,
-                       "pairings_per_round": m + 1, "mode": "recover", "parallelism": f"shard{world}"},
-            "stage_ms": stage_ms, "verdict_mismatches": int(mism_t.item()),
-            "unrecoverable_rounds_rank0": int((~expect_ok).sum()), "gen_s": t_gen,
-            "roofline": roof, "cpu_baseline": cpu}))
+        res["cpu_baseline"] = cpu
+    del d_msgs, d_parts, d_plen, d_out, d_ok
+    return res
 
 
-def main_verify(args, world, rank, local):
+# ---------------------------------------------------------------- configs[1..3]
+def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="per-round", e2e=False, rlc=False,
+               cpu_seconds=None, main=False):
+    """One chain of `scheme`, n_total rounds sharded over the ranks, verified
+    `steps` times with inputs resident in HBM (dgpu_verify_beacons_device),
+    verdicts all-gathered (RCCL) and checked against the construction; plus
+    optionally the host-record pass (e2e) and the RLC pass over the same chain."""
     import torch
-    import torch.distributed as dist
     from drand_amd import _lib
     from drand_amd.chain import get_context
     from drand_amd.dist import gather_verdict_bits, shard_range
     from drand_amd.synth import corrupt_global
 
-    n_total = args.rounds or 10_000_000
     lo, hi = shard_range(n_total, world, rank)
     n = hi - lo
-    code = _lib.load().dgpu_scheme_from_name(args.scheme.encode())
+    code = _lib.load().dgpu_scheme_from_name(scheme.encode())
     t_gen = time.time()
-    log(f"generating rounds [{lo + 1}, {hi}] of a {n_total}-round {args.scheme} chain")
-    chain = shard_chain(args, code, n_total, lo, hi, local)
+    log(f"generating rounds [{lo + 1}, {hi}] of a {n_total}-round {scheme} chain")
+    chain = shard_chain(args.seed, args.seg_len, code, lo, hi, local)
     bad = corrupt_global(chain, args.seed, n_total, lo, rate=args.corrupt_rate)
     t_gen = time.time() - t_gen
     log(f"chain ready in {t_gen:.1f} s")
@@ -325,117 +374,242 @@ def main_verify(args, world, rank, local):
     lib = ctx.lib
     pk = np.frombuffer(chain.pk, dtype=np.uint8).copy()
     stream = torch.cuda.current_stream(dev)
-    mode = _lib.MODE_RLC if args.mode == "rlc" else _lib.MODE_PER_ROUND
+    mcode = _lib.MODE_RLC if mode == "rlc" else _lib.MODE_PER_ROUND
     seed = args.rlc_seed + 7 * rank
 
-    def step():
+    def step_mode(md, sd):
         _lib.check(lib.dgpu_verify_beacons_device(
             ctx.handle, code, _lib.ptr(pk), pk.size, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96,
-            d_sig_len.data_ptr(), d_prev.data_ptr(), 96, d_prev_len.data_ptr(), mode, seed, d_bits.data_ptr(),
+            d_sig_len.data_ptr(), d_prev.data_ptr(), 96, d_prev_len.data_ptr(), md, sd, d_bits.data_ptr(),
             None, ctypes.c_void_p(stream.cuda_stream)))
 
-    for _ in range(args.warmup):
+    step = lambda: step_mode(mcode, seed)  # noqa: E731
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    log("warmup done")
+    log(f"{scheme} warmup done")
     # per-stage kernel timing (HIP events on the launch stream), single lane;
     # the first of the two passes absorbs the single-lane buffer growth
-    stage_ms = stage_times(lib, ctx, step, passes=2)
+    stage_ms = stage_times(lib, ctx, step, passes=2 if main else 1)
     log("stage times", json.dumps(stage_ms))
-
     # the exchange step: every rank's verdict bitmap to every rank (RCCL)
-    elapsed, verdicts = timed(step, args.steps, world, dev,
+    elapsed, verdicts = timed(step, steps, world, dev,
                               after=lambda: gather_verdict_bits(d_bits, n, n_total, world, rank))
-
-    log(f"timed: {args.steps} steps in {elapsed:.3f} s")
-    # verdicts vs construction (the corruption catalog is global, seeded)
+    log(f"{scheme}: {steps} steps in {elapsed:.3f} s")
     expect = np.ones(n_total, dtype=bool)
     expect[list(bad.keys())] = False
-    mism = int((verdicts != expect).sum())
+    res = {"value": n_total * steps / elapsed, "unit": "rounds/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": elapsed / steps * 1e3, "stage_ms": stage_ms,
+           "verdict_mismatches": int((verdicts != expect).sum()), "corrupted_rounds_total": len(bad),
+           "chain_gen_s": t_gen, "scheme": scheme, "rounds_total": n_total, "rounds_per_gpu": n}
+    g1 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
+    pipeline = "rlc" if mode == "rlc" else ("g1" if g1 else "g2")
+    if rank == 0:
+        res["roofline"] = roofline_for(stage_ms, n, pipeline)
 
-    # end to end: host records through dgpu_verify_beacons (H2D + D2H inside)
-    e2e = None
-    if not args.no_e2e:
+    if e2e:  # host records through dgpu_verify_beacons (H2D + D2H inside)
         h_bits = np.zeros((n + 7) // 8, dtype=np.uint8)
 
         def step_host():
             _lib.check(lib.dgpu_verify_beacons(
                 ctx.handle, code, _lib.ptr(pk), pk.size, n, _lib.ptr(chain.rounds), _lib.ptr(chain.sigs), 96,
-                _lib.ptr(chain.sig_len), _lib.ptr(chain.prev), 96, _lib.ptr(chain.prev_len), mode, seed,
+                _lib.ptr(chain.sig_len), _lib.ptr(chain.prev), 96, _lib.ptr(chain.prev_len), mcode, seed,
                 _lib.ptr(h_bits), None))
 
-        e2e_steps = max(1, min(args.steps, 2))
+        e2e_steps = max(1, min(steps, 2))
         t_host, _ = timed(step_host, e2e_steps, world, dev)
         host_ok = np.unpackbits(h_bits, bitorder="little")[:n].astype(bool)
-        e2e = {"value": n_total * e2e_steps / t_host, "unit": "rounds/s", "ms_per_step": t_host / e2e_steps * 1e3,
-               "steps": e2e_steps, "api": "dgpu_verify_beacons (pageable host records: H2D, verify, D2H)",
-               "verdicts_equal_device_path": bool(np.array_equal(host_ok, verdicts[lo:hi]))}
+        res["end_to_end"] = {"value": n_total * e2e_steps / t_host, "unit": "rounds/s",
+                             "ms_per_step": t_host / e2e_steps * 1e3, "steps": e2e_steps,
+                             "api": "dgpu_verify_beacons (pageable host records: H2D, verify, D2H)",
+                             "verdicts_equal_device_path": bool(np.array_equal(host_ok, verdicts[lo:hi]))}
 
     # configs[2] beside the metric: RLC batch verification (one multi-Miller
     # loop + one final exponentiation per checked node, root first, exact
     # per-round verdicts by bisection) over the same resident chain
-    rlc = None
-    if args.mode == "per-round" and not args.no_rlc and code in (_lib.SCHEME_CHAINED, _lib.SCHEME_UNCHAINED):
-        def step_rlc():
-            _lib.check(lib.dgpu_verify_beacons_device(
-                ctx.handle, code, _lib.ptr(pk), pk.size, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96,
-                d_sig_len.data_ptr(), d_prev.data_ptr(), 96, d_prev_len.data_ptr(), _lib.MODE_RLC, seed + 1,
-                d_bits.data_ptr(), None, ctypes.c_void_p(stream.cuda_stream)))
-
+    if rlc and mode == "per-round" and not g1:
+        step_rlc = lambda: step_mode(_lib.MODE_RLC, seed + 1)  # noqa: E731
         step_rlc()
         rlc_ms = stage_times(lib, ctx, step_rlc)
-        rlc_steps = max(1, min(args.steps, 3))
+        rlc_steps = max(1, min(steps, 3))
         t_rlc, v_rlc = timed(step_rlc, rlc_steps, world, dev,
                              after=lambda: gather_verdict_bits(d_bits, n, n_total, world, rank))
-        rlc = {"value": n_total * rlc_steps / t_rlc, "unit": "rounds/s", "ms_per_step": t_rlc / rlc_steps * 1e3,
-               "steps": rlc_steps, "verdict_mismatches": int((v_rlc != expect).sum()), "stage_ms": rlc_ms,
-               "workload": "configs[2] on the same chain: RLC batch verify, root first, per-round verdicts by "
-                           "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)"}
-        log(f"rlc: {rlc['value']:.0f} rounds/s")
+        res["rlc"] = {"value": n_total * rlc_steps / t_rlc, "unit": "rounds/s", "ms_per_step": t_rlc / rlc_steps * 1e3,
+                      "steps": rlc_steps, "verdict_mismatches": int((v_rlc != expect).sum()), "stage_ms": rlc_ms,
+                      "roofline": roofline_for(rlc_ms, n, "rlc") if rank == 0 else None,
+                      "workload": "configs[2] on the same chain: RLC batch verify, root first, per-round verdicts by "
+                                  "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)"}
+        log(f"rlc: {res['rlc']['value']:.0f} rounds/s")
 
+    if rank == 0 and cpu_seconds and not args.no_cpu_baseline and world == 1:
+        try:
+            from oracle import cpu_baseline as cb
+            res["cpu_baseline"] = cb.run(chain, cpu_seconds, cpu_threads(), expect[lo:hi])
+        except Exception as e:  # reported, never fatal
+            res["cpu_baseline"] = {"error": repr(e)}
+        log("cpu baseline done")
+    del d_rounds, d_sigs, d_sig_len, d_prev, d_prev_len, d_bits, chain
+    gc.collect()
+    torch.cuda.empty_cache()
+    return res
+
+
+# ---------------------------------------------------------------- the product multi-GPU boundary
+def abi_devices(args, ngpu):
+    if args.abi_devices:
+        return [int(x) for x in args.abi_devices.split(",")]
+    return list(range(ngpu))
+
+
+def main_abi(args):
+    """One process drives every GPU through the C ABI as a Go caller of
+    crypto/gpu would: dgpu_verify_multi over host records
+    (per-device staging, verify, RCCL all-gather of the verdict bitmaps), and
+    dgpu_recover_multi for --mode recover.  No torch in this process."""
+    from drand_amd import _lib
+    from drand_amd.multi import MultiThresholdGroup, MultiVerifier
+    from drand_amd.scheme import get_scheme_by_id_with_default
+    from drand_amd.synth import corrupt_global, group_signatures, make_chain, make_group, make_recovery_batch
+    devs = abi_devices(args, args.gpus)
+    mctx = _lib.MultiContext(devs)
+    wall = lambda: time.perf_counter()  # noqa: E731
+    if args.mode == "recover":
+        n_total = args.rounds or 100_000
+        grp = make_group(args.seed, args.t, args.n, device=devs[0])
+        msgs, parts, expect_ok = make_recovery_batch(grp, n_total, args.seed, args.bad_rate, device=devs[0])
+        expect = group_signatures(grp, msgs, device=devs[0])
+        mg = MultiThresholdGroup(grp.commits, grp.n, mctx=mctx)
+        nr, m = parts.shape[:2]
+        mb = np.ascontiguousarray(msgs).reshape(-1)
+        plen = np.full((nr, m), 98, dtype=np.uint32)
+        run = lambda: mg.recover_records(mb, parts, plen)  # noqa: E731
+        for _ in range(args.warmup):
+            run()
+        t0 = wall()
+        for _ in range(args.steps):
+            sigs, _ = run()
+        el = wall() - t0
+        okv = np.array([s is not None for s in sigs])
+        mism = int((okv != expect_ok).sum()) + sum(1 for i, s in enumerate(sigs) if s is not None and expect_ok[i]
+                                                  and s != bytes(expect[i]))
+        res = {"value": n_total * args.steps / el, "unit": "rounds/s", "ms_per_step": el / args.steps * 1e3,
+               "rounds_total": n_total, "verdict_mismatches": mism, "workload": "configs[4] through dgpu_recover_multi"}
+    else:
+        n_total = args.rounds or 10_000_000
+        code = _lib.load().dgpu_scheme_from_name(args.scheme.encode())
+        t_gen = wall()
+        chain = make_chain(args.seed, n_total, code, seg_len=args.seg_len, device=devs[0])
+        bad = corrupt_global(chain, args.seed, n_total, 0, rate=args.corrupt_rate)
+        t_gen = wall() - t_gen
+        log(f"abi: {n_total}-round chain in {t_gen:.1f} s")
+        mv = MultiVerifier(get_scheme_by_id_with_default(args.scheme), mctx=mctx)
+        mcode = _lib.MODE_RLC if args.mode == "rlc" else _lib.MODE_PER_ROUND
+        run = lambda: mv.verify_records(chain.pk, chain.rounds, chain.sigs, chain.sig_len, chain.prev,  # noqa: E731
+                                        chain.prev_len, mcode, args.rlc_seed)
+        for _ in range(args.warmup):
+            run()
+        t0 = wall()
+        for _ in range(args.steps):
+            reason = run()
+        el = wall() - t0
+        expect = np.ones(n_total, dtype=bool)
+        expect[list(bad.keys())] = False
+        res = {"value": n_total * args.steps / el, "unit": "rounds/s", "ms_per_step": el / args.steps * 1e3,
+               "rounds_total": n_total, "verdict_mismatches": int(((reason == 0) != expect).sum()),
+               "chain_gen_s": t_gen, "scheme": args.scheme, "mode": args.mode,
+               "workload": "dgpu_verify_multi over host records (per-device H2D staging, verify, RCCL verdict "
+                           "all-gather, D2H)"}
+    res.update({"n_gpus": len(devs), "devices": devs, "steps": args.steps, "warmup": args.warmup,
+                "driver": "abi (one process, libdrand_gpu.so multi-GPU handle)",
+                "gather": "in-library device copies (DGPU_MULTI_ALLOW_SAME_DEVICE)" if os.environ.get(
+                    "DGPU_MULTI_ALLOW_SAME_DEVICE") == "1" else "RCCL ncclAllGather"})
+    mctx.close()
+    return res
+
+
+def multi_abi_leg(args, world, rank):
+    """The abi driver in a child process (this rank's GPU state stays as is;
+    the other ranks wait on a CPU barrier), bounded by a timeout: reported
+    beside the main line, never fatal."""
+    n_total = args.rounds or 10_000_000
+    cmd = [sys.executable, os.path.abspath(__file__), "--abi-child", "--gpus", str(world), "--rounds", str(n_total),
+           "--steps", str(args.leg_steps), "--warmup", "1", "--seed", str(args.seed)]
+    log("multi_abi: " + " ".join(cmd[2:]))
+    try:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300, text=True)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode != 0 or not lines:
+            return {"error": f"rc {p.returncode}", "stderr_tail": p.stderr[-800:]}
+        return json.loads(lines[-1])
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout (300 s)"}
+
+
+# ---------------------------------------------------------------- main
+def main_verify(args, world, rank, local):
+    import torch.distributed as dist
+    n_total = args.rounds or 10_000_000
+    main = verify_leg(args, world, rank, local, args.scheme, n_total, args.steps, args.warmup, mode=args.mode,
+                      e2e=not args.no_e2e, rlc=not args.no_rlc, cpu_seconds=args.cpu_seconds, main=True)
+    legs = {}
+    default_run = args.mode == "per-round" and args.scheme == "pedersen-bls-chained" and not args.no_legs
+    if default_run:
+        # configs[3]: the two unchained schemes at their stated size
+        legs["configs3"] = {}
+        for sch in ("pedersen-bls-unchained", "bls-unchained-on-g1"):
+            legs["configs3"][sch] = verify_leg(args, world, rank, local, sch, n_total, args.leg_steps, 1,
+                                               cpu_seconds=args.cpu_seconds / 2)
+        # configs[4]: threshold recovery at its stated shape
+        legs["recover"] = recover_leg(args, world, rank, local, 100_000, max(args.leg_steps, 3), 1,
+                                      args.cpu_seconds / 2)
+        # the product multi-GPU boundary over all ranks' GPUs, in a child process
+        gl = dist.new_group(backend="gloo") if world > 1 else None
+        if rank == 0:
+            legs["multi_abi"] = multi_abi_leg(args, world, rank)
+        if gl is not None:
+            dist.barrier(group=gl)
+    if rank != 0:
+        return
+    chained = args.scheme == "pedersen-bls-chained"
+    nm = f"{n_total / 1e6:g}M"
+    out = {
+        "metric": (f"verified beacon rounds/sec, {nm}-round chained BLS12-381 chain" if chained
+                   else f"verified beacon rounds/sec, {nm}-round {args.scheme} chain"),
+        "value": main["value"],
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": main["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32 (14x28-bit limb Fp, int32 VALU)",
+        "data": f"synthetic {args.scheme} chain generated on GPU (seeded), {args.corrupt_rate:.1%} corrupted",
+        "config": {"workload": ("configs[1] shape at the metric's size: chained G2 chain, per-round pairing "
+                                "verify" if chained and args.mode == "per-round"
+                                else "configs[2]: chained G2 chain, RLC batch verify + bisection"
+                                if args.mode == "rlc" else f"configs[3]: {args.scheme} chain, per-round verify"),
+                   "rounds_total": n_total, "rounds_per_gpu": main["rounds_per_gpu"], "seg_len": args.seg_len,
+                   "scheme": args.scheme, "mode": args.mode, "parallelism": f"shard{world}"},
+        "stage_ms": main["stage_ms"],
+        "verdict_mismatches": main["verdict_mismatches"],
+        "corrupted_rounds_total": main["corrupted_rounds_total"],
+        "chain_gen_s": main["chain_gen_s"],
+        "end_to_end": main.get("end_to_end"),
+        "rlc": main.get("rlc"),
+        "roofline": main.get("roofline"),
+        "cpu_baseline": main.get("cpu_baseline"),
+    }
+    out.update(legs)
+    print(json.dumps(out), flush=True)
+
+
+def main_recover(args, world, rank, local):
+    res = recover_leg(args, world, rank, local, args.rounds or 100_000, args.steps, args.warmup, args.cpu_seconds)
     if rank == 0:
-        value = n_total * args.steps / elapsed
-        roofline = roofline_for(stage_ms, n if args.mode == "per-round" else None)
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            try:
-                from oracle import cpu_baseline as cb
-                cpu = cb.run(chain, args.cpu_seconds, min(16, os.cpu_count() or 1), expect[lo:hi])
-            except Exception as e:  # reported, never fatal
-                cpu = {"error": repr(e)}
-        log("cpu baseline done" if cpu else "no cpu baseline")
-        chained = code == _lib.SCHEME_CHAINED
-        nm = f"{n_total / 1e6:g}M"
-        out = {
-            "metric": (f"verified beacon rounds/sec, {nm}-round chained BLS12-381 chain" if chained
-                       else f"verified beacon rounds/sec, {nm}-round {args.scheme} chain"),
-            "value": value,
-            "unit": "rounds/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "u32 (14x28-bit limb Fp, int32 VALU)",
-            "data": f"synthetic {args.scheme} chain generated on GPU (seeded), {args.corrupt_rate:.1%} corrupted",
-            "config": {"workload": ("configs[1] shape at the metric's size: chained G2 chain, per-round pairing "
-                                    "verify" if chained and args.mode == "per-round"
-                                    else "configs[2]: chained G2 chain, RLC batch verify + bisection"
-                                    if args.mode == "rlc" else f"configs[3]: {args.scheme} chain, per-round verify"),
-                       "rounds_total": n_total, "rounds_per_gpu": n, "seg_len": args.seg_len, "scheme": args.scheme,
-                       "mode": args.mode, "parallelism": f"shard{world}"},
-            "stage_ms": stage_ms,
-            "verdict_mismatches": mism,
-            "corrupted_rounds_total": len(bad),
-            "chain_gen_s": t_gen,
-            "end_to_end": e2e,
-            "rlc": rlc,
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
+        res["vs_baseline"] = None
+        print(json.dumps(res), flush=True)
 
 
 def dryrun(args):
@@ -461,6 +635,14 @@ def dryrun(args):
 
 def main():
     args = parse()
+    if args.abi_child or (args.driver == "abi" and "WORLD_SIZE" not in os.environ):
+        # one process over all GPUs (never under a rank launcher)
+        res = main_abi(args)
+        if not args.abi_child:
+            res.update({"metric": "verified beacon rounds/sec through dgpu_verify_multi", "higher_is_better": True,
+                        "scaling": "strong", "vs_baseline": None})
+        print(json.dumps(res), flush=True)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     if os.environ.get("DRAND_BENCH_DRYRUN"):

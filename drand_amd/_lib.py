@@ -72,6 +72,8 @@ SYMBOLS = [
     ("dgpu_multi_context", _c.c_int, [_P, _c.c_int, _c.POINTER(_P)]),
     ("dgpu_verify_multi", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P,
                                      _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P]),
+    ("dgpu_multi_set_group", _c.c_int, [_P, _c.c_int, _c.c_int, _P]),
+    ("dgpu_recover_multi", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P]),
 ]
 
 ABI_VERSION = 2

@@ -434,6 +434,18 @@ __global__ void k_pack_verdicts(size_t n, const uint8_t* __restrict__ status, ui
   bits[j] = b;
 }
 
+// nonzero bytes -> bitmap (bit = 1 where ok[i] != 0): recovery verdicts
+__global__ void k_pack_ok(size_t n, const uint8_t* __restrict__ ok, uint8_t* __restrict__ bits) {
+  size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j * 8 >= n) return;
+  uint8_t b = 0;
+  for (int k = 0; k < 8; ++k) {
+    size_t i = j * 8 + k;
+    if (i < n && ok[i]) b |= (uint8_t)(1u << k);
+  }
+  bits[j] = b;
+}
+
 // Public key decode (48-byte compressed G1, kilic G1.FromCompressed (R)) on one thread.
 __global__ void k_decode_g1_pk(const uint8_t* __restrict__ in48, uint32_t* __restrict__ out, int* __restrict__ rc) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;

@@ -17,6 +17,14 @@
 //    verdicts, and the bitmaps are gathered as in per-round mode.
 // RCCL is loaded at dgpu_multi_open (dlopen), so the single-GPU library has
 // no link-time dependency on it.
+//
+// Test mode: with DGPU_MULTI_ALLOW_SAME_DEVICE=1 in the environment a handle
+// may list one device several times (devs = {0, 0, 0}: one context each, own
+// streams and buffers) and its all-gathers are in-library device copies
+// ordered by events instead of RCCL (a communicator cannot hold one device
+// twice).  Everything else -- shard bookkeeping, per-device seeds, root sum
+// and check on the first context, short / empty shard padding -- is the
+// production code path, so a one-GPU box executes the D >= 2 branches.
 
 namespace {
 
@@ -76,6 +84,8 @@ struct dgpu_multi {
   std::vector<multi_bufs> buf;
   rccl_api api;
   std::mutex mu;
+  bool loopback = false;          // DGPU_MULTI_ALLOW_SAME_DEVICE=1: device copies instead of RCCL (tests)
+  std::vector<hipEvent_t> gev;    // loopback: per-device "source ready" events
 };
 
 extern "C" {
@@ -83,11 +93,14 @@ extern "C" {
 int dgpu_multi_open(int ndev, const int* devs, dgpu_multi** out) {
   if (!out || !devs || ndev < 1) return set_err(DGPU_EINVAL, "bad arguments");
   *out = nullptr;
-  for (int i = 0; i < ndev; ++i)
+  const char* same = getenv("DGPU_MULTI_ALLOW_SAME_DEVICE");
+  const bool loopback = same && !strcmp(same, "1");
+  for (int i = 0; i < ndev && !loopback; ++i)
     for (int j = 0; j < i; ++j)
       if (devs[i] == devs[j]) return set_err(DGPU_EINVAL, "device %d listed twice", devs[i]);
   dgpu_multi* m = new dgpu_multi();
-  int rc = load_rccl(m->api);
+  m->loopback = loopback;
+  int rc = loopback ? DGPU_OK : load_rccl(m->api);
   if (rc) {
     delete m;
     return rc;
@@ -103,6 +116,18 @@ int dgpu_multi_open(int ndev, const int* devs, dgpu_multi** out) {
       return set_err(rc, "%s", msg.c_str());
     }
     m->ctx.push_back(c);
+  }
+  if (loopback) {
+    m->gev.assign(ndev, nullptr);
+    for (int i = 0; i < ndev; ++i) {
+      hipSetDevice(devs[i]);
+      if (hipEventCreateWithFlags(&m->gev[i], hipEventDisableTiming) != hipSuccess) {
+        dgpu_multi_close(m);
+        return set_err(DGPU_EDEVICE, "hipEventCreate failed");
+      }
+    }
+    *out = m;
+    return DGPU_OK;
   }
   m->comm.resize(ndev);
   ncclResult_t r = m->api.comm_init_all(m->comm.data(), ndev, devs);
@@ -125,6 +150,7 @@ void dgpu_multi_close(dgpu_multi* m) {
     for (DevBuf* b : {&m->buf[i].bits, &m->buf[i].reasons, &m->buf[i].all_bits, &m->buf[i].all_reasons,
                       &m->buf[i].root, &m->buf[i].all_roots})
       b->release();
+    if (i < m->gev.size() && m->gev[i]) hipEventDestroy(m->gev[i]);
     dgpu_close(m->ctx[i]);
   }
   delete m;
@@ -160,6 +186,34 @@ int for_each_device(dgpu_multi* m, Fn&& fn) {
   for (auto& t : th) t.join();
   for (int k = 0; k < m->ndev; ++k)
     if (rcs[k]) return set_err(rcs[k], "device %d: %s", m->devs[k], errs[k].c_str());
+  return DGPU_OK;
+}
+
+// One all-gather per device of `bytes` bytes: dst[k] + j * bytes <- src[j]
+// for every j, enqueued on each device's stream.  RCCL (one group) or, in
+// loopback mode, device copies ordered after every source stream's event.
+int multi_all_gather(dgpu_multi* m, const std::vector<const void*>& src, const std::vector<void*>& dst,
+                     size_t bytes) {
+  const int D = m->ndev;
+  if (!m->loopback) {
+    NCCL_TRY(m->api, m->api.group_start());
+    for (int k = 0; k < D; ++k)
+      NCCL_TRY(m->api, m->api.all_gather(src[k], dst[k], bytes, ncclUint8, m->comm[k], m->ctx[k]->stream));
+    NCCL_TRY(m->api, m->api.group_end());
+    return DGPU_OK;
+  }
+  for (int j = 0; j < D; ++j) {
+    HIP_TRY(hipSetDevice(m->devs[j]));
+    HIP_TRY(hipEventRecord(m->gev[j], m->ctx[j]->stream));
+  }
+  for (int k = 0; k < D; ++k) {
+    HIP_TRY(hipSetDevice(m->devs[k]));
+    for (int j = 0; j < D; ++j) {
+      HIP_TRY(hipStreamWaitEvent(m->ctx[k]->stream, m->gev[j], 0));
+      HIP_TRY(hipMemcpyAsync((uint8_t*)dst[k] + (size_t)j * bytes, src[j], bytes, hipMemcpyDeviceToDevice,
+                             m->ctx[k]->stream));
+    }
+  }
   return DGPU_OK;
 }
 
@@ -252,11 +306,13 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
                                  c->stream));
         }
       }
-      NCCL_TRY(m->api, m->api.group_start());
-      for (int k = 0; k < D; ++k)
-        NCCL_TRY(m->api, m->api.all_gather(m->buf[k].root.p, m->buf[k].all_roots.p, 2 * G2J_WORDS * 4, ncclUint8,
-                                           m->comm[k], m->ctx[k]->stream));
-      NCCL_TRY(m->api, m->api.group_end());
+      std::vector<const void*> src(D);
+      std::vector<void*> dst(D);
+      for (int k = 0; k < D; ++k) {
+        src[k] = m->buf[k].root.p;
+        dst[k] = m->buf[k].all_roots.p;
+      }
+      if ((rc = multi_all_gather(m, src, dst, 2 * G2J_WORDS * 4))) return rc;
       dgpu_ctx* c0 = m->ctx[0];
       HIP_TRY(hipSetDevice(c0->device));
       if ((rc = c0->rlc_root.ensure(2 * G2J_WORDS * 4))) return rc;
@@ -287,15 +343,18 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
       HIP_TRY(hipMemsetAsync((uint8_t*)m->buf[k].bits.p + b0, 0, per / 8 - b0, m->ctx[k]->stream));
     }
   }
-  NCCL_TRY(m->api, m->api.group_start());
-  for (int k = 0; k < D; ++k) {
-    NCCL_TRY(m->api, m->api.all_gather(m->buf[k].bits.p, m->buf[k].all_bits.p, per / 8, ncclUint8, m->comm[k],
-                                       m->ctx[k]->stream));
-    if (reason)
-      NCCL_TRY(m->api, m->api.all_gather(m->buf[k].reasons.p, m->buf[k].all_reasons.p, per, ncclUint8, m->comm[k],
-                                         m->ctx[k]->stream));
+  {
+    std::vector<const void*> src(D), rsrc(D);
+    std::vector<void*> dst(D), rdst(D);
+    for (int k = 0; k < D; ++k) {
+      src[k] = m->buf[k].bits.p;
+      dst[k] = m->buf[k].all_bits.p;
+      rsrc[k] = m->buf[k].reasons.p;
+      rdst[k] = m->buf[k].all_reasons.p;
+    }
+    if ((rc = multi_all_gather(m, src, dst, per / 8))) return rc;
+    if (reason && (rc = multi_all_gather(m, rsrc, rdst, per))) return rc;
   }
-  NCCL_TRY(m->api, m->api.group_end());
   for (int k = 0; k < D; ++k) {
     HIP_TRY(hipSetDevice(m->ctx[k]->device));
     HIP_TRY(hipStreamSynchronize(m->ctx[k]->stream));
@@ -309,6 +368,107 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
     HIP_TRY(hipEventRecord(m->ctx[k]->done, m->ctx[k]->stream));
     HIP_TRY(hipStreamSynchronize(m->ctx[k]->stream));
   }
+  return DGPU_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int dgpu_multi_set_group(dgpu_multi* m, int t, int n, const uint8_t* commits48) {
+  if (!m) return set_err(DGPU_EINVAL, "null handle");
+  std::lock_guard<std::mutex> mlk(m->mu);
+  for (int k = 0; k < m->ndev; ++k) {
+    int rc = dgpu_set_group(m->ctx[k], t, n, commits48);
+    if (rc) return set_err(rc, "device %d: %s", m->devs[k], std::string(g_last_error).c_str());
+  }
+  return DGPU_OK;
+}
+
+// Threshold recovery over the node: rounds shard contiguously like the verify
+// batch (dgpu_shard_range); each device stages and recovers its shard
+// (recover_device_locked: VerifyPartial / selection / Lagrange + MSM /
+// VerifyRecovered), the per-device recovery bitmaps are all-gathered (RCCL),
+// and the recovered signatures and per-partial statuses -- data, not
+// verdicts -- go to the host straight from the device that made them.
+int dgpu_recover_multi(dgpu_multi* m, size_t n_rounds, const uint8_t* msgs32, size_t m_slots, const uint8_t* partials,
+                       size_t partial_stride, const uint32_t* partial_len, uint8_t* out_sigs96, uint8_t* ok_bits,
+                       uint8_t* partial_valid) {
+  if (!m || !msgs32 || !partials || !partial_len || !out_sigs96 || !ok_bits) return set_err(DGPU_EINVAL, "null argument");
+  if (n_rounds == 0) return DGPU_OK;
+  if (m_slots == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
+  const size_t items = n_rounds * m_slots;
+  for (size_t i = 0; i < items; ++i)
+    if (partial_len[i] > partial_stride) return set_err(DGPU_EINVAL, "partial_len[%zu] > stride", i);
+  std::lock_guard<std::mutex> mlk(m->mu);
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (dgpu_ctx* c : m->ctx) locks.emplace_back(c->mu);
+  const int D = m->ndev;
+  const size_t per = (((n_rounds + (size_t)D - 1) / (size_t)D) + 7) & ~(size_t)7;
+  std::vector<size_t> lo(D), hi(D);
+  int rc;
+  for (int k = 0; k < D; ++k) {
+    dgpu_ctx* c = m->ctx[k];
+    if (!c->grp_t) return set_err(DGPU_ENOKEY, "device %d: no threshold group installed (dgpu_multi_set_group)",
+                                  m->devs[k]);
+    dgpu_shard_range(n_rounds, D, k, &lo[k], &hi[k]);
+    HIP_TRY(hipSetDevice(c->device));
+    multi_bufs& b = m->buf[k];
+    if ((rc = b.bits.ensure(per / 8)) || (rc = b.all_bits.ensure(D * per / 8))) return rc;
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
+  }
+  std::vector<std::vector<uint8_t>> stv(D);
+  rc = for_each_device(m, [&](int k) -> int {
+    dgpu_ctx* c = m->ctx[k];
+    hipStream_t s = c->stream;
+    const size_t nr = hi[k] - lo[k], it = nr * m_slots;
+    int r;
+    if (nr == 0) {
+      HIP_TRY(hipMemsetAsync(m->buf[k].bits.p, 0, per / 8, s));
+      return DGPU_OK;
+    }
+    if ((r = c->rec_msgs.ensure(nr * 32)) || (r = c->rec_parts.ensure(it * partial_stride)) ||
+        (r = c->rec_plen.ensure(it * 4)) || (r = c->rec_out.ensure(nr * 96)) || (r = c->rec_ok.ensure(nr)) ||
+        (r = c->out_reason.ensure(it)))
+      return r;
+    HIP_TRY(hipMemcpyAsync(c->rec_msgs.p, msgs32 + lo[k] * 32, nr * 32, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->rec_parts.p, partials + lo[k] * m_slots * partial_stride, it * partial_stride,
+                           hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->rec_plen.p, partial_len + lo[k] * m_slots, it * 4, hipMemcpyHostToDevice, s));
+    if ((r = recover_device_locked(c, nr, (const uint8_t*)c->rec_msgs.p, m_slots, (const uint8_t*)c->rec_parts.p,
+                                   partial_stride, (const uint32_t*)c->rec_plen.p, (uint8_t*)c->rec_out.p,
+                                   (uint8_t*)c->rec_ok.p, (uint8_t*)c->out_reason.p, s)))
+      return r;
+    HIP_TRY(hipMemsetAsync(m->buf[k].bits.p, 0, per / 8, s));
+    hipLaunchKernelGGL(k_pack_ok, dim3(grid_for((nr + 7) / 8, 256)), dim3(256), 0, s, nr, (const uint8_t*)c->rec_ok.p,
+                       (uint8_t*)m->buf[k].bits.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out_sigs96 + lo[k] * 96, c->rec_out.p, nr * 96, hipMemcpyDeviceToHost, s));
+    if (partial_valid) {
+      stv[k].resize(it);
+      HIP_TRY(hipMemcpyAsync(stv[k].data(), c->out_reason.p, it, hipMemcpyDeviceToHost, s));
+    }
+    return DGPU_OK;
+  });
+  if (rc) return rc;
+  std::vector<const void*> src(D);
+  std::vector<void*> dst(D);
+  for (int k = 0; k < D; ++k) {
+    src[k] = m->buf[k].bits.p;
+    dst[k] = m->buf[k].all_bits.p;
+  }
+  if ((rc = multi_all_gather(m, src, dst, per / 8))) return rc;
+  dgpu_ctx* c0 = m->ctx[0];
+  HIP_TRY(hipSetDevice(c0->device));
+  HIP_TRY(hipMemcpyAsync(ok_bits, m->buf[0].all_bits.p, (n_rounds + 7) / 8, hipMemcpyDeviceToHost, c0->stream));
+  for (int k = 0; k < D; ++k) {
+    HIP_TRY(hipSetDevice(m->ctx[k]->device));
+    HIP_TRY(hipEventRecord(m->ctx[k]->done, m->ctx[k]->stream));
+    HIP_TRY(hipStreamSynchronize(m->ctx[k]->stream));
+  }
+  if (partial_valid)
+    for (int k = 0; k < D; ++k)
+      for (size_t i = 0; i < stv[k].size(); ++i) partial_valid[lo[k] * m_slots + i] = stv[k][i] == ST_OK;
   return DGPU_OK;
 }
 

@@ -12,15 +12,16 @@ import numpy as np
 from . import _lib
 from .chain import pack_beacons, rlc_seed_for
 from .scheme import Scheme, scheme_code
+from .threshold import pack_partials, unpack_recovered
 
 
 class MultiVerifier:
     """chain.Verifier's batch surface over several GPUs (one dgpu_multi handle)."""
 
-    def __init__(self, scheme: Scheme, devices):
+    def __init__(self, scheme: Scheme, devices=None, mctx=None):
         self.scheme = scheme
         self._code = scheme_code(scheme)
-        self.mctx = _lib.MultiContext(devices)
+        self.mctx = mctx if mctx is not None else _lib.MultiContext(devices)
 
     def close(self):
         self.mctx.close()
@@ -47,3 +48,37 @@ class MultiVerifier:
         if not np.array_equal(valid, reason == _lib.REASON_OK):
             raise _lib.DrandGPUError(_lib.DGPU_EINVAL, "verdict bitmap and reasons disagree")
         return reason
+
+
+class MultiThresholdGroup:
+    """ThresholdGroup's batch recovery over several GPUs (dgpu_multi_set_group
+    + dgpu_recover_multi): rounds shard contiguously across the devices."""
+
+    def __init__(self, commits, n, devices=None, mctx=None):
+        self.commits = [bytes(c) for c in commits]
+        self.t, self.n = len(self.commits), n
+        self.mctx = mctx if mctx is not None else _lib.MultiContext(devices)
+        buf = np.frombuffer(b"".join(self.commits), dtype=np.uint8).copy()
+        _lib.check(self.mctx.lib.dgpu_multi_set_group(self.mctx.handle, self.t, n, _lib.ptr(buf)))
+
+    def close(self):
+        self.mctx.close()
+
+    def recover_batch(self, msgs, partials):
+        """As ThresholdGroup.recover_batch: (sigs or None per round, per-partial validity)."""
+        nr = len(msgs)
+        if nr == 0:
+            return [], []
+        mb, buf, plen, m, stride = pack_partials(msgs, partials)
+        return self.recover_records(mb, buf, plen, partials)
+
+    def recover_records(self, mb, buf, plen, partials=None):
+        nr, m, stride = buf.shape
+        out = np.zeros(nr * 96, dtype=np.uint8)
+        ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
+        pv = np.zeros(nr * m, dtype=np.uint8)
+        _lib.check(self.mctx.lib.dgpu_recover_multi(self.mctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
+                                                    _lib.ptr(plen), _lib.ptr(out), _lib.ptr(ok), _lib.ptr(pv)))
+        if partials is None:
+            partials = [[b"x"] * m for _ in range(nr)]
+        return unpack_recovered(out, ok, pv, partials, m)

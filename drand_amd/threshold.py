@@ -31,6 +31,33 @@ def index_of(partial):
     return struct.unpack(">H", partial[:2])[0]
 
 
+def pack_partials(msgs, partials):
+    """Fixed-stride partial records of the C-ABI: (msgs (nr*32,), partials
+    (nr, m, stride), partial_len (nr, m), m, stride); empty slots have length 0."""
+    nr = len(msgs)
+    m = max(1, max(len(p) for p in partials))
+    stride = max([98] + [len(s) for p in partials for s in p])
+    buf = np.zeros((nr, m, stride), dtype=np.uint8)
+    plen = np.zeros((nr, m), dtype=np.uint32)
+    for r, plist in enumerate(partials):
+        for j, s in enumerate(plist):
+            plen[r, j] = len(s)
+            if s:
+                buf[r, j, :len(s)] = np.frombuffer(s, dtype=np.uint8)
+    mb = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
+    if mb.size != 32 * nr:
+        raise ValueError("messages must be 32 bytes (DigestMessage output)")
+    return mb, buf, plen, m, stride
+
+
+def unpack_recovered(out, ok, pv, partials, m):
+    nr = len(partials)
+    okb = np.unpackbits(ok, bitorder="little")[:nr]
+    sigs = [bytes(out[96 * r:96 * (r + 1)]) if okb[r] else None for r in range(nr)]
+    valid = [[bool(pv[r * m + j]) for j in range(len(partials[r]))] for r in range(nr)]
+    return sigs, valid
+
+
 class ThresholdGroup:
     """A group's share.PubPoly installed on one GPU context."""
 
@@ -61,18 +88,7 @@ class ThresholdGroup:
         nr = len(msgs)
         if nr == 0:
             return [], []
-        m = max(1, max(len(p) for p in partials))
-        stride = max([98] + [len(s) for p in partials for s in p])
-        buf = np.zeros((nr, m, stride), dtype=np.uint8)
-        plen = np.zeros((nr, m), dtype=np.uint32)
-        for r, plist in enumerate(partials):
-            for j, s in enumerate(plist):
-                plen[r, j] = len(s)
-                if s:
-                    buf[r, j, :len(s)] = np.frombuffer(s, dtype=np.uint8)
-        mb = np.frombuffer(b"".join(msgs), dtype=np.uint8).copy()
-        if mb.size != 32 * nr:
-            raise ValueError("messages must be 32 bytes (DigestMessage output)")
+        mb, buf, plen, m, stride = pack_partials(msgs, partials)
         out = np.zeros(nr * 96, dtype=np.uint8)
         ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
         pv = np.zeros(nr * m, dtype=np.uint8)
@@ -80,10 +96,7 @@ class ThresholdGroup:
             self._install()
             _lib.check(self.ctx.lib.dgpu_recover_batch(self.ctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
                                                        _lib.ptr(plen), _lib.ptr(out), _lib.ptr(ok), _lib.ptr(pv)))
-        okb = np.unpackbits(ok, bitorder="little")[:nr]
-        sigs = [bytes(out[96 * r:96 * (r + 1)]) if okb[r] else None for r in range(nr)]
-        valid = [[bool(pv[r * m + j]) for j in range(len(partials[r]))] for r in range(nr)]
-        return sigs, valid
+        return unpack_recovered(out, ok, pv, partials, m)
 
     def recover(self, msg, sigs):
         """key.Scheme.Recover(pub, msg, sigs, t, n): the recovered 96-byte

@@ -293,6 +293,24 @@ int dgpu_verify_multi(dgpu_multi *m, int scheme, const uint8_t *pk, size_t pk_le
                       size_t prev_stride, const uint32_t *prev_len, int mode, uint64_t rlc_seed,
                       uint8_t *verdict_bits, uint8_t *reason);
 
+/* dgpu_set_group on every device of the handle (the aggregator's group,
+ * chain/beacon/chain.go:158-168 -> key.Scheme.Recover). */
+int dgpu_multi_set_group(dgpu_multi *m, int t, int n, const uint8_t *commits48);
+
+/* dgpu_recover_batch over the node: rounds shard contiguously across the
+ * devices (dgpu_shard_range over n_rounds), each device recovers its shard,
+ * RCCL all-gathers the per-device recovery bitmaps; recovered signatures and
+ * per-partial validity go to the host from the device that computed them.
+ * Arguments and results exactly as dgpu_recover_batch. */
+int dgpu_recover_multi(dgpu_multi *m, size_t n_rounds, const uint8_t *msgs32, size_t m_slots, const uint8_t *partials,
+                       size_t partial_stride, const uint32_t *partial_len, uint8_t *out_sigs96, uint8_t *ok_bits,
+                       uint8_t *partial_valid);
+
+/* Test mode (environment, read by dgpu_multi_open): DGPU_MULTI_ALLOW_SAME_DEVICE=1
+ * lets devs list one GPU several times (one context each) and replaces the
+ * RCCL all-gathers with in-library device copies, so one GPU runs every
+ * multi-device branch (shard padding, per-device seeds, root sum). */
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,7 +16,40 @@ SCHEME_BY_CODE = {0: "pedersen-bls-chained", 1: "pedersen-bls-unchained", 2: "bl
                   3: "bls-unchained-g1-rfc9380"}
 
 
+def host_cores():
+    """The box's CPU view, stated with every baseline: all host cores
+    (os.cpu_count), the cores this process may run on (sched_getaffinity),
+    and the cgroup CPU quota when one is set (cpu.max, in cores)."""
+    info = {"host_cores": os.cpu_count(), "affinity_cores": len(os.sched_getaffinity(0))}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cores"] = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def _timed(fn):
+    """wall and process CPU seconds (all threads) of fn()"""
+    c0, t0 = time.process_time(), time.perf_counter()
+    out = fn()
+    return out, time.perf_counter() - t0, time.process_time() - c0
+
+
+def sample_size(n, seconds, cores, per_round_1core, calib_rate=None):
+    """Rounds for ~`seconds` of wall time: from a measured parallel rate when
+    there is one (quota-limited boxes run fewer cores than threads)."""
+    rate = calib_rate if calib_rate else cores / max(per_round_1core, 1e-6)
+    return int(max(cores, min(n, seconds * rate)))
+
+
 def run(chain, seconds, cores, expect_valid=None):
+    """`cores` threads of the C restatement over a bounded uniform sample of
+    the chain: calibrated single-threaded (the reference's bulk loop is one
+    goroutine, chain/beacon/sync_manager.go:188) and on all threads, then
+    timed; reports wall rate, CPU seconds used and the effective parallelism."""
     n = len(chain)
     chained = chain.scheme_code == 0
     on_g1 = chain.scheme_code >= 2
@@ -32,23 +65,26 @@ def run(chain, seconds, cores, expect_valid=None):
             impl = "oracle/c/bls381_ref.c (C restatement, 6x64-bit limbs, [r]Q subgroup test as kilic (R))"
             verify = lambda sub, thr: c_ref.verify_batch(chained, chain.pk, *sub, thr)  # noqa: E731
         cols = (chain.rounds, chain.sigs, chain.sig_len, chain.prev, chain.prev_len)
-        # calibrate on a few rounds single-threaded
-        idx0 = np.arange(min(4, n))
-        t = time.perf_counter()
-        verify([np.ascontiguousarray(a[idx0]) for a in cols], 1)
-        per = (time.perf_counter() - t) / len(idx0)
-        sample = int(max(cores, min(n, seconds * cores / max(per, 1e-6))))
         rng = np.random.default_rng(12345)
-        idx = np.sort(rng.choice(n, size=sample, replace=False))
-        sub = [np.ascontiguousarray(a[idx]) for a in cols]
-        t = time.perf_counter()
-        reason = verify(sub, cores)
-        wall = time.perf_counter() - t
+        pick = lambda k: np.sort(rng.choice(n, size=min(n, k), replace=False))  # noqa: E731
+        sub_of = lambda idx: [np.ascontiguousarray(a[idx]) for a in cols]  # noqa: E731
+        # single-threaded calibration, then a short all-threads calibration
+        idx0 = pick(4)
+        _, w1, _ = _timed(lambda: verify(sub_of(idx0), 1))
+        per = w1 / len(idx0)
+        idxc = pick(2 * cores)
+        _, wc, _ = _timed(lambda: verify(sub_of(idxc), cores))
+        sample = sample_size(n, seconds, cores, per, len(idxc) / max(wc, 1e-6))
+        idx = pick(sample)
+        sub = sub_of(idx)
+        reason, wall, cpu_s = _timed(lambda: verify(sub, cores))
     except Exception as e:  # C build unavailable: pure-Python oracle
         return _run_py(chain, seconds, cores, repr(e))
     out = {"value": sample / wall, "unit": "rounds/s", "cores": cores, "kind": "port", "impl": impl,
            "sample": f"{sample} uniformly sampled rounds of the bench chain", "wall_s": wall,
-           "single_core_ms_per_round": per * 1e3}
+           "cpu_s": cpu_s, "effective_parallelism": cpu_s / wall,
+           "single_core_ms_per_round": per * 1e3, "single_core_value": 1.0 / per}
+    out.update(host_cores())
     if expect_valid is not None:
         out["sample_verdict_mismatches"] = int(((reason == 0) != expect_valid[idx]).sum())
     return out
@@ -131,21 +167,25 @@ def run_recover(commits, t, n, msgs, parts, expect_sigs, seconds, cores):
     try:
         from oracle import c_ref
         c_ref.load()
-        t0 = time.perf_counter()
-        c_ref.recover_batch(commits, t, msgs[:1], parts[:1], 1)
-        per = time.perf_counter() - t0
-        sample = int(max(cores, min(nr, seconds * cores / max(per, 1e-6))))
-        idx = np.sort(np.random.default_rng(12345).choice(nr, size=sample, replace=False))
-        t0 = time.perf_counter()
-        sigs, ok = c_ref.recover_batch(commits, t, np.ascontiguousarray(msgs[idx]), np.ascontiguousarray(parts[idx]),
-                                       cores)
-        wall = time.perf_counter() - t0
+        rng = np.random.default_rng(12345)
+        pick = lambda k: np.sort(rng.choice(nr, size=min(nr, k), replace=False))  # noqa: E731
+        run_idx = lambda idx, thr: c_ref.recover_batch(  # noqa: E731
+            commits, t, np.ascontiguousarray(msgs[idx]), np.ascontiguousarray(parts[idx]), thr)
+        _, w1, _ = _timed(lambda: run_idx(pick(1), 1))
+        idxc = pick(cores)
+        _, wc, _ = _timed(lambda: run_idx(idxc, cores))
+        sample = sample_size(nr, seconds, cores, w1, len(idxc) / max(wc, 1e-6))
+        idx = pick(sample)
+        (sigs, ok), wall, cpu_s = _timed(lambda: run_idx(idx, cores))
         mism = sum(1 for k, i in enumerate(idx) if (bytes(sigs[k]) if ok[k] else None) != expect_sigs[i])
-        return {"value": sample / wall, "unit": "rounds/s", "cores": cores, "kind": "port",
-                "impl": "oracle/c/bls381_ref.c ref_recover (C restatement of kyber tbls.Recover (R): VerifyPartial x t, "
-                        "Lagrange in Fr, G2 MSM, VerifyRecovered)",
-                "sample": f"{sample} uniformly sampled rounds of the bench batch", "wall_s": wall,
-                "single_core_ms_per_round": per * 1e3, "sample_mismatches": mism}
+        out = {"value": sample / wall, "unit": "rounds/s", "cores": cores, "kind": "port",
+               "impl": "oracle/c/bls381_ref.c ref_recover (C restatement of kyber tbls.Recover (R): VerifyPartial x t, "
+                       "Lagrange in Fr, G2 MSM, VerifyRecovered)",
+               "sample": f"{sample} uniformly sampled rounds of the bench batch", "wall_s": wall, "cpu_s": cpu_s,
+               "effective_parallelism": cpu_s / wall, "single_core_ms_per_round": w1 * 1e3,
+               "single_core_value": 1.0 / w1, "sample_mismatches": mism}
+        out.update(host_cores())
+        return out
     except (OSError, AttributeError):
         return _run_recover_py(commits, t, n, msgs, parts, expect_sigs, seconds, cores)
 

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-3 GPU session: GPU tests (+ smoke), then the default bench (every
+# BASELINE config leg), optionally a rocprofv3 kernel-stats pass.  Each GPU
+# step has its own time limit; the script stops at the first failure.
+export TMPDIR=/tmp
+TAG=${TAG:-r03a}
+O=gpurun_out/$TAG
+mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+if [ -z "$NOTEST" ]; then
+step pytest
+timeout -k 10 720 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log
+[ $rc -ne 0 ] && exit $rc
+step smoke
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
+tail -1 $O/smoke.log
+fi
+if [ -z "$NOBENCH" ]; then
+step bench
+timeout -k 10 ${BENCH_T:-600} python -u bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || exit $?
+head -c 400 $O/bench.json; echo
+fi
+if [ -n "$PROF" ]; then
+step rocprof
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --no-e2e --no-legs --steps 2 > $O/prof.out 2>&1 || exit $?
+python3 tools/rocpd_stats.py $(find $O/prof -name "*results.db" | head -1) > $O/kernel_stats.csv
+fi
+echo done

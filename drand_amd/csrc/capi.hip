@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -170,6 +171,10 @@ struct dgpu_ctx {
   int grp_t = 0, grp_n = 0;
   DevBuf grp_commits, grp_table, rec_msgs, rec_parts, rec_plen, rec_hidx, rec_pk, rec_idx, rec_lam, rec_out, rec_ok,
       rec_pts, rec_vpk, rec_sel, rec_part, rec_st;
+  // batched recovery check: the group's window table of the share keys, round
+  // classes, and the compact batch of rounds that take the exact path
+  DevBuf grp_wtab, rec_cls, rec_x_list, rec_x_msgs, rec_x_parts, rec_x_plen, rec_x_out, rec_x_ok, rec_x_st;
+  bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call (event pool;
@@ -840,6 +845,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");
   if (sgv && !strcmp(sgv, "decode")) c->decode_subgroup = true;
+  const char* rcv = getenv("DGPU_RECOVER");
+  if (rcv && !strcmp(rcv, "exact")) c->recover_exact = true;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
@@ -874,7 +881,9 @@ void dgpu_close(dgpu_ctx* c) {
   }
   for (DevBuf* b : {&c->grp_commits, &c->grp_table, &c->rec_msgs, &c->rec_parts, &c->rec_plen, &c->rec_hidx,
                     &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk,
-                    &c->rec_st, &c->rec_sel, &c->rec_part, &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1,
+                    &c->rec_st, &c->rec_sel, &c->rec_part, &c->grp_wtab, &c->rec_cls, &c->rec_x_list,
+                    &c->rec_x_msgs, &c->rec_x_parts, &c->rec_x_plen, &c->rec_x_out, &c->rec_x_ok, &c->rec_x_st,
+                    &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
                     &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->in_rounds, &c->in_sigs,
                     &c->in_sig_len, &c->in_prev, &c->in_prev_len, &c->in_msgs, &c->in_msg_len, &c->out_bits,
@@ -1256,6 +1265,10 @@ int dgpu_set_group(dgpu_ctx* c, int t, int n, const uint8_t* commits48) {
   hipLaunchKernelGGL(k_pubpoly_table, dim3(grid_for(n, 64)), dim3(64), 0, s, n, t, (const uint32_t*)c->grp_commits.p,
                      (uint32_t*)c->grp_table.p);
   HIP_TRY(hipGetLastError());
+  if ((rc = c->grp_wtab.ensure((size_t)n * 8 * REC_WTAB_WORDS * 4))) return rc;
+  hipLaunchKernelGGL(k_pubpoly_wtable, dim3(grid_for(8 * (size_t)n, 64)), dim3(64), 0, s, n,
+                     (const uint32_t*)c->grp_table.p, (uint32_t*)c->grp_wtab.p);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(s));
   c->grp_t = t;
   c->grp_n = n;
@@ -1264,10 +1277,11 @@ int dgpu_set_group(dgpu_ctx* c, int t, int n, const uint8_t* commits48) {
 
 }  // extern "C"
 
-// Recovery over device buffers (the body of both recover entry points).
-// d_ok: one byte per round (1 = recovered and VerifyRecovered passed);
-// d_status (optional): ST_* of every partial item.
-static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msgs, size_t m,
+// Exact per-partial recovery over device buffers: VerifyPartial of every
+// partial, selection, Lagrange + MSM, VerifyRecovered -- the reference's
+// walk, pairing by pairing.  d_ok: one byte per round (1 = recovered and
+// VerifyRecovered passed); d_status (optional): ST_* of every partial item.
+static int recover_exact_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msgs, size_t m,
                                  const uint8_t* d_parts, size_t stride, const uint32_t* d_plen, uint8_t* d_out,
                                  uint8_t* d_ok, uint8_t* d_status, hipStream_t s) {
   if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
@@ -1278,7 +1292,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   if ((rc = c->rec_hidx.ensure(items * 4))) return rc;
   if ((rc = c->rec_pk.ensure(items * 2 * FP_LIMBS * 4))) return rc;
   if ((rc = c->rec_idx.ensure(items * 4))) return rc;
-  if ((rc = c->rec_lam.ensure(n_rounds * RECOVER_MAX_T * 8 * 4))) return rc;
+  if ((rc = c->rec_lam.ensure(n_rounds * RECOVER_MAX_T * RECOVER_SLOTS * 8))) return rc;
   if ((rc = c->rec_pts.ensure(n_rounds * G2A_WORDS * 4))) return rc;
   if ((rc = c->rec_vpk.ensure(n_rounds * 2 * FP_LIMBS * 4))) return rc;
   if ((rc = c->rec_st.ensure(n_rounds))) return rc;
@@ -1289,7 +1303,6 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
   uint8_t* st = (uint8_t*)c->status.p;
   uint32_t* hidx = (uint32_t*)c->rec_hidx.p;
-  c->n_ev = 0;
   mark(c, s, "recover_hash");
   hipLaunchKernelGGL(k_hash_to_g2_msgs_pts, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds, d_msgs, h);
   HIP_TRY(hipGetLastError());
@@ -1307,7 +1320,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   uint32_t* rpk = (uint32_t*)c->rec_vpk.p;
   uint8_t* rst = (uint8_t*)c->rec_st.p;
   if ((rc = c->rec_sel.ensure(n_rounds * RECOVER_MAX_T * 2 * 4)) ||
-      (rc = c->rec_part.ensure(n_rounds * 4 * G2J_WORDS * 4)))
+      (rc = c->rec_part.ensure(n_rounds * 5 * G2J_WORDS * 4)))
     return rc;
   uint32_t* sel = (uint32_t*)c->rec_sel.p;
   uint32_t* xs = sel + n_rounds * RECOVER_MAX_T;
@@ -1321,7 +1334,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   HIP_TRY(hipGetLastError());
   mark(c, s, "recover_lagrange");
   hipLaunchKernelGGL(k_recover_lagrange, dim3(grid_for(n_rounds * RECOVER_MAX_T, 256)), dim3(256), 0, s, n_rounds, t,
-                     (const uint8_t*)d_ok, (const uint32_t*)xs, dig);
+                     (const uint8_t*)d_ok, (const uint32_t*)xs, dig, (uint64_t)0);
   HIP_TRY(hipGetLastError());
   mark(c, s, "recover_msm");
 #if defined(DG_RECOVER_MSM_BITS)
@@ -1333,12 +1346,12 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
     auto msm = t <= 8 ? k_recover_msm_w4<8> : t <= 16 ? k_recover_msm_w4<16> : t <= 24 ? k_recover_msm_w4<24>
                                                                                          : k_recover_msm_w4<32>;
     hipLaunchKernelGGL(msm, dim3(grid_for(4 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t, (const uint8_t*)d_ok,
-                       (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part);
+                       (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part, 4);
   }
 #endif
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_recover_finish, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, (const uint8_t*)d_ok,
-                     (const uint32_t*)part, d_out, rpts, rst);
+                     (const uint32_t*)part, d_out, rpts, rst, 4);
   HIP_TRY(hipGetLastError());
   // VerifyRecovered: e(C_0, H(msg)) e(-g1, sig) == 1
   if ((rc = eng_pairing_locked(c, consts, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;
@@ -1347,6 +1360,114 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   HIP_TRY(hipGetLastError());
   if (d_status) HIP_TRY(hipMemcpyAsync(d_status, st, items, hipMemcpyDeviceToDevice, s));
   mark(c, s);
+  return DGPU_OK;
+}
+
+// Recovery over device buffers (the body of every recover entry point):
+// the batched check (recover.cuh) for every round it decides, the exact
+// per-partial path for the rest (compacted, then scattered back).
+static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msgs, size_t m,
+                                 const uint8_t* d_parts, size_t stride, const uint32_t* d_plen, uint8_t* d_out,
+                                 uint8_t* d_ok, uint8_t* d_status, hipStream_t s) {
+  if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
+  c->n_ev = 0;
+  if (c->recover_exact)
+    return recover_exact_locked(c, n_rounds, d_msgs, m, d_parts, stride, d_plen, d_out, d_ok, d_status, s);
+  const size_t items = n_rounds * m;
+  if (items > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "batch too large (%zu items)", items);
+  const uint32_t* consts = (const uint32_t*)c->eng_consts.p;
+  const int t = c->grp_t;
+  int rc;
+  if ((rc = c->rec_hidx.ensure(items * 4)) || (rc = c->rec_pk.ensure(items * 2 * FP_LIMBS * 4)) ||
+      (rc = c->rec_idx.ensure(items * 4)) || (rc = c->rec_lam.ensure(n_rounds * RECOVER_MAX_T * RECOVER_SLOTS * 8)) ||
+      (rc = c->rec_pts.ensure(n_rounds * G2A_WORDS * 4)) || (rc = c->rec_vpk.ensure(n_rounds * 2 * FP_LIMBS * 4)) ||
+      (rc = c->rec_st.ensure(n_rounds)) || (rc = c->rec_cls.ensure(n_rounds)) ||
+      (rc = c->h_pts.ensure(n_rounds * G2A_WORDS * 4)) || (rc = c->sig_pts.ensure(items * G2A_WORDS * 4)) ||
+      (rc = c->status.ensure(items)) || (rc = c->rec_sel.ensure(n_rounds * RECOVER_MAX_T * 2 * 4)) ||
+      (rc = c->rec_part.ensure(n_rounds * 5 * G2J_WORDS * 4)))
+    return rc;
+  uint32_t* h = (uint32_t*)c->h_pts.p;
+  uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  uint32_t* sel = (uint32_t*)c->rec_sel.p;
+  uint32_t* xs = sel + n_rounds * RECOVER_MAX_T;
+  uint64_t* dig = (uint64_t*)c->rec_lam.p;
+  uint32_t* part = (uint32_t*)c->rec_part.p;
+  uint32_t* rpts = (uint32_t*)c->rec_pts.p;
+  uint32_t* rpk = (uint32_t*)c->rec_vpk.p;
+  uint8_t* rst = (uint8_t*)c->rec_st.p;
+  uint8_t* cls = (uint8_t*)c->rec_cls.p;
+  // fresh, unpredictable coefficients per call (partials come from peers)
+  std::random_device rd;
+  uint64_t seed = ((uint64_t)rd() << 32) ^ rd();
+  if (!seed) seed = 1;
+  mark(c, s, "recover_hash");
+  hipLaunchKernelGGL(k_hash_to_g2_msgs_pts, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds, d_msgs, h);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_decode");
+  hipLaunchKernelGGL(k_decode_partials, dim3(grid_for(items, 256)), dim3(256), 0, s, items, d_parts, stride, d_plen,
+                     c->grp_n, c->grp_t, (const uint32_t*)c->grp_table.p, (const uint32_t*)c->grp_commits.p, sg,
+                     (uint32_t*)c->rec_pk.p, (uint32_t*)c->rec_idx.p, st);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_select");
+  hipLaunchKernelGGL(k_recover_cand, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, m, t, d_status ? 1 : 0,
+                     (const uint32_t*)c->rec_idx.p, (const uint8_t*)st, sel, xs, cls, d_ok, d_out);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_lagrange");
+  hipLaunchKernelGGL(k_recover_lagrange, dim3(grid_for(n_rounds * RECOVER_MAX_T, 256)), dim3(256), 0, s, n_rounds, t,
+                     (const uint8_t*)d_ok, (const uint32_t*)xs, dig, seed);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_msm");
+  {
+    auto msm = t <= 8 ? k_recover_msm_w4<8> : t <= 16 ? k_recover_msm_w4<16> : t <= 24 ? k_recover_msm_w4<24>
+                                                                                         : k_recover_msm_w4<32>;
+    hipLaunchKernelGGL(msm, dim3(grid_for(5 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t, (const uint8_t*)d_ok,
+                       (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part, 5);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_recover_finish, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, (const uint8_t*)d_ok,
+                     (const uint32_t*)part, d_out, rpts, rst, 5);
+  HIP_TRY(hipGetLastError());
+  mark(c, s, "recover_rlc_g1");
+  hipLaunchKernelGGL(k_recover_rlc_g1, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, t, c->grp_n,
+                     (const uint32_t*)sel, (const uint32_t*)c->rec_idx.p, (const uint64_t*)dig,
+                     (const uint32_t*)c->grp_wtab.p, (const uint32_t*)c->grp_commits.p, cls, d_ok, rpk, rst);
+  HIP_TRY(hipGetLastError());
+  // one pairing per round: e(A, H) e(-g1, B) == 1
+  if ((rc = eng_pairing_locked(c, consts, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;
+  mark(c, s, "recover_verdict");
+  hipLaunchKernelGGL(k_recover_rlc_verdict, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds,
+                     (const uint8_t*)rst, cls, d_ok, d_out);
+  HIP_TRY(hipGetLastError());
+  if (d_status) HIP_TRY(hipMemcpyAsync(d_status, st, items, hipMemcpyDeviceToDevice, s));
+  // rounds left to the exact path
+  std::vector<uint8_t> hc(n_rounds);
+  HIP_TRY(hipMemcpyAsync(hc.data(), cls, n_rounds, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  std::vector<uint32_t> list;
+  for (size_t r = 0; r < n_rounds; ++r)
+    if ((hc[r] & 0x0F) == REC_EXACT) list.push_back((uint32_t)r);
+  mark(c, s);
+  const size_t nx = list.size();
+  if (nx == 0) return DGPU_OK;
+  const size_t xi = nx * m;
+  if ((rc = c->rec_x_list.ensure(nx * 4)) || (rc = c->rec_x_msgs.ensure(nx * 32)) ||
+      (rc = c->rec_x_parts.ensure(xi * stride)) || (rc = c->rec_x_plen.ensure(xi * 4)) ||
+      (rc = c->rec_x_out.ensure(nx * 96)) || (rc = c->rec_x_ok.ensure(nx)) || (rc = c->rec_x_st.ensure(xi)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(c->rec_x_list.p, list.data(), nx * 4, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_gather_rounds, dim3(grid_for(xi, 256)), dim3(256), 0, s, nx, (const uint32_t*)c->rec_x_list.p,
+                     m, stride, d_msgs, d_parts, d_plen, (uint8_t*)c->rec_x_msgs.p, (uint8_t*)c->rec_x_parts.p,
+                     (uint32_t*)c->rec_x_plen.p);
+  HIP_TRY(hipGetLastError());
+  if ((rc = recover_exact_locked(c, nx, (const uint8_t*)c->rec_x_msgs.p, m, (const uint8_t*)c->rec_x_parts.p, stride,
+                                 (const uint32_t*)c->rec_x_plen.p, (uint8_t*)c->rec_x_out.p, (uint8_t*)c->rec_x_ok.p,
+                                 (uint8_t*)c->rec_x_st.p, s)))
+    return rc;
+  hipLaunchKernelGGL(k_scatter_rounds, dim3(grid_for(xi, 256)), dim3(256), 0, s, nx, (const uint32_t*)c->rec_x_list.p,
+                     m, (const uint8_t*)c->rec_x_out.p, (const uint8_t*)c->rec_x_ok.p, (const uint8_t*)c->rec_x_st.p,
+                     d_out, d_ok, d_status);
+  HIP_TRY(hipGetLastError());
   return DGPU_OK;
 }
 
@@ -1393,7 +1514,7 @@ int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size
   HIP_TRY(hipMemcpyAsync(c->rec_plen.p, partial_len, items * 4, hipMemcpyHostToDevice, s));
   if ((rc = recover_device_locked(c, n_rounds, (const uint8_t*)c->rec_msgs.p, m, (const uint8_t*)c->rec_parts.p,
                                   partial_stride, (const uint32_t*)c->rec_plen.p, (uint8_t*)c->rec_out.p,
-                                  (uint8_t*)c->rec_ok.p, (uint8_t*)c->out_reason.p, s)))
+                                  (uint8_t*)c->rec_ok.p, partial_valid ? (uint8_t*)c->out_reason.p : nullptr, s)))
     return rc;
   std::vector<uint8_t> okv(n_rounds), stv(partial_valid ? items : 0);
   HIP_TRY(hipMemcpyAsync(out_sigs96, c->rec_out.p, n_rounds * 96, hipMemcpyDeviceToHost, s));

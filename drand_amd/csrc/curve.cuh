@@ -443,6 +443,33 @@ DG_FN g1j g1_add_body(const g1j& p, const g1j& q) {
 
 DG_NOINL g1j g1_add(const g1j& p, const g1j& q) { return g1_add_body(p, q); }
 
+// Mixed addition p + q, q affine (madd-2007-bl, a = 0: 7M + 4S), exceptional
+// cases resolved (p == q -> dbl, p == -q -> infinity, p infinity -> q).
+DG_FN g1j g1_add_affine_body(const g1j& p, const g1a& q) {
+  const fp z1z1 = fp_sqr(p.z);
+  const fp u2 = fp_mul(q.x, z1z1);
+  const fp s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  const fp h = fp_sub(u2, p.x);
+  const fp rr = fp_dbl(fp_sub(s2, p.y));
+  const bool p_inf = g1_is_inf(p);
+  const bool h0 = fp_is_zero(h), r0 = fp_is_zero(rr);
+  const fp hh = fp_sqr(h);
+  const fp i = fp_dbl(fp_dbl(hh));
+  const fp j = fp_mul(h, i);
+  const fp v = fp_mul(p.x, i);
+  g1j r;
+  r.x = fp_sub(fp_sub(fp_sqr(rr), j), fp_dbl(v));
+  r.y = fp_sub(fp_mul(rr, fp_sub(v, r.x)), fp_dbl(fp_mul(p.y, j)));
+  r.z = fp_sub(fp_sqr(fp_add(p.z, h)), fp_add(z1z1, hh));
+  if (h0 && !p_inf) r = r0 ? g1_dbl(g1j{q.x, q.y, fp_one()}) : g1_infinity();
+  if (p_inf) r = g1j{q.x, q.y, fp_one()};
+  return r;
+}
+
+DG_FN g1j g1_cmov(const g1j& a, const g1j& b, bool take_b) {
+  return g1j{fp_cmov(a.x, b.x, take_b), fp_cmov(a.y, b.y, take_b), fp_cmov(a.z, b.z, take_b)};
+}
+
 // generic scalar multiplication by a little-endian 32-bit-word scalar
 DG_NOINL g1j g1_mul_words(const g1j& p, const uint32_t* k, int nwords) {
   g1j r = g1_infinity();

@@ -437,7 +437,7 @@ int dgpu_recover_multi(dgpu_multi* m, size_t n_rounds, const uint8_t* msgs32, si
     HIP_TRY(hipMemcpyAsync(c->rec_plen.p, partial_len + lo[k] * m_slots, it * 4, hipMemcpyHostToDevice, s));
     if ((r = recover_device_locked(c, nr, (const uint8_t*)c->rec_msgs.p, m_slots, (const uint8_t*)c->rec_parts.p,
                                    partial_stride, (const uint32_t*)c->rec_plen.p, (uint8_t*)c->rec_out.p,
-                                   (uint8_t*)c->rec_ok.p, (uint8_t*)c->out_reason.p, s)))
+                                   (uint8_t*)c->rec_ok.p, partial_valid ? (uint8_t*)c->out_reason.p : nullptr, s)))
       return r;
     HIP_TRY(hipMemsetAsync(m->buf[k].bits.p, 0, per / 8, s));
     hipLaunchKernelGGL(k_pack_ok, dim3(grid_for((nr + 7) / 8, 256)), dim3(256), 0, s, nr, (const uint8_t*)c->rec_ok.p,

@@ -11,6 +11,21 @@
 // sum_j lambda_j sig_j (4-way split by the psi endomorphism, Straus, mixed additions),
 // compressed to 96 bytes; then VerifyRecovered (chain.go:165) of every
 // recovered signature under C_0 on the engine.
+//
+// Batched check (the default path, capi.hip recover_device_locked): all
+// partials of a round sign the same H(msg), so instead of t VerifyPartial
+// pairings the round's first t decodable partials (the candidates) are
+// checked together with the recovered signature in ONE two-pair pairing:
+//   e(C_0 + sum_j r_j Eval(i_j), H) * e(-g1, sigma + sum_j r_j sig_j) == 1
+// with fresh uniform 64-bit r_j.  With E_j = sig_j - s_j H the error of
+// candidate j, sigma - sk H = sum_j lambda_j E_j, so the check holds iff
+// sum_j (r_j + lambda_j) E_j = 0: always when every candidate is valid (then
+// the selection is exactly the reference's "first t good"), and with
+// probability <= 2^-64 otherwise.  A failing round is decided without
+// pairings when no decodable partial is left beyond the candidates (the
+// reference cannot reach t good ones either); otherwise it, and every round
+// whose per-partial statuses are requested, takes the exact per-partial path
+// above.
 #pragma once
 #include "fr.cuh"
 #include "kernels.cuh"
@@ -18,6 +33,13 @@
 namespace dgpu {
 
 constexpr int RECOVER_MAX_T = 32;
+// digits per (round, j): the four base-|x| digits of lambda_j, then the RLC
+// coefficient r_j of the batched check
+constexpr int RECOVER_SLOTS = 5;
+
+// recovery class of a round (k_recover_cand; REC_MORE flags a decodable
+// partial beyond the candidates)
+enum : uint8_t { REC_RLC = 0, REC_FAIL = 1, REC_EXACT = 2, REC_MORE = 0x10 };
 
 // Group commitments C_j (48-byte compressed G1) -> affine SoA [x, y][limb][t]
 // (Montgomery); rc[j] = decode code.  kyber UnmarshalBinary semantics (R).
@@ -211,9 +233,11 @@ __global__ void __launch_bounds__(64) k_recover_select(size_t n_rounds, size_t m
   ok[r] = 1;
 }
 
+// rlc_seed != 0: slot 4 = r_j of the batched check (SplitMix64 of the seed
+// and the (round, j) position, as the beacon RLC's rlc_coeff)
 __global__ void __launch_bounds__(256) k_recover_lagrange(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
                                                           const uint32_t* __restrict__ xs,
-                                                          uint64_t* __restrict__ digits) {
+                                                          uint64_t* __restrict__ digits, uint64_t rlc_seed) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_rounds * RECOVER_MAX_T) return;
   const size_t r = g / RECOVER_MAX_T;
@@ -221,11 +245,12 @@ __global__ void __launch_bounds__(256) k_recover_lagrange(size_t n_rounds, int t
   if (j >= t || !ok[r]) return;
   uint32_t w[8];
   fr_lagrange_at_zero(xs + r * RECOVER_MAX_T, t, j, w);
-  uint64_t* d = digits + g * 4;
+  uint64_t* d = digits + g * RECOVER_SLOTS;
   d[0] = div_absx(w);
   d[1] = div_absx(w);
   d[2] = div_absx(w);
   d[3] = ((uint64_t)w[1] << 32) | w[0];  // the last quotient, < |x| since lambda < r < |x|^4
+  d[4] = rlc_seed ? rlc_coeff(rlc_seed, g) : 0;
 }
 
 __global__ void __launch_bounds__(256, 2) k_recover_msm(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
@@ -238,13 +263,13 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm(size_t n_rounds, int t, 
   const size_t r = g >> 2;
   const int i = (int)(g & 3);
   if (!ok[r]) return;
-  const uint64_t* d = digits + r * RECOVER_MAX_T * 4 + i;
+  const uint64_t* d = digits + r * RECOVER_MAX_T * RECOVER_SLOTS + i;
   const uint32_t* sl = sel + r * RECOVER_MAX_T;
   g2j acc = g2_infinity();
   for (int b = 63; b >= 0; --b) {
     acc = g2_dbl_body(acc);
     for (int j = 0; j < t; ++j)
-      if ((d[4 * j] >> b) & 1ull) acc = g2_add_affine_body(acc, ld_g2a(sig_pts, n_items, sl[j]));
+      if ((d[RECOVER_SLOTS * j] >> b) & 1ull) acc = g2_add_affine_body(acc, ld_g2a(sig_pts, n_items, sl[j]));
   }
   st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
 }
@@ -266,19 +291,21 @@ DG_FN int win4_digit64(uint64_t k, int j) {
 // [1..8] sig_j (Jacobian, private memory, 1 doubling + 6 mixed additions),
 // then 17 signed radix-16 windows of 4 doublings + t additions (a zero
 // digit's addition computed and discarded): 16 t + 7 t additions in all.
-// TMAX bounds t (private table TMAX x 8 points).
+// TMAX bounds t (private table TMAX x 8 points).  `slices` threads per
+// round: the four digit slices of lambda, and (slices = 5) the batched
+// check's sum_j r_j sig_j.
 template <int TMAX>
 __global__ void __launch_bounds__(256, 2) k_recover_msm_w4(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
                                                          const uint32_t* __restrict__ sel,
                                                          const uint64_t* __restrict__ digits,
                                                          const uint32_t* __restrict__ sig_pts, size_t n_items,
-                                                         uint32_t* __restrict__ part) {
+                                                         uint32_t* __restrict__ part, int slices) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= 4 * n_rounds) return;
-  const size_t r = g >> 2;
-  const int i = (int)(g & 3);
+  if (g >= (size_t)slices * n_rounds) return;
+  const size_t r = g / slices;
+  const int i = (int)(g % slices);
   if (!ok[r] || t > TMAX) return;
-  const uint64_t* d = digits + r * RECOVER_MAX_T * 4 + i;
+  const uint64_t* d = digits + r * RECOVER_MAX_T * RECOVER_SLOTS + i;
   const uint32_t* sl = sel + r * RECOVER_MAX_T;
   g2j T[TMAX][8];
 #pragma unroll 1
@@ -298,7 +325,7 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm_w4(size_t n_rounds, int 
     }
 #pragma unroll 1
     for (int j = 0; j < t; ++j) {
-      const int dg = win4_digit64(d[4 * j], w);
+      const int dg = win4_digit64(d[RECOVER_SLOTS * j], w);
       const int mag = dg < 0 ? -dg : dg;
       g2j e = T[j][(mag - 1) & 7];
       e.y = fp2_cmov(e.y, fp2_neg(e.y), dg < 0);
@@ -308,9 +335,12 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm_w4(size_t n_rounds, int 
   st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
 }
 
+// slices = 5 (batched check): rec_pts gets B = sigma + sum_j r_j sig_j
+// instead of sigma, and rec_st whether B is the identity.
 __global__ void __launch_bounds__(64) k_recover_finish(size_t n_rounds, const uint8_t* __restrict__ ok,
                                                        const uint32_t* __restrict__ part, uint8_t* __restrict__ out96,
-                                                       uint32_t* __restrict__ rec_pts, uint8_t* __restrict__ rec_st) {
+                                                       uint32_t* __restrict__ rec_pts, uint8_t* __restrict__ rec_st,
+                                                       int slices) {
   const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rounds || !ok[r]) return;
   const g2j p0 = ld_g2j(part, n_rounds, r);
@@ -323,6 +353,13 @@ __global__ void __launch_bounds__(64) k_recover_finish(size_t n_rounds, const ui
   const bool inf = g2_is_inf(acc);
   const g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(acc);
   g2_compress(out96 + r * 96, a, inf);
+  if (slices == 5) {
+    const g2j b = g2_add(acc, ld_g2j(part + 4 * G2J_WORDS * n_rounds, n_rounds, r));
+    const bool binf = g2_is_inf(b);
+    st_g2a(rec_pts, n_rounds, r, binf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(b));
+    rec_st[r] = binf ? (uint8_t)ST_INFINITY : (uint8_t)ST_OK;
+    return;
+  }
   st_g2a(rec_pts, n_rounds, r, a);
   rec_st[r] = inf ? (uint8_t)ST_INFINITY : (uint8_t)ST_OK;
 }
@@ -335,6 +372,191 @@ __global__ void __launch_bounds__(256) k_recover_verdict(size_t n_rounds, const 
   if (r >= n_rounds || !ok[r] || rec_st[r] == ST_OK) return;
   ok[r] = 0;
   for (int k = 0; k < 96; ++k) out96[r * 96 + k] = 0;
+}
+
+// ================================================================ batched check
+// Window table of the share keys for the batched check: entry (i, m) =
+// [m + 1] PubPoly.Eval(i) affine, i < n (AoS: x limbs then y limbs), from
+// the (-x, y) Eval table; an identity Eval (y = 0 marks it: G1 has no 2-torsion)
+// stores zeros.  One thread per entry, once per group (dgpu_set_group).
+constexpr int REC_WTAB_WORDS = 2 * FP_LIMBS;
+__global__ void k_pubpoly_wtable(int n, const uint32_t* __restrict__ table, uint32_t* __restrict__ wtab) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= 8 * n) return;
+  const int i = g >> 3;
+  const uint32_t k = (uint32_t)(g & 7) + 1;
+  const fp nx = ld_fp(table, n, i), y = ld_fp(table + FP_LIMBS * n, n, i);
+  g1a a{fp_zero(), fp_zero()};
+  if (!fp_is_zero(y)) {
+    const g1j q = g1_mul_words(g1j{fp_neg(nx), y, fp_one()}, &k, 1);
+    if (!g1_is_inf(q)) a = g1_to_affine(q);
+  }
+  uint32_t* o = wtab + (size_t)g * REC_WTAB_WORDS;
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) {
+    o[l] = a.x.l[l];
+    o[FP_LIMBS + l] = a.y.l[l];
+  }
+}
+
+// Per round: the candidates = the first t partials that decode (status
+// ST_OK after k_decode_partials), in input order, duplicates included (the
+// reference counts every verified partial towards t), and the class:
+//   fewer than t candidates      -> REC_FAIL (the reference finds fewer than t
+//                                   good ones whatever the pairings say)
+//   t candidates, an index twice -> REC_FAIL if nothing decodable is left,
+//                                   else REC_EXACT (validity decides which)
+//   t distinct candidates        -> REC_RLC (batched check), ok = 1 for now
+// with want_status every round whose per-partial statuses need pairings
+// (decodable partials that are not checked candidates) goes REC_EXACT.
+__global__ void __launch_bounds__(64) k_recover_cand(size_t n_rounds, size_t m, int t, int want_status,
+                                                     const uint32_t* __restrict__ idx,
+                                                     const uint8_t* __restrict__ status, uint32_t* __restrict__ sel,
+                                                     uint32_t* __restrict__ xs, uint8_t* __restrict__ cls,
+                                                     uint8_t* __restrict__ ok, uint8_t* __restrict__ out96) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rounds) return;
+  uint32_t ids[RECOVER_MAX_T];
+  uint32_t* sl = sel + r * RECOVER_MAX_T;
+  int cnt = 0;
+  bool more = false;
+  for (size_t j = 0; j < m; ++j) {
+    const size_t item = r * m + j;
+    if (status[item] != ST_OK) continue;
+    if (cnt == t) {
+      more = true;
+      break;
+    }
+    sl[cnt] = (uint32_t)item;
+    ids[cnt] = idx[item];
+    ++cnt;
+  }
+  bool distinct = cnt == t;
+  for (int a = 0; a < cnt && distinct; ++a)
+    for (int b = 0; b < a; ++b) distinct = distinct && ids[a] != ids[b];
+  uint8_t c;
+  if (cnt < t)
+    c = (want_status && cnt > 0) ? REC_EXACT : REC_FAIL;
+  else if (!distinct)
+    c = (more || want_status) ? REC_EXACT : REC_FAIL;
+  else
+    c = (want_status && more) ? REC_EXACT : REC_RLC;
+  if (c == REC_RLC)
+    for (int k = 0; k < t; ++k) xs[r * RECOVER_MAX_T + k] = ids[k] + 1;
+  cls[r] = c | (more ? REC_MORE : 0);
+  ok[r] = c == REC_RLC ? 1 : 0;
+  if (c == REC_FAIL)
+    for (int k = 0; k < 96; ++k) out96[r * 96 + k] = 0;
+}
+
+// The batched check's G1 side, per REC_RLC round: A = C_0 + sum_j r_j
+// Eval(i_j) (Straus, signed radix-16 windows over the group's window table,
+// the same operation sequence in every lane), stored as the engine's pair-0
+// key (-x, y); rec_st combines A with B's identity flag from
+// k_recover_finish (both identity: trivially equal; one: fails).  A
+// candidate index without a table entry (i >= n) sends the round REC_EXACT.
+__global__ void __launch_bounds__(64) k_recover_rlc_g1(size_t n_rounds, int t, int n_group,
+                                                       const uint32_t* __restrict__ sel,
+                                                       const uint32_t* __restrict__ idx,
+                                                       const uint64_t* __restrict__ digits,
+                                                       const uint32_t* __restrict__ wtab,
+                                                       const uint32_t* __restrict__ commits, uint8_t* __restrict__ cls,
+                                                       uint8_t* __restrict__ ok, uint32_t* __restrict__ rec_pk,
+                                                       uint8_t* __restrict__ rec_st) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rounds || (cls[r] & 0x0F) != REC_RLC) return;
+  const uint32_t* sl = sel + r * RECOVER_MAX_T;
+  const uint64_t* d = digits + r * RECOVER_MAX_T * RECOVER_SLOTS + 4;
+  bool table_ok = true;
+  for (int j = 0; j < t; ++j) table_ok = table_ok && idx[sl[j]] < (uint32_t)n_group;
+  if (!table_ok) {
+    cls[r] = (uint8_t)((cls[r] & REC_MORE) | REC_EXACT);
+    ok[r] = 0;
+    rec_st[r] = ST_DECODE;
+    return;
+  }
+  g1j acc = g1_infinity();
+#pragma unroll 1
+  for (int w = 16; w >= 0; --w) {
+    if (w < 16) {
+#pragma unroll 1
+      for (int s = 0; s < 4; ++s) acc = g1_dbl_body(acc);
+    }
+#pragma unroll 1
+    for (int j = 0; j < t; ++j) {
+      const int dg = win4_digit64(d[RECOVER_SLOTS * j], w);
+      const int mag = dg < 0 ? -dg : dg;
+      const uint32_t* e = wtab + ((size_t)idx[sl[j]] * 8 + ((mag - 1) & 7)) * REC_WTAB_WORDS;
+      g1a q;
+#pragma unroll
+      for (int l = 0; l < FP_LIMBS; ++l) {
+        q.x.l[l] = e[l];
+        q.y.l[l] = e[FP_LIMBS + l];
+      }
+      const bool qinf = fp_is_zero(q.y);
+      q.y = fp_cmov(q.y, fp_neg(q.y), dg < 0);
+      acc = g1_cmov(acc, g1_add_affine_body(acc, q), mag != 0 && !qinf);
+    }
+  }
+  const g1a c0{ld_fp(commits, t, 0), ld_fp(commits + FP_LIMBS * t, t, 0)};
+  acc = g1_add_affine_body(acc, c0);
+  const bool ainf = g1_is_inf(acc);
+  const bool binf = rec_st[r] == ST_INFINITY;
+  const g1a a = ainf ? g1a{fp_zero(), fp_zero()} : g1_to_affine(acc);
+  st_fp(rec_pk, n_rounds, r, fp_neg(a.x));
+  st_fp(rec_pk + FP_LIMBS * n_rounds, n_rounds, r, a.y);
+  rec_st[r] = (ainf && binf) ? RLC_TRIVIAL : (ainf || binf) ? (uint8_t)ST_PAIRING : (uint8_t)ST_OK;
+}
+
+// The batched check's verdict per REC_RLC round: pass -> recovered (out96
+// already holds sigma); fail -> REC_EXACT when a decodable partial is left
+// beyond the candidates (the reference walks on to it), else a failure.
+__global__ void __launch_bounds__(256) k_recover_rlc_verdict(size_t n_rounds, const uint8_t* __restrict__ rec_st,
+                                                             uint8_t* __restrict__ cls, uint8_t* __restrict__ ok,
+                                                             uint8_t* __restrict__ out96) {
+  const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rounds || (cls[r] & 0x0F) != REC_RLC) return;
+  if (rec_st[r] == ST_OK || rec_st[r] == RLC_TRIVIAL) return;
+  ok[r] = 0;
+  if (cls[r] & REC_MORE) {
+    cls[r] = REC_MORE | REC_EXACT;
+    return;
+  }
+  cls[r] = REC_FAIL;
+  for (int k = 0; k < 96; ++k) out96[r * 96 + k] = 0;
+}
+
+// Rounds list[0..nx) of a recovery batch -> a compact batch (messages,
+// partial slots, lengths): one thread per (round, slot).
+__global__ void __launch_bounds__(256) k_gather_rounds(size_t nx, const uint32_t* __restrict__ list, size_t m,
+                                                       size_t stride, const uint8_t* __restrict__ msgs,
+                                                       const uint8_t* __restrict__ parts,
+                                                       const uint32_t* __restrict__ plen, uint8_t* __restrict__ x_msgs,
+                                                       uint8_t* __restrict__ x_parts, uint32_t* __restrict__ x_plen) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nx * m) return;
+  const size_t k = g / m, j = g % m, r = list[k];
+  const uint8_t* src = parts + (r * m + j) * stride;
+  uint8_t* dst = x_parts + g * stride;
+  for (size_t b = 0; b < stride; ++b) dst[b] = src[b];
+  x_plen[g] = plen[r * m + j];
+  if (j == 0)
+    for (int b = 0; b < 32; ++b) x_msgs[k * 32 + b] = msgs[r * 32 + b];
+}
+
+// The compact batch's results back to their rounds (status optional).
+__global__ void __launch_bounds__(256) k_scatter_rounds(size_t nx, const uint32_t* __restrict__ list, size_t m,
+                                                        const uint8_t* __restrict__ x_out, const uint8_t* __restrict__ x_ok,
+                                                        const uint8_t* __restrict__ x_st, uint8_t* __restrict__ out96,
+                                                        uint8_t* __restrict__ ok, uint8_t* __restrict__ status) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nx * m) return;
+  const size_t k = g / m, j = g % m, r = list[k];
+  if (status) status[r * m + j] = x_st[g];
+  if (j == 0) {
+    ok[r] = x_ok[k];
+    for (int b = 0; b < 96; ++b) out96[r * 96 + b] = x_out[k * 96 + b];
+  }
 }
 
 }  // namespace dgpu

@@ -64,19 +64,19 @@ class MultiThresholdGroup:
     def close(self):
         self.mctx.close()
 
-    def recover_batch(self, msgs, partials):
-        """As ThresholdGroup.recover_batch: (sigs or None per round, per-partial validity)."""
+    def recover_batch(self, msgs, partials, statuses=True):
+        """As ThresholdGroup.recover_batch: (sigs or None per round, per-partial validity or None)."""
         nr = len(msgs)
         if nr == 0:
             return [], []
         mb, buf, plen, m, stride = pack_partials(msgs, partials)
-        return self.recover_records(mb, buf, plen, partials)
+        return self.recover_records(mb, buf, plen, partials, statuses)
 
-    def recover_records(self, mb, buf, plen, partials=None):
+    def recover_records(self, mb, buf, plen, partials=None, statuses=False):
         nr, m, stride = buf.shape
         out = np.zeros(nr * 96, dtype=np.uint8)
         ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
-        pv = np.zeros(nr * m, dtype=np.uint8)
+        pv = np.zeros(nr * m, dtype=np.uint8) if statuses else None
         _lib.check(self.mctx.lib.dgpu_recover_multi(self.mctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
                                                     _lib.ptr(plen), _lib.ptr(out), _lib.ptr(ok), _lib.ptr(pv)))
         if partials is None:

@@ -54,6 +54,8 @@ def unpack_recovered(out, ok, pv, partials, m):
     nr = len(partials)
     okb = np.unpackbits(ok, bitorder="little")[:nr]
     sigs = [bytes(out[96 * r:96 * (r + 1)]) if okb[r] else None for r in range(nr)]
+    if pv is None:
+        return sigs, None
     valid = [[bool(pv[r * m + j]) for j in range(len(partials[r]))] for r in range(nr)]
     return sigs, valid
 
@@ -80,18 +82,20 @@ class ThresholdGroup:
             _lib.check(self.ctx.lib.dgpu_set_group(self.ctx.handle, self.t, self.n, _lib.ptr(buf)))
             ThresholdGroup._active = key
 
-    def recover_batch(self, msgs, partials):
+    def recover_batch(self, msgs, partials, statuses=True):
         """msgs: list of 32-byte messages (DigestMessage of each round);
         partials: list (per round) of lists of partial signatures (bytes).
         Returns (sigs, valid): sigs[r] = 96-byte recovered signature or None
-        (the reference's error), valid[r][j] = partial j verified."""
+        (the reference's error), valid[r][j] = partial j verified.  With
+        statuses=False valid is None and the library verifies each round's
+        candidates with one batched pairing (recover.cuh)."""
         nr = len(msgs)
         if nr == 0:
             return [], []
         mb, buf, plen, m, stride = pack_partials(msgs, partials)
         out = np.zeros(nr * 96, dtype=np.uint8)
         ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
-        pv = np.zeros(nr * m, dtype=np.uint8)
+        pv = np.zeros(nr * m, dtype=np.uint8) if statuses else None
         with ThresholdGroup._lock:
             self._install()
             _lib.check(self.ctx.lib.dgpu_recover_batch(self.ctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
@@ -101,7 +105,7 @@ class ThresholdGroup:
     def recover(self, msg, sigs):
         """key.Scheme.Recover(pub, msg, sigs, t, n): the recovered 96-byte
         signature, or RecoverError."""
-        out, _ = self.recover_batch([msg], [list(sigs)])
+        out, _ = self.recover_batch([msg], [list(sigs)], statuses=False)
         if out[0] is None:
             raise RecoverError("share: not enough good public shares to reconstruct secret commitment")
         return out[0]

@@ -155,3 +155,74 @@ def test_gpu_recover_device_entry_point_bench_batch():
     assert (ok == expect_ok).all()
     assert (out[ok] == expect[ok]).all() and not out[~ok].any()
     assert ((st != 0).sum(axis=1) == (~expect_ok).astype(int)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FIXTURES)
+def test_gpu_recover_batched_check_matches_fixtures(name):
+    """Without per-partial statuses the library checks each round's first t
+    decodable partials and the recovered signature with one pairing
+    (recover.cuh, batched check) and sends the undecided rounds down the
+    exact per-partial path: recovered bytes and failures equal the fixture
+    for every case kind (bad partials, duplicates, short ones, index >= n)."""
+    from drand_amd.threshold import ThresholdGroup
+    g = load_golden(name)
+    grp = ThresholdGroup([bytes.fromhex(c) for c in g["commits"]], g["n"])
+    msgs = [bytes.fromhex(c["msg"]) for c in g["cases"]]
+    parts = [[bytes.fromhex(p) for p in c["partials"]] for c in g["cases"]]
+    sigs, valid = grp.recover_batch(msgs, parts, statuses=False)
+    assert valid is None
+    assert [s.hex() if s else None for s in sigs] == [c["recovered"] for c in g["cases"]]
+
+
+def _cancelling_partials(t=3, n=8, seed=3):
+    """Partials whose errors cancel in the Lagrange combination: sig_1 + l_2 D
+    and sig_2 - l_1 D (l_j the Lagrange coefficients of the chosen indices),
+    so sum_j l_j sig_j is still the group signature, yet both partials fail
+    VerifyPartial and the reference (chain/beacon/chain.go:160 -> Recover)
+    skips them."""
+    import hashlib
+    co = D.share_poly(seed, t)
+    msg = hashlib.sha256(b"drand-mi355x/cancel").digest()
+    idx = [1, 4, 6, 2, 7]
+    parts = [D.partial_sign(i, D.poly_eval(co, i + 1), msg) for i in idx]
+    lam = D.lagrange_at_zero([i + 1 for i in idx[:t]])
+    Dp = B.g2_mul(B.G2_GEN, 0x1234567)
+    s1 = B.g2_add(B.g2_decompress(parts[0][2:]), B.g2_mul(Dp, lam[1]))
+    s2 = B.g2_add(B.g2_decompress(parts[1][2:]), B.g2_neg(B.g2_mul(Dp, lam[0])))
+    parts[0] = parts[0][:2] + B.g2_compress(s1)
+    parts[1] = parts[1][:2] + B.g2_compress(s2)
+    return co, msg, parts
+
+
+def test_cancelling_partials_fail_the_reference():
+    """CPU: the crafted set recovers the group signature under plain
+    interpolation, but the reference's walk rejects both bad partials."""
+    co, msg, parts = _cancelling_partials()
+    cpts = [B.g1_decompress(c) for c in D.pub_poly_commits(co)]
+    sig = B.sign_g2(co[0], msg)
+    lam = D.lagrange_at_zero([struct.unpack(">H", p[:2])[0] + 1 for p in parts[:3]])
+    acc = None
+    for lj, p in zip(lam, parts[:3]):
+        acc = B.g2_add(acc, B.g2_mul(B.g2_decompress(p[2:]), lj))
+    assert B.g2_compress(acc) == sig                      # the errors cancel
+    assert D.recover(cpts, msg, parts[:3], 3, 8) is None  # yet the reference fails the round
+    assert D.recover(cpts, msg, parts, 3, 8) == sig       # and recovers from the three good ones
+
+
+@pytest.mark.gpu
+def test_gpu_recover_cancelling_partials_rejected():
+    """GPU, batched check: the random coefficients expose the cancelling
+    errors (the round with only these three partials fails like the
+    reference); with two more good partials the round recovers through the
+    exact path; per-partial statuses mark exactly the two crafted ones."""
+    from drand_amd.threshold import ThresholdGroup
+    co, msg, parts = _cancelling_partials()
+    grp = ThresholdGroup(D.pub_poly_commits(co), 8)
+    sig = B.sign_g2(co[0], msg)
+    for _ in range(3):  # fresh coefficients per call
+        got, _ = grp.recover_batch([msg, msg], [parts[:3], parts], statuses=False)
+        assert got == [None, sig]
+    got, valid = grp.recover_batch([msg, msg], [parts[:3], parts], statuses=True)
+    assert got == [None, sig]
+    assert valid == [[False, False, True], [False, False, True, True, True]]

@@ -9,7 +9,7 @@ mkdir -p $O
 step() { echo "== $1 $(date +%T)"; }
 if [ -z "$NOTEST" ]; then
 step pytest
-timeout -k 10 720 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1
+timeout -k 10 720 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log
 [ $rc -ne 0 ] && exit $rc
 step smoke

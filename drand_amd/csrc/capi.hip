@@ -1437,7 +1437,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   if ((rc = eng_pairing_locked(c, consts, n_rounds, h, rpts, rst, s, n_rounds, nullptr, rpk))) return rc;
   mark(c, s, "recover_verdict");
   hipLaunchKernelGGL(k_recover_rlc_verdict, dim3(grid_for(n_rounds, 256)), dim3(256), 0, s, n_rounds,
-                     (const uint8_t*)rst, cls, d_ok, d_out);
+                     d_status ? 1 : 0, (const uint8_t*)rst, cls, d_ok, d_out);
   HIP_TRY(hipGetLastError());
   if (d_status) HIP_TRY(hipMemcpyAsync(d_status, st, items, hipMemcpyDeviceToDevice, s));
   // rounds left to the exact path

@@ -510,15 +510,17 @@ __global__ void __launch_bounds__(64) k_recover_rlc_g1(size_t n_rounds, int t, i
 
 // The batched check's verdict per REC_RLC round: pass -> recovered (out96
 // already holds sigma); fail -> REC_EXACT when a decodable partial is left
-// beyond the candidates (the reference walks on to it), else a failure.
-__global__ void __launch_bounds__(256) k_recover_rlc_verdict(size_t n_rounds, const uint8_t* __restrict__ rec_st,
+// beyond the candidates (the reference walks on to it) or the per-partial
+// statuses are wanted (which candidate failed), else a failure.
+__global__ void __launch_bounds__(256) k_recover_rlc_verdict(size_t n_rounds, int want_status,
+                                                             const uint8_t* __restrict__ rec_st,
                                                              uint8_t* __restrict__ cls, uint8_t* __restrict__ ok,
                                                              uint8_t* __restrict__ out96) {
   const size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n_rounds || (cls[r] & 0x0F) != REC_RLC) return;
   if (rec_st[r] == ST_OK || rec_st[r] == RLC_TRIVIAL) return;
   ok[r] = 0;
-  if (cls[r] & REC_MORE) {
+  if ((cls[r] & REC_MORE) || want_status) {
     cls[r] = REC_MORE | REC_EXACT;
     return;
   }

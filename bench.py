@@ -32,6 +32,7 @@ import ctypes
 import gc
 import json
 import os
+import struct
 import subprocess
 import sys
 import time
@@ -64,6 +65,8 @@ def parse(argv=None):
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the configs[3] / configs[4] / multi_abi legs of the default run")
     ap.add_argument("--leg-steps", type=int, default=2, help="timed steps of each extra leg")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the bolt-store check-chain ingest leg")
+    ap.add_argument("--ingest-rounds", type=int, default=1_000_000)
     ap.add_argument("--mode", choices=["per-round", "rlc", "recover"], default="per-round",
                     help="per-round: configs[1] / the metric; rlc: configs[2] (random linear combination + "
                          "bisection); recover: configs[4] (t-of-n threshold recovery, n=32, t=17)")
@@ -141,10 +144,26 @@ STAGE_WORK = {
     # RLC: the per-round stages only (node checks are data-dependent: 1 at 0% corruption)
     "rlc": {"rlc_hash_to_g2_raw": "rlc_hash_to_g2_raw", "decode_g2": "k_decode_g2_sigs+subgroup",
             "rlc_leaves_tree": "rlc_leaves_tree"},
-    # recovery: items = partials + rounds of engine checks
+    # recovery (batched check): per round, one pairing check and the MSMs
     "recover": {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv",
-                "eng_fe": "k_eng_fe"},
+                "eng_fe": "k_eng_fe", "recover_msm": "recover_msm", "recover_rlc_g1": "recover_rlc_g1"},
 }
+
+
+def recover_work(t, slices=5):
+    """Per-round v_mad_u64_u32 of the recovery MSM kernels, composed from the
+    counted group-law ops (profiles/op_counts.json group_ops) along the code's
+    operation sequence (recover.cuh): k_recover_msm_w4, per slice, a table
+    [1..8] sig_j (1 doubling + 6 mixed additions per point) then 17 signed
+    radix-16 windows of 4 doublings (16 of them) + t full additions; k_recover_rlc_g1
+    64 G1 doublings + 17 t mixed additions + C_0."""
+    go = _load_json("profiles", "op_counts.json").get("group_ops")
+    if not go:
+        return {}
+    m = lambda k: go[k]["mads"]  # noqa: E731
+    slice_mads = t * (m("g2_dbl") + 6 * m("g2_add_affine")) + 64 * m("g2_dbl") + 17 * t * m("g2_add")
+    g1 = 64 * m("g1_dbl") + (17 * t + 1) * m("g1_add_affine")
+    return {"recover_msm": {"mads": slices * slice_mads}, "recover_rlc_g1": {"mads": g1}}
 # stage -> kernel symbol for the traffic lookup
 STAGE_KERNEL = {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
                 "eng_lines_fixed": "k_eng_lines_fixed", "hash_to_g2": "hash_to_g2", "decode_g2": "k_decode_g2_sigs",
@@ -166,7 +185,7 @@ def traffic_for(kern, items):
     return None, None
 
 
-def roofline_for(stage_ms, items, pipeline="g2", stage_items=None):
+def roofline_for(stage_ms, items, pipeline="g2", stage_items=None, extra_work=None):
     """Roofline of the dominant stage (largest summed launch time among the
     stages with a work figure; chunked stages are summed over their
     launches): achieved = algorithmic v_mad_u64_u32 products over the launches
@@ -178,6 +197,7 @@ def roofline_for(stage_ms, items, pipeline="g2", stage_items=None):
         return None
     wmap = STAGE_WORK[pipeline]
     work = dict(hash_work(), **engine_work())
+    work.update(extra_work or {})
     have = {s: t for s, t in stage_ms.items() if s in wmap and wmap[s] in work and t > 0}
     if not have:
         return None
@@ -191,7 +211,9 @@ def roofline_for(stage_ms, items, pipeline="g2", stage_items=None):
     out = {"bound": "valu-int32", "unit": "T mad_u64_u32/s", "kernel": key, "stage": name, "launch_ms_total": ms,
            "items": it, "peak": PEAK_MAD_U64_PER_S / 1e12, "achieved": achieved / 1e12,
            "frac": achieved / PEAK_MAD_U64_PER_S, "traffic": None, "work_per_item_mads": per_item,
-           "work_source": "profiles/engine_work.json" if key in engine_work() else "profiles/op_counts.json"}
+           "work_source": ("profiles/engine_work.json" if key in engine_work() else
+                           "profiles/op_counts.json group_ops (bench.recover_work)" if key in (extra_work or {}) else
+                           "profiles/op_counts.json")}
     out["stage_frac"] = {s: stage_items.get(s, items) * work[wmap[s]]["mads"] / (t * 1e-3) / PEAK_MAD_U64_PER_S
                          for s, t in have.items()}
     traffic, src = traffic_for(STAGE_KERNEL.get(name, key), it)
@@ -324,9 +346,10 @@ def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
            "stage_ms": stage_ms, "verdict_mismatches": int(mism_t.item()),
            "unrecoverable_rounds_rank0": int((~expect_ok).sum()), "gen_s": t_gen}
     if rank == 0:
-        res["roofline"] = roofline_for(stage_ms, n * (m + 1), "recover")
+        res["roofline"] = roofline_for(stage_ms, n, "recover", extra_work=recover_work(args.t))
         if res["roofline"]:
-            res["roofline"]["items_note"] = "pairing checks per pass (engine items)"
+            res["roofline"]["items_note"] = ("rounds per pass (the batched check: one pairing and the MSMs per "
+                                             "round; rounds on the exact path add engine items)")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
@@ -338,6 +361,78 @@ def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
         res["cpu_baseline"] = cpu
     del d_msgs, d_parts, d_plen, d_out, d_ok
     return res
+
+
+# ---------------------------------------------------------------- check-chain ingest
+def _hex_rows(a, lens):
+    """numpy (n, stride) bytes -> lowercase hex of each row's first lens[i] bytes"""
+    table = np.frombuffer(b"".join(b"%02x" % v for v in range(256)), dtype=np.uint8).reshape(256, 2)
+    hx = table[a].reshape(a.shape[0], -1)
+    return [bytes(hx[i, :2 * int(lens[i])]) for i in range(a.shape[0])]
+
+
+def ingest_leg(chain, n_rows, scheme, window=1 << 18):
+    """The bulk check-chain path end to end from a drand bolt store: n_rows
+    rounds of the bench chain written (outside the timed region, with the
+    test writer tests/bolt_writer.py) as Beacon.Marshal rows keyed by
+    RoundToBytes (chain/boltdb/store.go:72-86), then CheckPastBeacons
+    (chain/beacon/sync_manager.go:171-232) timed over the file: native B+tree
+    walk + hexjson decode of each window overlapped with the GPU verify of the
+    previous one (drand_amd/sync.py, drand_amd/ingest.py)."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from bolt_writer import write_bolt
+    from drand_amd import ingest
+    from drand_amd.boltstore import BoltStore
+    from drand_amd.chain import Verifier
+    from drand_amd.scheme import get_scheme_by_id_with_default
+    from drand_amd.sync import check_past_beacons
+    n = min(n_rows, len(chain))
+    t0 = time.perf_counter()
+    sig_hex = _hex_rows(chain.sigs[:n], chain.sig_len[:n])
+    prev_hex = _hex_rows(chain.prev[:n], chain.prev_len[:n])
+    kv = {struct.pack(">Q", 0): b'{"PreviousSig":null,"Round":0,"Signature":"' + chain.genesis.hex().encode() + b'"}'}
+    for i in range(n):
+        r = int(chain.rounds[i])
+        p = b'"' + prev_hex[i] + b'"' if chain.prev_len[i] else b"null"
+        kv[struct.pack(">Q", r)] = (b'{"PreviousSig":' + p + b',"Round":' + str(r).encode() + b',"Signature":"' +
+                                   sig_hex[i] + b'"}')
+    del sig_hex, prev_hex
+    d = tempfile.mkdtemp(prefix="drand_ingest_")
+    path = os.path.join(d, "drand.db")
+    write_bolt(path, kv)
+    del kv
+    t_write = time.perf_counter() - t0
+    log(f"ingest: {n}-round bolt file written in {t_write:.1f} s")
+    bs = BoltStore(path)
+    v = Verifier(get_scheme_by_id_with_default(scheme))
+    try:
+        check_past_beacons(bs, v, chain.pk, 1 << 16, window=1 << 16)  # warm: key decode, buffers, page cache
+        t0 = time.perf_counter()
+        faulty = check_past_beacons(bs, v, chain.pk, 10 ** 12, window=window)
+        el = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for lo in range(1, n + 1, window):
+            ingest.window_records(bs, lo, min(n + 1, lo + window))
+        t_dec = time.perf_counter() - t0
+        expect = [int(chain.rounds[i]) for i in range(n) if not _valid_by_construction(chain, i)]
+        res = {"value": n / el, "unit": "rounds/s", "rounds": n, "seconds": el, "window": window,
+               "faulty_rounds": len(faulty or []), "faulty_equal_construction": (faulty or []) == expect,
+               "decode_only_rounds_per_s": n / t_dec, "file_bytes": os.path.getsize(path),
+               "write_s": t_write, "decode_threads": ingest.DECODE_THREADS,
+               "api": "sync.check_past_beacons(BoltStore) -> native scan/decode -> dgpu_verify_beacons"}
+    finally:
+        bs.close()
+        os.remove(path)
+        os.rmdir(d)
+    return res
+
+
+_EXPECT = {}
+
+
+def _valid_by_construction(chain, i):
+    return _EXPECT.get(id(chain), {}).get(i, True)
 
 
 # ---------------------------------------------------------------- configs[1..3]
@@ -441,6 +536,13 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
                                   "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)"}
         log(f"rlc: {res['rlc']['value']:.0f} rounds/s")
 
+    if main and rank == 0 and world == 1 and not args.no_ingest:
+        _EXPECT[id(chain)] = {gi - lo: False for gi in bad if lo <= gi < hi}
+        try:
+            res["ingest"] = ingest_leg(chain, args.ingest_rounds, scheme)
+            log(f"ingest: {res['ingest']['value']:.0f} rounds/s")
+        except Exception as e:  # reported, never fatal
+            res["ingest"] = {"error": repr(e)}
     if rank == 0 and cpu_seconds and not args.no_cpu_baseline and world == 1:
         try:
             from oracle import cpu_baseline as cb
@@ -598,6 +700,7 @@ def main_verify(args, world, rank, local):
         "chain_gen_s": main["chain_gen_s"],
         "end_to_end": main.get("end_to_end"),
         "rlc": main.get("rlc"),
+        "ingest": main.get("ingest"),
         "roofline": main.get("roofline"),
         "cpu_baseline": main.get("cpu_baseline"),
     }

@@ -178,6 +178,7 @@ class BoltStore:
         if v is None:
             raise BoltFormatError(f"{path}: no bucket {bucket!r}")
         self._b = _Bucket(self, v)
+        self._buf = None
 
     def _read_meta(self, off):
         """The meta at byte offset `off` (a page start), or None if it fails
@@ -232,11 +233,42 @@ class BoltStore:
 
     def close(self):
         self._cache.clear()
-        self._mm.close()
+        self._buf = None
+        try:
+            self._mm.close()
+        except BufferError:  # arrays over the mapping still alive: it closes with them
+            pass
         self._f.close()
+
+    def buffer(self):
+        """The mapped file as a read-only uint8 array (native ingest input)."""
+        if self._buf is None:
+            import numpy as np
+            self._buf = np.frombuffer(self._mm, dtype=np.uint8)
+        return self._buf
+
+    def scan_offsets(self, lo, hi):
+        """(rounds, value offsets, value lengths, buffer) of the rows with
+        lo <= round < hi in key order: the native B+tree walk over the
+        mapped file (drand_amd/ingest.py) when the bucket has its own pages,
+        else this reader's walk with the values copied into a small buffer."""
+        import numpy as np
+        from . import ingest
+        if self._b.inline is None and ingest.load() is not None:
+            rr, off, ln = ingest.scan(self.buffer(), self.page_size, self._b.root, lo, hi)
+            return rr, off, ln, self.buffer()
+        rows = list(self.scan(lo, hi))
+        ln = np.array([len(v) for _, v in rows], dtype=np.uint32)
+        off = np.concatenate([[0], np.cumsum(ln, dtype=np.uint64)[:-1]]).astype(np.uint64) if rows else \
+            np.zeros(0, dtype=np.uint64)
+        buf = np.frombuffer(b"".join(v for _, v in rows) or b"\0", dtype=np.uint8)
+        return np.array([r for r, _ in rows], dtype=np.uint64), off, ln, buf
 
     # ---- chain.Store (read side)
     def len(self):
+        from . import ingest
+        if self._b.inline is None and ingest.load() is not None:
+            return ingest.count(self.buffer(), self.page_size, self._b.root)
         return self._b.key_n()
 
     def last(self):

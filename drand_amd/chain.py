@@ -159,6 +159,14 @@ class Verifier:
         if n == 0:
             return np.zeros(0, dtype=np.uint8)
         rounds, sigs, sig_len, prev, prev_len = pack_beacons(beacons)
+        return self.verify_records(pubkey, rounds, sigs, sig_len, prev, prev_len, mode, rlc_seed)
+
+    def verify_records(self, pubkey, rounds, sigs, sig_len, prev, prev_len, mode=_lib.MODE_PER_ROUND, rlc_seed=None):
+        """Fixed-stride host records (numpy, as pack_beacons builds them or
+        the native bolt ingest decodes them): DGPU_REASON_* per record."""
+        n = len(rounds)
+        if n == 0:
+            return np.zeros(0, dtype=np.uint8)
         bits = np.zeros((n + 7) // 8, dtype=np.uint8)
         reason = np.zeros(n, dtype=np.uint8)
         pk = np.frombuffer(bytes(pubkey), dtype=np.uint8).copy()

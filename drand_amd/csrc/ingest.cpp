@@ -108,45 +108,78 @@ int scan_page(scan_state& S, uint64_t pgid) {
   return 0;
 }
 
-inline int hexval(uint8_t c) {
-  if (c >= '0' && c <= '9') return c - '0';
-  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-  return -1;
-}
+// hex digit value, -1 for any other byte
+struct hex_lut {
+  int8_t v[256];
+  constexpr hex_lut() : v() {
+    for (int i = 0; i < 256; ++i) v[i] = -1;
+    for (int i = 0; i < 10; ++i) v['0' + i] = (int8_t)i;
+    for (int i = 0; i < 6; ++i) {
+      v['a' + i] = (int8_t)(10 + i);
+      v['A' + i] = (int8_t)(10 + i);
+    }
+  }
+};
+constexpr hex_lut HEX{};
 
-inline bool lit(const uint8_t*& p, const uint8_t* end, const char* s) {
-  const size_t n = strlen(s);
+inline bool lit(const uint8_t*& p, const uint8_t* end, const char* s, size_t n) {
   if ((size_t)(end - p) < n || memcmp(p, s, n)) return false;
   p += n;
   return true;
 }
+#define LIT(p, end, s) lit(p, end, s, sizeof(s) - 1)
 
 // "<hex>" or null -> out (stride bytes), *len; false = not canonical
 inline bool hex_field(const uint8_t*& p, const uint8_t* end, uint8_t* out, size_t stride, uint32_t* len) {
-  if (lit(p, end, "null")) {
+  if (LIT(p, end, "null")) {
     *len = 0;
     return true;
   }
   if (p >= end || *p != '"') return false;
-  const uint8_t* q = ++p;
-  while (q < end && *q != '"') ++q;
-  if (q >= end) return false;
-  const size_t nh = (size_t)(q - p);
-  if ((nh & 1) || nh / 2 > stride) return false;
-  for (size_t i = 0; i < nh / 2; ++i) {
-    const int a = hexval(p[2 * i]), b = hexval(p[2 * i + 1]);
-    if (a < 0 || b < 0) return false;
-    out[i] = (uint8_t)(a << 4 | b);
+  ++p;
+  size_t k = 0;
+  while (p + 1 < end) {
+    const int a = HEX.v[p[0]];
+    if (a < 0) break;
+    const int b = HEX.v[p[1]];
+    if (b < 0 || k == stride) return false;
+    out[k++] = (uint8_t)(a << 4 | b);
+    p += 2;
   }
-  *len = (uint32_t)(nh / 2);
-  p = q + 1;
+  if (p >= end || *p != '"') return false;  // odd length, a non-hex byte, or no closing quote
+  *len = (uint32_t)k;
+  ++p;
   return true;
+}
+
+// leaf elements under page pgid (bucket.Stats().KeyN counts every leaf
+// element of the bucket's tree); -1: malformed
+long count_page(const uint8_t* file, size_t file_len, size_t ps, uint64_t pgid, int depth) {
+  if (depth > 64 || pgid > (file_len - PAGE_HEADER) / ps) return -1;
+  const uint8_t* p = file + (size_t)pgid * ps;
+  const uint16_t flags = rd16(p + 8), count = rd16(p + 10);
+  if ((size_t)pgid * ps + PAGE_HEADER + (size_t)count * ELEMENT > file_len) return -1;
+  if (flags & LEAF_PAGE) return count;
+  if (!(flags & BRANCH_PAGE)) return -1;
+  long total = 0;
+  for (int i = 0; i < count; ++i) {
+    const long c = count_page(file, file_len, ps, rd64(p + PAGE_HEADER + (size_t)i * ELEMENT + 8), depth + 1);
+    if (c < 0) return -1;
+    total += c;
+  }
+  return total;
 }
 
 }  // namespace
 
 extern "C" {
+
+// bucket.Stats().KeyN of the bucket rooted at root_pgid (chain/boltdb/store.go
+// Len, :51-62); -1 for a malformed file.
+long dgpu_ingest_count(const uint8_t* file, size_t file_len, size_t page_size, uint64_t root_pgid) {
+  if (!file || page_size < 64 || file_len < 2 * page_size) return -1;
+  return count_page(file, file_len, page_size, root_pgid, 0);
+}
 
 // In-order walk of a bucket's B+tree (bbolt pages of page_size bytes in the
 // mapped file, root page root_pgid) collecting the elements whose key k
@@ -187,8 +220,8 @@ size_t dgpu_ingest_decode(size_t n, const uint8_t* base, const uint64_t* val_off
     const uint8_t* end = p + val_len[i];
     uint8_t* so = sigs + i * sig_stride;
     uint8_t* po = prev + i * prev_stride;
-    bool g = lit(p, end, "{\"PreviousSig\":") && hex_field(p, end, po, prev_stride, prev_len + i) &&
-             lit(p, end, ",\"Round\":");
+    bool g = LIT(p, end, "{\"PreviousSig\":") && hex_field(p, end, po, prev_stride, prev_len + i) &&
+             LIT(p, end, ",\"Round\":");
     uint64_t r = 0;
     if (g) {
       const uint8_t* d = p;
@@ -201,7 +234,7 @@ size_t dgpu_ingest_decode(size_t n, const uint8_t* base, const uint64_t* val_off
         else r = r * 10 + dig;
       }
     }
-    g = g && lit(p, end, ",\"Signature\":") && hex_field(p, end, so, sig_stride, sig_len + i) && lit(p, end, "}") &&
+    g = g && LIT(p, end, ",\"Signature\":") && hex_field(p, end, so, sig_stride, sig_len + i) && LIT(p, end, "}") &&
         p == end;
     if (!g) {
       memset(so, 0, sig_stride);

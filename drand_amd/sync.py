@@ -138,6 +138,8 @@ def check_past_beacons(store, verifier, pubkey, up_to, cb=None, window=1 << 16, 
     if last.round < up_to:
         up_to = last.round
     n = store.len()
+    if hasattr(store, "scan_offsets") and hasattr(verifier, "verify_records"):
+        return _check_past_records(store, verifier, pubkey, up_to, n, cb, window, cancelled, mode)
     faulty = []
     i = 1
     while i < n:
@@ -178,6 +180,53 @@ def check_past_beacons(store, verifier, pubkey, up_to, cb=None, window=1 << 16, 
             if r >= up_to:
                 return faulty or None
         i = hi
+    return faulty or None
+
+
+def _check_past_records(store, verifier, pubkey, up_to, n, cb, window, cancelled, mode):
+    """CheckPastBeacons over a BoltStore with the native ingest
+    (drand_amd/ingest.py): each window's rows are walked and decoded into
+    fixed-stride records off the Python heap -- the next window's while the
+    GPU verifies the current one (the ctypes call releases the GIL) -- and
+    replayed with the loop's exact rules: rounds visited 1 .. min(Len-1,
+    upTo); a missing or undecodable row faults its round i, a failed
+    verification the stored beacon's Round; callbacks and cancellation per
+    visited round when given."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    from .ingest import window_records
+    end = min(n, up_to + 1)  # visited rounds: [1, end)
+    if end <= 1:
+        return None
+    bounds = [(lo, min(end, lo + window)) for lo in range(1, end, window)]
+    faulty = []
+    with ThreadPoolExecutor(1) as ex:
+        nxt = ex.submit(window_records, store, *bounds[0])
+        for k in range(len(bounds)):
+            rec = nxt.result()
+            if k + 1 < len(bounds):
+                nxt = ex.submit(window_records, store, *bounds[k + 1])
+            reasons = verifier.verify_records(pubkey, rec.rounds, rec.sigs, rec.sig_len, rec.prev, rec.prev_len,
+                                              mode) if len(rec.rounds) else np.zeros(0, dtype=np.uint8)
+            # the faulty value of every visited round of the window, in order
+            size = rec.hi - rec.lo
+            val = np.zeros(size, dtype=np.uint64)
+            hit = np.zeros(size, dtype=bool)
+            hit[rec.bad] = True
+            val[rec.bad] = rec.lo + rec.bad.astype(np.uint64)
+            fail = reasons != 0
+            hit[rec.index[fail]] = True
+            val[rec.index[fail]] = rec.rounds[fail]
+            if cb is None and cancelled is None:
+                faulty.extend(val[hit].tolist())
+                continue
+            for j in range(size):
+                if cancelled is not None and cancelled():
+                    raise Cancelled()
+                if cb is not None:
+                    cb(rec.lo + j, up_to)
+                if hit[j]:
+                    faulty.append(int(val[j]))
     return faulty or None
 
 

@@ -31,6 +31,28 @@ def host_cores():
     return info
 
 
+def quota_threads(info):
+    """Threads that match the CPU time the box actually grants (the cgroup
+    quota), when that is below the affinity count."""
+    q = info.get("cgroup_quota_cores")
+    return max(1, min(info["affinity_cores"], int(q))) if q else info["affinity_cores"]
+
+
+def _quota_and_projection(out, run_k, seconds, rate_hint):
+    """Beside the all-affinity-threads figure: (a) the same sample size run on
+    quota_threads threads when a cgroup quota caps the box below its
+    affinity count (oversubscribed threads only add switching), and (b) the
+    single-core rate times every host core -- the ideal-scaling upper bound of
+    the reference's verifier with GOMAXPROCS = the host core count."""
+    out["projected_all_host_cores_value"] = out["single_core_value"] * out["host_cores"]
+    qt = quota_threads(out)
+    if qt >= out["cores"]:
+        return
+    k = int(max(qt, seconds / 2 * rate_hint))
+    _, wall, cpu_s = _timed(lambda: run_k(k))
+    out["quota_threads"] = {"threads": qt, "value": k / wall, "wall_s": wall, "effective_parallelism": cpu_s / wall}
+
+
 def _timed(fn):
     """wall and process CPU seconds (all threads) of fn()"""
     c0, t0 = time.process_time(), time.perf_counter()
@@ -85,6 +107,7 @@ def run(chain, seconds, cores, expect_valid=None):
            "cpu_s": cpu_s, "effective_parallelism": cpu_s / wall,
            "single_core_ms_per_round": per * 1e3, "single_core_value": 1.0 / per}
     out.update(host_cores())
+    _quota_and_projection(out, lambda k: verify(sub_of(pick(k)), quota_threads(out)), seconds, sample / wall)
     if expect_valid is not None:
         out["sample_verdict_mismatches"] = int(((reason == 0) != expect_valid[idx]).sum())
     return out
@@ -185,6 +208,7 @@ def run_recover(commits, t, n, msgs, parts, expect_sigs, seconds, cores):
                "effective_parallelism": cpu_s / wall, "single_core_ms_per_round": w1 * 1e3,
                "single_core_value": 1.0 / w1, "sample_mismatches": mism}
         out.update(host_cores())
+        _quota_and_projection(out, lambda k: run_idx(pick(k), quota_threads(out)), seconds, sample / wall)
         return out
     except (OSError, AttributeError):
         return _run_recover_py(commits, t, n, msgs, parts, expect_sigs, seconds, cores)

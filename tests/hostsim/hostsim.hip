@@ -162,6 +162,36 @@ int hs_count_extra(const uint8_t* msg32, const uint8_t* sig96, const uint8_t* si
 #endif
 }
 
+// Group-law op counts (DG_COUNT_OPS builds): out[2k], out[2k+1] = mul, sqr of
+// k=0 g2_dbl_body, 1 g2_add_body, 2 g2_add_affine_body, 3 g1_dbl_body,
+// 4 g1_add_affine_body, 5 g2_psi, 6 g2_to_affine -- the terms of the recovery
+// MSM's work figure (recover.cuh k_recover_msm_w4 / k_recover_rlc_g1).
+int hs_count_group_ops(const uint8_t* msg32, unsigned long long* out) {
+#ifdef DG_COUNT_OPS
+  uint32_t m[8];
+  msg_words(msg32, m);
+  const g2j P = hash_to_g2(m);
+  const g2j Q = g2_dbl(P);
+  const g2a Qa = g2_to_affine(Q);
+  const g1j G{C_G1_X, C_G1_Y, fp_one()};
+  const g1j G2x = g1_dbl(G);
+  const g1a Ga = g1_to_affine(G2x);
+#define CNT(k, expr) dg_count_mul = dg_count_sqr = 0; (void)(expr); out[2 * (k)] = dg_count_mul; out[2 * (k) + 1] = dg_count_sqr;
+  CNT(0, g2_dbl_body(Q));
+  CNT(1, g2_add_body(P, Q));
+  CNT(2, g2_add_affine_body(P, Qa));
+  CNT(3, g1_dbl_body(G));
+  CNT(4, g1_add_affine_body(G, Ga));
+  CNT(5, g2_psi(Q));
+  CNT(6, g2_to_affine(Q));
+#undef CNT
+  return 0;
+#else
+  (void)msg32; (void)out;
+  return -100;
+#endif
+}
+
 // a*b, a+b, a-b, a^2 on canonical 48-byte big-endian inputs
 int hs_fp_ops(const uint8_t* a48, const uint8_t* b48, uint8_t* mul, uint8_t* add, uint8_t* sub, uint8_t* sqr,
               uint8_t* inv) {

@@ -170,3 +170,91 @@ def test_torn_meta0_opens_from_meta1(tmp_path):
     bq = BoltStore(q)
     assert bq.txid == 1 and bq.page_size == 16384 and bq.last() == st.last()
     bq.close()
+
+
+# hexjson rows the native decoder must leave to beacon_unmarshal (or decode
+# identically): whitespace, key order and case, null fields, uppercase hex,
+# Round edge cases, escapes, odd / non-hex strings, lengths past the stride
+MALFORMED = [
+    b'{"PreviousSig":"aa","Round":5,"Signature":"bb"}',
+    b'{"PreviousSig":null,"Round":6,"Signature":"CC"}',
+    b'{"PreviousSig":"","Round":7,"Signature":null}',
+    b'{"Round":8,"PreviousSig":"aa","Signature":"bb"}',
+    b'{"previoussig":"aa","round":9,"signature":"bb"}',
+    b'{ "PreviousSig":"aa","Round":10,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":011,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":12.0,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":-13,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":18446744073709551615,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":18446744073709551616,"Signature":"bb"}',
+    b'{"PreviousSig":"a","Round":15,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":16,"Signature":"b b"}',
+    b'{"PreviousSig":"aa","Round":17,"Signature":"zz"}',
+    b'{"PreviousSig":"\\u0061a","Round":18,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":19,"Signature":"bb"}  ',
+    b'{"PreviousSig":"aa","Round":20,"Signature":"bb","Extra":1}',
+    b'{"PreviousSig":"aa","Round":21,"Round":22,"Signature":"bb"}',
+    b'{"PreviousSig":"aa","Round":23,"Signature":"bb"',
+    b'not json',
+    b'[1,2,3]',
+    b'{"PreviousSig":"' + b"ab" * 200 + b'","Round":24,"Signature":"' + b"cd" * 96 + b'"}',
+    b'{"PreviousSig":"ab","Round":25,"Signature":"' + b"cd" * 150 + b'"}',
+    b'{"PreviousSig":"ab","Round":26,"Signature":7}',
+    b'{"PreviousSig":"ab","Round":true,"Signature":"cd"}',
+    b'{}',
+    b'{"PreviousSig":"AbCd","Round":0,"Signature":"' + b"Ef" * 96 + b'"}',
+]
+
+
+def test_native_decoder_equals_beacon_unmarshal(tmp_path):
+    """The native window decode (drand_amd/ingest.py over libdrand_ingest.so)
+    gives, row for row, what beacon_unmarshal gives: the same record, or an
+    Unmarshal error for the same rows (VERDICT r02 #8)."""
+    import numpy as np
+    from drand_amd import ingest
+    from drand_amd.sync import beacon_unmarshal
+    assert ingest.load() is not None, "libdrand_ingest.so not built"
+    kv = {struct.pack(">Q", 100 + i): v for i, v in enumerate(MALFORMED)}
+    kv[struct.pack(">Q", 0)] = b'{"PreviousSig":null,"Round":0,"Signature":"00"}'
+    p = tmp_path / "drand.db"
+    write_bolt(p, kv)
+    bs = BoltStore(p)
+    rec = ingest.window_records(bs, 100, 100 + len(MALFORMED))
+    bad = set(rec.bad.tolist())
+    got = {int(j): k for k, j in enumerate(rec.index)}
+    for i, v in enumerate(MALFORMED):
+        try:
+            want = beacon_unmarshal(v)
+        except ValueError:
+            assert i in bad and i not in got, v
+            continue
+        assert i in got, v
+        k = got[i]
+        assert int(rec.rounds[k]) == want.round, v
+        sl = int(rec.sig_len[k])
+        if len(want.signature) > rec.sigs.shape[1]:
+            assert sl == 0xFFFFFFFF
+        else:
+            assert bytes(rec.sigs[k, :sl]) == want.signature and not rec.sigs[k, sl:].any(), v
+        assert bytes(rec.prev[k, :rec.prev_len[k]]) == want.previous_sig, v
+    assert len(got) + len(bad) == len(MALFORMED)
+    bs.close()
+
+
+def test_native_scan_equals_python_scan(tmp_path):
+    """The native B+tree walk returns the Python reader's rows (multi-level
+    tree, overflow pages, a missing row range at both window ends)."""
+    import numpy as np
+    from drand_amd import ingest
+    st, _ = _random_store(random.Random(7), 3000, 9000)
+    p = tmp_path / "drand.db"
+    write_bolt(p, _kv(st))
+    bs = BoltStore(p)
+    assert bs._b.inline is None
+    buf = bs.buffer()
+    for lo, hi in ((0, 3001), (1, 2), (500, 1500), (2990, 4000), (5000, 6000)):
+        rr, off, ln = ingest.scan(buf, bs.page_size, bs._b.root, lo, hi)
+        want = list(bs.scan(lo, hi))
+        assert rr.tolist() == [r for r, _ in want]
+        assert [bytes(buf[o:o + n]) for o, n in zip(off, ln)] == [v for _, v in want]
+    bs.close()

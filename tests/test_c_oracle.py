@@ -86,3 +86,30 @@ def test_recover_golden(cref):
     for case in g["cases"]:
         got = cref.recover(commits, g["t"], bytes.fromhex(case["msg"]), [bytes.fromhex(p) for p in case["partials"]])
         assert (got.hex() if got else None) == case["recovered"], case["kind"]
+
+
+def test_cpu_baseline_reports_host_view():
+    """bench.py's cpu_baseline leg on a golden chain: every affinity core as
+    threads, the host / affinity / quota core counts, the
+    single-core figure and the all-host-cores projection; verdicts equal the
+    fixture's."""
+    import numpy as np
+    from drand_amd.synth import Chain
+    from oracle import cpu_baseline as cb
+    g = load_golden("chain_chained_s1.json")
+    rows = g["rounds"]
+    n = len(rows)
+    sigs = np.zeros((n, 96), dtype=np.uint8)
+    prev = np.zeros((n, 96), dtype=np.uint8)
+    plen = np.zeros(n, dtype=np.uint32)
+    for i, r in enumerate(rows):
+        s, p = bytes.fromhex(r["sig"]), bytes.fromhex(r["prev"])
+        sigs[i, :len(s)] = np.frombuffer(s, dtype=np.uint8)
+        prev[i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+        plen[i] = len(p)
+    ch = Chain(0, bytes.fromhex(g["pk"]), np.array([r["round"] for r in rows], dtype=np.uint64), sigs,
+               np.full(n, 96, dtype=np.uint32), prev, plen, bytes.fromhex(g["genesis"]))
+    out = cb.run(ch, 0.2, 2, np.ones(n, dtype=bool))
+    assert out["kind"] == "port" and out["sample_verdict_mismatches"] == 0
+    assert out["cores"] == 2 and out["host_cores"] >= 1 and out["affinity_cores"] >= 1
+    assert out["projected_all_host_cores_value"] == pytest.approx(out["single_core_value"] * out["host_cores"])

@@ -25,6 +25,12 @@ class MarkerVerifier:
         self.calls += 1
         return np.array([3 if b.signature.startswith(b"BAD") else 0 for b in beacons], dtype=np.uint8)
 
+    def verify_records(self, pubkey, rounds, sigs, sig_len, prev, prev_len, mode=0):
+        """The fixed-stride form (native bolt ingest, drand_amd/ingest.py)."""
+        self.calls += 1
+        return np.array([3 if sig_len[i] > sigs.shape[1] or bytes(sigs[i, :3]) == b"BAD" and sig_len[i] >= 3 else 0
+                         for i in range(len(rounds))], dtype=np.uint8)
+
 
 def _random_store(rng, n):
     st = MemoryStore()

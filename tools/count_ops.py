@@ -72,8 +72,16 @@ def main():
     kernels["k_g1_batch_affine"] = ent((1, "g1_affine"))
     kernels["k_g2_batch_affine"] = ent((1, "g2_affine"))
     kernels["k_decode_g1_sigs"] = ent((1, "decode_g1"))
+    # group-law ops: the recovery MSM's work figure is composed from these
+    go = (ctypes.c_ulonglong * 14)()
+    assert L.hs_count_group_ops(msg, go) == 0
+    res_ops = {}
+    for i, name in enumerate(["g2_dbl", "g2_add", "g2_add_affine", "g1_dbl", "g1_add_affine", "g2_psi",
+                              "g2_to_affine"]):
+        mul, sqr = go[2 * i], go[2 * i + 1]
+        res_ops[name] = {"fp_mul": mul, "fp_sqr": sqr, "mads": MADS_MUL * mul + MADS_SQR * sqr}
     res = {"per_round_verify": {"fp_mul": tot_mul, "fp_sqr": tot_sqr, "stages": stages},
-           "kernels": kernels,
+           "kernels": kernels, "group_ops": res_ops,
            "unit": "per round; mads = v_mad_u64_u32 issued by the Fp multiplications (%d per mul, %d per sqr)"
                    % (MADS_MUL, MADS_SQR),
            "note": "executed algorithm of drand_amd/csrc, counted on one chained round by the host build of the "

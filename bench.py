@@ -326,6 +326,13 @@ def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
     torch.cuda.synchronize()
     stage_ms = stage_times(lib, ctx, step)
     elapsed, _ = timed(step, steps, world, dev)
+    # per-step wall times (diagnostic: host-side gaps between the kernels)
+    step_ms = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        step_ms.append((time.perf_counter() - t0) * 1e3)
 
     ok = d_ok.cpu().numpy().astype(bool)
     out = d_out.cpu().numpy()
@@ -343,7 +350,8 @@ def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
            "config": {"workload": "configs[4]: threshold recovery, n=%d, t=%d" % (args.n, args.t),
                       "rounds_total": n_total, "rounds_per_gpu": n, "partials_per_round": m, "mode": "recover",
                       "parallelism": f"shard{world}"},
-           "stage_ms": stage_ms, "verdict_mismatches": int(mism_t.item()),
+           "stage_ms": stage_ms, "stage_ms_total": sum(stage_ms.values()), "extra_step_ms": step_ms,
+           "verdict_mismatches": int(mism_t.item()),
            "unrecoverable_rounds_rank0": int((~expect_ok).sum()), "gen_s": t_gen}
     if rank == 0:
         res["roofline"] = roofline_for(stage_ms, n, "recover", extra_work=recover_work(args.t))

@@ -174,6 +174,7 @@ struct dgpu_ctx {
   // batched recovery check: the group's window table of the share keys, round
   // classes, and the compact batch of rounds that take the exact path
   DevBuf grp_wtab, rec_cls, rec_x_list, rec_x_msgs, rec_x_parts, rec_x_plen, rec_x_out, rec_x_ok, rec_x_st;
+  DevBuf rec_tab, rec_tabz, rec_tabpre;  // the batched check's shared affine window tables
   bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
@@ -883,6 +884,7 @@ void dgpu_close(dgpu_ctx* c) {
                     &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk,
                     &c->rec_st, &c->rec_sel, &c->rec_part, &c->grp_wtab, &c->rec_cls, &c->rec_x_list,
                     &c->rec_x_msgs, &c->rec_x_parts, &c->rec_x_plen, &c->rec_x_out, &c->rec_x_ok, &c->rec_x_st,
+                    &c->rec_tab, &c->rec_tabz, &c->rec_tabpre,
                     &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
                     &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->in_rounds, &c->in_sigs,
@@ -1419,10 +1421,21 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   HIP_TRY(hipGetLastError());
   mark(c, s, "recover_msm");
   {
-    auto msm = t <= 8 ? k_recover_msm_w4<8> : t <= 16 ? k_recover_msm_w4<16> : t <= 24 ? k_recover_msm_w4<24>
-                                                                                         : k_recover_msm_w4<32>;
-    hipLaunchKernelGGL(msm, dim3(grid_for(5 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t, (const uint8_t*)d_ok,
-                       (const uint32_t*)sel, (const uint64_t*)dig, (const uint32_t*)sg, items, part, 5);
+    // shared affine window tables [1..8] sig_j, then 5 slices of mixed-addition windows
+    const size_t ne = n_rounds * (size_t)t * 8;
+    if ((rc = c->rec_tab.ensure(ne * G2A_WORDS * 4)) || (rc = c->rec_tabz.ensure(ne * 2 * FP_WORDS * 4)) ||
+        (rc = c->rec_tabpre.ensure(ne * FP_WORDS * 4)))
+      return rc;
+    uint32_t* tab = (uint32_t*)c->rec_tab.p;
+    hipLaunchKernelGGL(k_recover_tables, dim3(grid_for(n_rounds * (size_t)t, 256)), dim3(256), 0, s, n_rounds, t,
+                       (const uint8_t*)d_ok, (const uint32_t*)sel, (const uint32_t*)sg, items, tab,
+                       (uint32_t*)c->rec_tabz.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((ne + 15) / 16, 256)), dim3(256), 0, s, ne, tab,
+                       (const uint32_t*)c->rec_tabz.p, (uint32_t*)c->rec_tabpre.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_recover_msm_aff, dim3(grid_for(5 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t,
+                       (const uint8_t*)d_ok, (const uint64_t*)dig, (const uint32_t*)tab, part, 5);
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_recover_finish, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, (const uint8_t*)d_ok,

@@ -335,6 +335,81 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm_w4(size_t n_rounds, int 
   st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
 }
 
+// Batched-check MSM with shared window tables.  k_recover_tables: one
+// thread per (round, candidate j) builds [1..8] sig_j once (1 doubling + 6
+// mixed additions, Jacobian; rounds not on the batched check write the
+// identity-free placeholder (0, 0, 1) so the batch inversion stays sound),
+// k_g2_batch_affine turns every entry affine, and k_recover_msm_aff's
+// `slices` threads per round (the four base-|x| slices of lambda and the RLC
+// coefficients) run their signed radix-16 windows with mixed additions over
+// the shared affine entries -- the table is built once per point instead
+// of once per slice, and every window addition is a mixed one.
+// Table layout: entry (r, j, m) = [m + 1] sig_j at index (r * t + j) * 8 + m
+// of a G2 SoA (X, Y in tab, Z in tabz).
+__global__ void __launch_bounds__(256, 2) k_recover_tables(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
+                                                        const uint32_t* __restrict__ sel,
+                                                        const uint32_t* __restrict__ sig_pts, size_t n_items,
+                                                        uint32_t* __restrict__ tab, uint32_t* __restrict__ tabz) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_rounds * (size_t)t) return;
+  const size_t r = g / t;
+  const int j = (int)(g % t);
+  const size_t N = n_rounds * (size_t)t * 8;
+  auto put = [&](int m, const g2j& p) {
+    const size_t e = g * 8 + m;
+    st_g2a(tab, N, e, g2a{p.x, p.y});
+    st_fp(tabz, N, e, p.z.c0);
+    st_fp(tabz + FP_WORDS * N, N, e, p.z.c1);
+  };
+  if (!ok[r]) {
+    const g2j ph{fp2_zero(), fp2_zero(), fp2_one()};
+#pragma unroll 1
+    for (int m = 0; m < 8; ++m) put(m, ph);
+    return;
+  }
+  const g2a q = ld_g2a(sig_pts, n_items, sel[r * RECOVER_MAX_T + j]);
+  g2j acc = g2_from_affine(q);
+  put(0, acc);
+  acc = g2_dbl_body(acc);
+  put(1, acc);
+#pragma unroll 1
+  for (int m = 2; m < 8; ++m) {
+    acc = g2_add_affine_body(acc, q);
+    put(m, acc);
+  }
+}
+
+__global__ void __launch_bounds__(256, 2) k_recover_msm_aff(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
+                                                          const uint64_t* __restrict__ digits,
+                                                          const uint32_t* __restrict__ tab,
+                                                          uint32_t* __restrict__ part, int slices) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (size_t)slices * n_rounds) return;
+  const size_t r = g / slices;
+  const int i = (int)(g % slices);
+  if (!ok[r]) return;
+  const uint64_t* d = digits + r * RECOVER_MAX_T * RECOVER_SLOTS + i;
+  const size_t N = n_rounds * (size_t)t * 8;
+  const size_t base = r * (size_t)t * 8;
+  g2j acc = g2_infinity();
+#pragma unroll 1
+  for (int w = 16; w >= 0; --w) {
+    if (w < 16) {
+#pragma unroll 1
+      for (int s = 0; s < 4; ++s) acc = g2_dbl_body(acc);
+    }
+#pragma unroll 1
+    for (int j = 0; j < t; ++j) {
+      const int dg = win4_digit64(d[RECOVER_SLOTS * j], w);
+      const int mag = dg < 0 ? -dg : dg;
+      g2a e = ld_g2a(tab, N, base + (size_t)j * 8 + ((mag - 1) & 7));
+      e.y = fp2_cmov(e.y, fp2_neg(e.y), dg < 0);
+      acc = g2_cmov(acc, g2_add_affine_body(acc, e), mag != 0);
+    }
+  }
+  st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);
+}
+
 // slices = 5 (batched check): rec_pts gets B = sigma + sum_j r_j sig_j
 // instead of sigma, and rec_st whether B is the identity.
 __global__ void __launch_bounds__(64) k_recover_finish(size_t n_rounds, const uint8_t* __restrict__ ok,

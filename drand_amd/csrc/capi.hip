@@ -21,6 +21,7 @@
 #include "pairing_engine.cuh"
 #include "recover.cuh"
 #include "g1sig.cuh"
+#include "rlc_msm.cuh"
 
 using namespace dgpu;
 
@@ -159,6 +160,9 @@ struct dgpu_ctx {
   DevBuf h_pts, sig_pts, status, h_z, h_pre, h_tmp;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
   DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st, rlc_root;
+  // RLC root by bucket MSM (rlc_msm.cuh): AoS points, flags, counts / offsets /
+  // cursors, bucket lists, bucket sums, per-run window sums
+  DevBuf msm_aos, msm_flags, msm_counts, msm_list, msm_buckets, msm_runs, msm_root;
   // pairing engine (per-round mode): per-chunk lines / f / norms
   DevBuf eng_lines, eng_f, eng_n1;
   // second lane's scratch (same roles as h_pts .. eng_n1)
@@ -364,31 +368,32 @@ struct rlc_trees {
   int top() const { return (int)sz.size() - 1; }
 };
 
-// RLC phase 1: R_i = pre-cofactor H(m_i) (affine), sig_i decoded (+ subgroup),
-// leaves P_i = r_i R_i, S_i = r_i sig_i (r_i from the seed and the batch
-// position i), segment tree of sums up to the root.  Asynchronous on s.
-int rlc_build_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+// RLC phase 1: R_i = pre-cofactor H(m_i) (affine, in rlc_tree's tail),
+// sig_i decoded (+ subgroup, required before any combination: soundness).
+// Asynchronous on s.
+uint32_t* rlc_rpts(dgpu_ctx* c, size_t n) {
+  // R_i after the two trees' levels: the layout rlc_tree_locked keeps
+  size_t total = 0;
+  for (size_t v = n;; v = (v + 1) / 2) {
+    total += v;
+    if (v <= 1) break;
+  }
+  return (uint32_t*)c->rlc_tree.p + 2 * total * G2J_WORDS;
+}
+
+int rlc_points_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s) {
   const unsigned B = 256;
   const size_t n = a.n;
-  T.sz.assign(1, n);
-  while (T.sz.back() > 1) T.sz.push_back((T.sz.back() + 1) / 2);
   size_t total = 0;
-  for (size_t v : T.sz) total += v;
+  for (size_t v = n;; v = (v + 1) / 2) {
+    total += v;
+    if (v <= 1) break;
+  }
   int rc;
   if ((rc = c->rlc_tree.ensure(2 * total * G2J_WORDS * 4 + n * G2J_WORDS * 4))) return rc;
   if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
   if ((rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
-  uint32_t* tree = (uint32_t*)c->rlc_tree.p;
-  T.P.assign(T.sz.size(), nullptr);
-  T.S.assign(T.sz.size(), nullptr);
-  size_t off = 0;
-  for (size_t l = 0; l < T.sz.size(); ++l) {
-    T.P[l] = tree + off;
-    off += T.sz[l] * G2J_WORDS;
-    T.S[l] = tree + off;
-    off += T.sz[l] * G2J_WORDS;
-  }
-  uint32_t* rpts = tree + off;
+  uint32_t* rpts = rlc_rpts(c, n);
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
   uint8_t* st = (uint8_t*)c->status.p;
   mark(c, s, "rlc_hash_to_g2_raw");
@@ -404,16 +409,91 @@ int rlc_build_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees
     HIP_TRY(hipGetLastError());
   }
   mark(c, s, "decode_g2");
-  // RLC needs subgroup-checked signatures before the leaves (soundness)
   hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
                      1, sg, st);
   HIP_TRY(hipGetLastError());
-  mark(c, s, "rlc_leaves_tree");
+  mark(c, s, "rlc_affine");
   // R_i to affine in place (X, Y slots; Z follows them in the Jacobian SoA)
   hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, rpts,
                      (const uint32_t*)(rpts + 4 * FP_WORDS * n), (uint32_t*)c->h_pre.p);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed, rpts, sg, st, T.P[0], T.S[0]);
+  return DGPU_OK;
+}
+
+// RLC root by bucket MSM (rlc_msm.cuh) into root (P then S, stride-1
+// Jacobian).  Asynchronous on s.
+int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root) {
+  const unsigned B = 256;
+  const size_t n = a.n;
+  if (n > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "RLC batch too large (%zu)", n);
+  int rc;
+  if ((rc = c->msm_aos.ensure(2 * n * MSM_AOS_WORDS * 4)) || (rc = c->msm_flags.ensure(n)) ||
+      (rc = c->msm_counts.ensure(3 * MSM_KEYS * 4)) || (rc = c->msm_list.ensure(MSM_MW * n * 4 + 4)) ||
+      (rc = c->msm_buckets.ensure(MSM_KEYS * G2J_WORDS * 4)) ||
+      (rc = c->msm_runs.ensure(2 * (size_t)MSM_MW * MSM_RUNS * G2J_WORDS * 4)))
+    return rc;
+  uint32_t* aos = (uint32_t*)c->msm_aos.p;
+  uint8_t* flags = (uint8_t*)c->msm_flags.p;
+  uint32_t* counts = (uint32_t*)c->msm_counts.p;
+  uint32_t* offsets = counts + MSM_KEYS;
+  uint32_t* cursor = offsets + MSM_KEYS;
+  uint32_t* list = (uint32_t*)c->msm_list.p;
+  mark(c, s, "rlc_root_msm");
+  hipLaunchKernelGGL(k_msm_aos, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)rlc_rpts(c, n),
+                     (const uint32_t*)c->sig_pts.p, (const uint8_t*)c->status.p, aos, flags);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemsetAsync(counts, 0, MSM_KEYS * 4, s));
+  hipLaunchKernelGGL(k_msm_count, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.seed, (const uint8_t*)flags, counts);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)counts, offsets, cursor);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_msm_scatter, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.seed, (const uint8_t*)flags, cursor,
+                     list);
+  HIP_TRY(hipGetLastError());
+  uint32_t* buckets = (uint32_t*)c->msm_buckets.p;
+  hipLaunchKernelGGL(k_msm_bucket, dim3(grid_for(MSM_KEYS, B)), dim3(B), 0, s, n, (const uint32_t*)offsets,
+                     (const uint32_t*)counts, (const uint32_t*)list, (const uint32_t*)aos, buckets);
+  HIP_TRY(hipGetLastError());
+  uint32_t* runs = (uint32_t*)c->msm_runs.p;
+  uint32_t* runs2 = runs + (size_t)MSM_MW * MSM_RUNS * G2J_WORDS;
+  hipLaunchKernelGGL(k_msm_window, dim3(grid_for((size_t)MSM_MW * MSM_RUNS, B)), dim3(B), 0, s,
+                     (const uint32_t*)buckets, runs);
+  HIP_TRY(hipGetLastError());
+  size_t len = MSM_RUNS;
+  while (len > 1) {  // pairwise tree per (MSM, window), ping-pong between the two run buffers
+    const size_t nl = (len + 1) / 2;
+    hipLaunchKernelGGL(k_g2_sum_level, dim3(grid_for((size_t)MSM_MW * nl, B)), dim3(B), 0, s, MSM_MW, len,
+                       (const uint32_t*)runs, nl, runs2);
+    HIP_TRY(hipGetLastError());
+    std::swap(runs, runs2);
+    len = nl;
+  }
+  hipLaunchKernelGGL(k_msm_root, dim3(1), dim3(64), 0, s, (const uint32_t*)runs, root, root + G2J_WORDS);
+  HIP_TRY(hipGetLastError());
+  return DGPU_OK;
+}
+
+// The segment trees of one RLC batch (leaves P_i = r_i R_i, S_i = r_i sig_i,
+// r_i from the seed and the batch position i; then sums up to the root),
+// built from rlc_points_locked's points.  Asynchronous on s.
+int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+  const unsigned B = 256;
+  const size_t n = a.n;
+  T.sz.assign(1, n);
+  while (T.sz.back() > 1) T.sz.push_back((T.sz.back() + 1) / 2);
+  uint32_t* tree = (uint32_t*)c->rlc_tree.p;
+  T.P.assign(T.sz.size(), nullptr);
+  T.S.assign(T.sz.size(), nullptr);
+  size_t off = 0;
+  for (size_t l = 0; l < T.sz.size(); ++l) {
+    T.P[l] = tree + off;
+    off += T.sz[l] * G2J_WORDS;
+    T.S[l] = tree + off;
+    off += T.sz[l] * G2J_WORDS;
+  }
+  mark(c, s, "rlc_leaves_tree");
+  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed, (const uint32_t*)rlc_rpts(c, n),
+                     (const uint32_t*)c->sig_pts.p, (const uint8_t*)c->status.p, T.P[0], T.S[0]);
   HIP_TRY(hipGetLastError());
   for (size_t l = 0; l + 1 < T.sz.size(); ++l) {
     hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(2 * T.sz[l + 1], B)), dim3(B), 0, s, T.sz[l], T.P[l], T.S[l],
@@ -462,7 +542,8 @@ int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32
 // check every node of the level with <= 64Ki nodes (a multiple of D = 5 levels
 // up from the leaves), then all descendants D levels down of each failing
 // node, to the leaves; a failing leaf is an invalid round (ST_PAIRING).
-int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hipStream_t s) {
+int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hipStream_t s,
+                       bool root_failed = false) {
   const unsigned B = 256;
   const int D = 5;
   const int top = T.top();
@@ -470,7 +551,7 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
   std::vector<uint8_t> fail;
   std::vector<uint32_t> cand{0};
   mark(c, s, "rlc_bisection");
-  if (top > 0) {
+  if (top > 0 && !root_failed) {
     int rc = rlc_check_locked(c, key, cand, 1, T.P[top], T.S[top], s, &fail);
     if (rc) return rc;
     if (!fail[0]) return DGPU_OK;  // every decodable round verifies
@@ -682,9 +763,24 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   c->n_ev = 0;
   if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
   if (a.mode == DGPU_MODE_RLC) {
+    // root first, by bucket MSM; the tree of leaves only when it fails
+    if ((rc = rlc_points_locked(c, a, s))) return rc;
+    if ((rc = c->rlc_root.ensure(2 * G2J_WORDS * 4))) return rc;
+    uint32_t* root = (uint32_t*)c->rlc_root.p;
+    if ((rc = rlc_root_msm_locked(c, a, s, root))) return rc;
+    std::vector<uint8_t> fail;
+    if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, root, root + G2J_WORDS, s, &fail))) return rc;
+    if (!fail[0] || a.n == 1) {
+      if (fail[0]) {  // one round: its leaf is the root
+        hipLaunchKernelGGL(k_rlc_mark, dim3(1), dim3(64), 0, s, (size_t)1, (const uint32_t*)c->rlc_idx.p,
+                           (const uint8_t*)c->rlc_fail.p, (uint8_t*)c->status.p);
+        HIP_TRY(hipGetLastError());
+      }
+      return DGPU_OK;
+    }
     rlc_trees T;
-    if ((rc = rlc_build_locked(c, a, s, T))) return rc;
-    return rlc_descend_locked(c, key, T, s);
+    if ((rc = rlc_tree_locked(c, a, s, T))) return rc;
+    return rlc_descend_locked(c, key, T, s, true);
   }
   const uint32_t* consts = (const uint32_t*)key->consts.p;
   const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z, &c->h_pre, &c->h_tmp, &c->eng_lines, &c->eng_f, &c->eng_n1};
@@ -887,6 +983,8 @@ void dgpu_close(dgpu_ctx* c) {
                     &c->rec_tab, &c->rec_tabz, &c->rec_tabpre,
                     &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
+                    &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs,
+                    &c->msm_root,
                     &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->in_rounds, &c->in_sigs,
                     &c->in_sig_len, &c->in_prev, &c->in_prev_len, &c->in_msgs, &c->in_msg_len, &c->out_bits,
                     &c->out_reason, &c->misc, &c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp,

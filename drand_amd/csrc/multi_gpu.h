@@ -11,10 +11,11 @@
 //    reason bytes) -- shards are multiples of 8 rounds, so the gathered
 //    bitmaps concatenate into the batch's bitmap;
 //  - RLC mode: one all-gather of the per-device RLC roots (two Jacobian G2
-//    sums, 672 bytes), summed on device 0 and checked there with a single
-//    pairing (one final exponentiation for the whole node); only when that
-//    fails does each device descend its own tree (root first) to per-round
-//    verdicts, and the bitmaps are gathered as in per-round mode.
+//    sums, 672 bytes, each computed by bucket MSM, rlc_msm.cuh), summed on
+//    device 0 and checked there with a single pairing (one final
+//    exponentiation for the whole node); only when that fails does each
+//    device build its tree of leaves and descend it (root first) to
+//    per-round verdicts, and the bitmaps are gathered as in per-round mode.
 // RCCL is loaded at dgpu_multi_open (dlopen), so the single-GPU library has
 // no link-time dependency on it.
 //
@@ -279,14 +280,17 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
     if ((r = stage_inputs_locked(c, a, s))) return r;
     if ((r = c->status.ensure(a.n))) return r;
     c->n_ev = 0;
-    if (rlc) return rlc_build_locked(c, a, s, trees[k]);
+    if (rlc) {  // the shard's points and its root by bucket MSM (the leaves wait for a failing root)
+      if ((r = rlc_points_locked(c, a, s)) || (r = c->msm_root.ensure(2 * G2J_WORDS * 4))) return r;
+      return rlc_root_msm_locked(c, a, s, (uint32_t*)c->msm_root.p);
+    }
     if ((r = verify_status_locked(c, keys[k], a, s))) return r;
     return pack_shard_locked(c, a.n, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, s);
   });
   if (rc) return rc;
   if (rlc) {
     bool all_ok = false;
-    if (D > 1) {
+    {
       // the per-device roots to every device; one check of their sum on device 0
       g2j inf = g2_infinity();
       uint32_t inf_words[G2J_WORDS];
@@ -300,10 +304,7 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
           HIP_TRY(hipMemcpyAsync(root, inf_words, sizeof inf_words, hipMemcpyHostToDevice, c->stream));
           HIP_TRY(hipMemcpyAsync(root + G2J_WORDS, inf_words, sizeof inf_words, hipMemcpyHostToDevice, c->stream));
         } else {
-          const int top = trees[k].top();
-          HIP_TRY(hipMemcpyAsync(root, trees[k].P[top], G2J_WORDS * 4, hipMemcpyDeviceToDevice, c->stream));
-          HIP_TRY(hipMemcpyAsync(root + G2J_WORDS, trees[k].S[top], G2J_WORDS * 4, hipMemcpyDeviceToDevice,
-                                 c->stream));
+          HIP_TRY(hipMemcpyAsync(root, c->msm_root.p, 2 * G2J_WORDS * 4, hipMemcpyDeviceToDevice, c->stream));
         }
       }
       std::vector<const void*> src(D);
@@ -330,7 +331,10 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
       const size_t cnt = args[k].n;
       if (cnt == 0) return DGPU_OK;
       int r;
-      if (!all_ok && (r = rlc_descend_locked(c, keys[k], trees[k], c->stream))) return r;
+      if (!all_ok) {  // this shard's tree, its own root first (D = 1: that root is the node's, known failing)
+        if ((r = rlc_tree_locked(c, args[k], c->stream, trees[k]))) return r;
+        if ((r = rlc_descend_locked(c, keys[k], trees[k], c->stream, D == 1))) return r;
+      }
       return pack_shard_locked(c, cnt, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, c->stream);
     });
     if (rc) return rc;

@@ -151,10 +151,23 @@ def test_rlc_root_first_clean_and_single_bad(gpu_ctx):
     from drand_amd import _lib
     from drand_amd.chain import Verifier
     from drand_amd.synth import corrupt, make_chain
+    import ctypes
     v = Verifier(_sch("pedersen-bls-chained"))
     c = make_chain(43, 70000, _lib.SCHEME_CHAINED, seg_len=64)
     beacons = [c.beacon(i) for i in range(len(c))]
-    assert not v.verify_reasons(beacons, c.pk, _lib.MODE_RLC).any()
+    lib = v.ctx.lib
+    _lib.check(lib.dgpu_set_profiling(v.ctx.handle, 1))
+    try:
+        assert not v.verify_reasons(beacons, c.pk, _lib.MODE_RLC).any()
+        names = (ctypes.c_char_p * 32)()
+        ms = (ctypes.c_float * 32)()
+        ns = lib.dgpu_stage_times(v.ctx.handle, ms, 32, names)
+        stages = {names[i].decode() for i in range(ns)}
+    finally:
+        _lib.check(lib.dgpu_set_profiling(v.ctx.handle, 0))
+    # the bucket-MSM root (rlc_msm.cuh) equals the tree's: a clean batch
+    # passes on it alone, without building the leaves
+    assert "rlc_root_msm" in stages and "rlc_leaves_tree" not in stages, stages
     bad = corrupt(c, 43, rate=1e-5, kinds=(3,))  # one signature of another round
     (k,) = bad.keys()
     beacons[k] = c.beacon(k)

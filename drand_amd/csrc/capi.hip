@@ -180,6 +180,10 @@ struct dgpu_ctx {
   DevBuf grp_wtab, rec_cls, rec_x_list, rec_x_msgs, rec_x_parts, rec_x_plen, rec_x_out, rec_x_ok, rec_x_st;
   DevBuf rec_tab, rec_tabz, rec_tabpre;  // the batched check's shared affine window tables
   bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
+  // DGPU_ENG_FUSED_PROBE=1 (A/B probe only): dynamic LDS padding that puts
+  // k_eng_lines and k_eng_miller at the occupancy a fused lines+Miller kernel
+  // would have (74 slots per group: 22,064 B per block, 7 blocks per CU)
+  unsigned lds_pad_lines = 0, lds_pad_miller = 0;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call (event pool;
@@ -635,12 +639,12 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                            fixed_table, lines);
       } else {
         mark(c, s, "eng_lines");
-        hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
+        hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, r0, cnt, h, h_stride, h_idx, sg,
                            pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
       }
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_miller");
-      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
+      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_miller, s, cnt, consts, lines, f, n1);
       HIP_TRY(hipGetLastError());
     }
     const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
@@ -942,6 +946,12 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");
   if (sgv && !strcmp(sgv, "decode")) c->decode_subgroup = true;
+  const char* fpv = getenv("DGPU_ENG_FUSED_PROBE");
+  if (fpv && !strcmp(fpv, "1")) {
+    const unsigned fused = (ENG_NCONST + 5 * 74) * ENG_SLOT_WORDS * 4;
+    c->lds_pad_lines = fused - ENG_LDS_SLOTS_LINES * ENG_SLOT_WORDS * 4;
+    c->lds_pad_miller = fused - ENG_LDS_SLOTS_MILLER * ENG_SLOT_WORDS * 4;
+  }
   const char* rcv = getenv("DGPU_RECOVER");
   if (rcv && !strcmp(rcv, "exact")) c->recover_exact = true;
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);

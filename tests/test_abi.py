@@ -39,3 +39,16 @@ def test_no_cpu_fallback_without_gpu():
     from drand_amd import _lib
     with pytest.raises(_lib.DrandGPUError):
         _lib.Context(0)
+
+
+def test_ingest_library_exports_its_header():
+    """libdrand_ingest.so (host-only ingest helpers) exports every symbol
+    include/drand_ingest.h declares, and drand_amd/ingest.py binds them."""
+    from drand_amd import ingest
+    txt = open(os.path.join(ROOT, "include", "drand_ingest.h")).read()
+    names = sorted(set(re.findall(r"\b(dgpu_[a-z0-9_]+)\s*\(", txt)))
+    assert names == ["dgpu_ingest_count", "dgpu_ingest_decode", "dgpu_ingest_scan"]
+    lib = ingest.load()
+    assert lib is not None, "libdrand_ingest.so not built (__graft_entry__.build())"
+    for n in names:
+        assert hasattr(lib, n), n

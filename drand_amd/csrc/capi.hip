@@ -84,9 +84,14 @@ inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && s
 // 256Ki 1.383M, 512Ki 1.394M rounds/s.
 constexpr size_t ENG_CHUNK = 524288;
 constexpr size_t ENG_CHUNK_MIN = 16384;
-// engine bytes per round and lane: line buffer + f planes + N1
+// Karabina FE state per round and lane: the planes (t, t2, m, six stored
+// values), the product of the six norms + its prefix products (k_eng_inv),
+// the flag and the fallback list entry
+constexpr size_t ENG_KB_XWORDS = (size_t)ENG_KB_PLANES * 12 * FP_LIMBS;
+constexpr size_t ENG_KB_BYTES_PER_ROUND = ENG_KB_XWORDS * 4 + 2 * (size_t)FP_LIMBS * 4 + 1 + 4;
+// engine bytes per round and lane: line buffer + f planes + N1 + Karabina state
 constexpr size_t ENG_BYTES_PER_ROUND =
-    (size_t)ENG_LINE_STEPS * FP_LIMBS * 12 * 4 + 2 * FP_LIMBS * 12 * 4 + FP_LIMBS * 4;
+    (size_t)ENG_LINE_STEPS * FP_LIMBS * 12 * 4 + 2 * FP_LIMBS * 12 * 4 + FP_LIMBS * 4 + ENG_KB_BYTES_PER_ROUND;
 // per-round G2 batches of at least this many rounds run on two lanes
 constexpr size_t LANE_MIN = 262144;
 // decoded public keys cached per context (chain/verify.go:38 passes the key per call)
@@ -96,7 +101,7 @@ constexpr int KEY_SLOTS = 8;
 // slice of the batch).  Two lanes overlap one slice's register-bound hash /
 // decode kernels with the other slice's LDS-bound pairing engine.
 struct lane_bufs {
-  DevBuf *h_pts, *sig_pts, *h_z, *h_pre, *h_tmp, *lines, *f, *n1;
+  DevBuf *h_pts, *sig_pts, *h_z, *h_pre, *h_tmp, *lines, *f, *n1, *kb;
 };
 
 // One decoded public key: the engine's block constants carry its pairing
@@ -164,9 +169,11 @@ struct dgpu_ctx {
   // cursors, bucket lists, bucket sums, per-run window sums
   DevBuf msm_aos, msm_flags, msm_counts, msm_list, msm_buckets, msm_runs, msm_root;
   // pairing engine (per-round mode): per-chunk lines / f / norms
-  DevBuf eng_lines, eng_f, eng_n1;
-  // second lane's scratch (same roles as h_pts .. eng_n1)
-  DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1;
+  DevBuf eng_lines, eng_f, eng_n1, eng_kb;
+  // second lane's scratch (same roles as h_pts .. eng_kb)
+  DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1, l2_kb;
+  bool fe_gs = false;            // DGPU_FE=gs: the Granger-Scott FE kernel instead of the Karabina chain (A/B)
+  size_t kb_inv_chain = 16;      // DGPU_KB_INV_CHAIN: norms per k_eng_inv thread in the Karabina FE (A/B)
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
@@ -595,6 +602,49 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
   return DGPU_OK;
 }
 
+// Karabina final exponentiation of one chunk (pairing_engine.cuh, DESIGN.md
+// 2b): segment 0 (easy part), then per exponentiation by |x| the 8-lane
+// compressed chain, the batched inversion of its six stored values' norms,
+// their decompression and the next 12-lane segment; last, the Granger-Scott
+// kernel for flagged items only.  kb: ENG_KB_BYTES_PER_ROUND x cap bytes.
+int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap, size_t r0, uint32_t* f,
+                     const uint32_t* n1inv, uint8_t* kb, uint8_t* st, hipStream_t s) {
+  uint32_t* xbuf = (uint32_t*)kb;  // cap is a multiple of 5: whole blocks
+  uint32_t* pbuf = xbuf + ENG_KB_XWORDS * cap;
+  uint32_t* pre = pbuf + (size_t)FP_LIMBS * cap;
+  uint32_t* fb = pre + (size_t)FP_LIMBS * cap;
+  uint8_t* flags = (uint8_t*)(fb + cap);
+  const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
+  const size_t inv_threads = std::max<size_t>(1, (cnt + c->kb_inv_chain - 1) / c->kb_inv_chain);
+  constexpr int nseg = (int)(sizeof(ENG_PROG_FEK_OFF) / sizeof(ENG_PROG_FEK_OFF[0])) - 1;
+  static_assert(nseg == 6, "segment 0 + one per exponentiation by |x|");
+  for (int seg = 0; seg < nseg; ++seg) {
+    if (seg > 0) {
+      mark(c, s, "eng_fe_chain");
+      hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
+      HIP_TRY(hipGetLastError());
+      mark(c, s, "eng_fe_kbinv");
+      hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, (const uint32_t*)xbuf, pbuf,
+                         flags);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, (const uint32_t*)pbuf,
+                         (const uint8_t*)flags);
+      HIP_TRY(hipGetLastError());
+    }
+    mark(c, s, "eng_fe");
+    hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
+                       ENG_PROG_FEK_OFF[seg + 1] - ENG_PROG_FEK_OFF[seg], seg == 0, seg == nseg - 1, cnt, r0, consts,
+                       (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_eng_fe_fb, dim3(ENG_FB_GRID), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1inv, st,
+                     (const uint8_t*)flags, (const uint32_t*)fb);
+  HIP_TRY(hipGetLastError());
+  return DGPU_OK;
+}
+
 // Per-round pairing checks on the lane-cooperative engine, chunk by chunk
 // (pairing_engine.cuh): lines -> Miller product + norm -> batch inversion ->
 // final exponentiation.  Decode verdicts in `st` stay final.
@@ -610,8 +660,10 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
   DevBuf* b_lines = L ? L->lines : &c->eng_lines;
   DevBuf* b_f = L ? L->f : &c->eng_f;
   DevBuf* b_n1 = L ? L->n1 : &c->eng_n1;
+  DevBuf* b_kb = L ? L->kb : &c->eng_kb;
   const bool need_lines = !(fixed_table && c->fused_fixed);
   int rc;
+  if (!c->fe_gs && (rc = b_kb->ensure(cap * ENG_KB_BYTES_PER_ROUND))) return rc;
   if (need_lines && (rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
   if ((rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
   if ((rc = b_n1->ensure(cap * FP_LIMBS * 4))) return rc;
@@ -651,9 +703,13 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
     mark(c, s, "eng_inv");
     hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, pre, st);
     HIP_TRY(hipGetLastError());
-    mark(c, s, "eng_fe");
-    hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
-    HIP_TRY(hipGetLastError());
+    if (c->fe_gs) {
+      mark(c, s, "eng_fe");
+      hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
+      HIP_TRY(hipGetLastError());
+    } else if ((rc = eng_fe_kb_locked(c, consts, cnt, cap, r0, f, n1, (uint8_t*)b_kb->p, st, s))) {
+      return rc;
+    }
   }
   return DGPU_OK;
 }
@@ -787,9 +843,10 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
     return rlc_descend_locked(c, key, T, s, true);
   }
   const uint32_t* consts = (const uint32_t*)key->consts.p;
-  const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z, &c->h_pre, &c->h_tmp, &c->eng_lines, &c->eng_f, &c->eng_n1};
-  const lane_bufs L1{&c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp, &c->l2_lines, &c->l2_f,
-                     &c->l2_n1};
+  const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z,     &c->h_pre, &c->h_tmp,
+                     &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb};
+  const lane_bufs L1{&c->l2_h_pts, &c->l2_sig_pts, &c->l2_h_z, &c->l2_h_pre, &c->l2_h_tmp,
+                     &c->l2_lines, &c->l2_f,      &c->l2_n1, &c->l2_kb};
   // Two lanes (streams) on the two halves of the batch once it spans more
   // than one engine chunk; lane 1 starts when lane 0's hash/decode kernels
   // are done, so its register-bound hash runs beside lane 0's LDS-bound
@@ -954,6 +1011,10 @@ int dgpu_open(int device, dgpu_ctx** out) {
   }
   const char* rcv = getenv("DGPU_RECOVER");
   if (rcv && !strcmp(rcv, "exact")) c->recover_exact = true;
+  const char* fev = getenv("DGPU_FE");
+  if (fev && !strcmp(fev, "gs")) c->fe_gs = true;
+  const char* kic = getenv("DGPU_KB_INV_CHAIN");
+  if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
@@ -991,7 +1052,7 @@ void dgpu_close(dgpu_ctx* c) {
                     &c->rec_st, &c->rec_sel, &c->rec_part, &c->grp_wtab, &c->rec_cls, &c->rec_x_list,
                     &c->rec_x_msgs, &c->rec_x_parts, &c->rec_x_plen, &c->rec_x_out, &c->rec_x_ok, &c->rec_x_st,
                     &c->rec_tab, &c->rec_tabz, &c->rec_tabpre,
-                    &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1,
+                    &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb, &c->l2_kb,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
                     &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs,
                     &c->msm_root,

@@ -34,15 +34,17 @@ struct eng_const_block {
 struct eng_lane {
   int g, k;      // group in the wave, lane in the group
   size_t i;      // chunk-local round (clamped)
+  size_t blk;    // the wave's block of 5 rounds (blockIdx.x, or a listed block: k_eng_fe_fb)
   bool valid;
 };
 
-__device__ __forceinline__ eng_lane eng_lane_id(size_t cnt) {
+__device__ __forceinline__ eng_lane eng_lane_id(size_t cnt, size_t blk) {
   const int lane = threadIdx.x & 63;
   eng_lane L;
   L.g = lane < 60 ? lane / 12 : 4;
   L.k = lane < 60 ? lane % 12 : lane - 60;
-  const size_t gi = (size_t)blockIdx.x * ENG_ROUNDS_PER_BLOCK + L.g;
+  L.blk = blk;
+  const size_t gi = blk * ENG_ROUNDS_PER_BLOCK + L.g;
   L.valid = gi < cnt;
   L.i = L.valid ? gi : cnt - 1;
   return L;
@@ -69,9 +71,10 @@ __device__ __forceinline__ fp ld_soa(const uint32_t* base, size_t stride, size_t
 // every limb access of a wave is one contiguous 240-byte segment (a
 // round-fastest SoA would scatter the 60 lanes over 12 planes, 20 bytes each).
 constexpr int ENG_WAVE_WORDS = ENG_GROUPS_PER_WAVE * 12;
-__device__ __forceinline__ size_t eng_blk_off(int planes, int plane, int g, int e) {
-  return ((size_t)blockIdx.x * planes + plane) * FP_LIMBS * ENG_WAVE_WORDS + g * 12 + e;
+__device__ __forceinline__ size_t eng_blk_off(size_t blk, int planes, int plane, int g, int e) {
+  return (blk * planes + plane) * FP_LIMBS * ENG_WAVE_WORDS + g * 12 + e;
 }
+__device__ __forceinline__ eng_lane eng_lane_id(size_t cnt) { return eng_lane_id(cnt, blockIdx.x); }
 __device__ __forceinline__ void st_blk(uint32_t* base, size_t off, const fp& a) {
 #pragma unroll
   for (int l = 0; l < FP_LIMBS; ++l) base[off + l * ENG_WAVE_WORDS] = a.l[l];
@@ -92,6 +95,7 @@ struct eng_io {
   const uint32_t* table = nullptr;  // FIXED: on-G1 line table (k_eng_lines_fixed's layout)
   fp mlt{};                         // FIXED: this lane's export multiplier (P coordinate)
   bool scale = false;               // FIXED: export L.k is linear in a P coordinate
+  uint32_t* xbuf = nullptr;         // Karabina FE: LD12 / ST12 address its ENG_KB_PLANES state planes instead of fbuf
 };
 
 // The program interpreter (one inlined copy of the op interpreter per kernel).
@@ -110,13 +114,14 @@ constexpr bool ENG_COMPILED = true;
 #else
 constexpr bool ENG_COMPILED = false;
 #endif
-template <bool FIXED = false, bool CYC = false, int FAM = -1>
+// KB: LD12 / ST12 address the Karabina FE planes (io.xbuf), else fbuf.
+template <bool FIXED = false, bool CYC = false, int FAM = -1, bool KB = false>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
   auto sink = [&](uint32_t e, const fp& v) {
     if (!L.valid) return;
-    if (e < 12) st_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, (int)e), v);
+    if (e < 12) st_blk(io.lines, eng_blk_off(L.blk, ENG_LINE_STEPS, step, L.g, (int)e), v);
     else st_soa(io.n1, io.cnt, L.i, v);
   };
 #pragma unroll 1
@@ -144,13 +149,17 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
         if (io.scale) v = fp_mul(v, io.mlt);
         eng_st(g + (a + L.k) * ENG_SLOT_WORDS, v);
       } else {
-        eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.lines, eng_blk_off(ENG_LINE_STEPS, step, L.g, L.k)));
+        eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.lines, eng_blk_off(L.blk, ENG_LINE_STEPS, step, L.g, L.k)));
       }
       ++step;
     } else if (opc == ENG_OPC_LD12) {
-      eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k)));
+      if constexpr (KB) eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.xbuf, eng_blk_off(L.blk, ENG_KB_PLANES, (int)b / 12, L.g, L.k)));
+      else eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.fbuf, eng_blk_off(L.blk, 2, (int)b / 12, L.g, L.k)));
     } else if (opc == ENG_OPC_ST12) {
-      if (L.valid) st_blk(io.fbuf, eng_blk_off(2, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
+      if (L.valid) {
+        if constexpr (KB) st_blk(io.xbuf, eng_blk_off(L.blk, ENG_KB_PLANES, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
+        else st_blk(io.fbuf, eng_blk_off(L.blk, 2, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
+      }
     }
     asm volatile("" ::: "memory");
   }
@@ -236,7 +245,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller(size_t cnt, const u
   eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
   asm volatile("" ::: "memory");
   eng_exec<false, false, 1>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
-  if (L.valid) st_blk(fbuf, eng_blk_off(2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
+  if (L.valid) st_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 
 // ---------------------------------------------------------------- k_eng_inv
@@ -272,15 +281,17 @@ __global__ void __launch_bounds__(256) k_eng_inv(size_t cnt, size_t r0, uint32_t
 }
 
 // ---------------------------------------------------------------- k_eng_fe
-__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
-                                                      uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ n1inv,
-                                                      uint8_t* __restrict__ status) {
-  __shared__ uint32_t lds[ENG_LDS_SLOTS_FE * ENG_SLOT_WORDS];
+// The Granger-Scott FE (prog_fe) of the block `blk` of 5 rounds.
+// only != nullptr: the Karabina path's fallback -- only flagged items take a verdict.
+__device__ __forceinline__ void eng_fe_block(size_t blk, size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
+                                             uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ n1inv,
+                                             uint8_t* __restrict__ status, const uint8_t* __restrict__ only,
+                                             uint32_t* lds) {
   uint32_t* c = lds;
   eng_load_consts(c, consts);
-  const eng_lane L = eng_lane_id(cnt);
+  const eng_lane L = eng_lane_id(cnt, blk);
   uint32_t* g = lds + ENG_GBASE_FE[L.g] * ENG_SLOT_WORDS;
-  eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(2, 0, L.g, L.k)));
+  eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k)));
   if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
   asm volatile("" ::: "memory");
   eng_exec<false, ENG_CYC_FAST, 2>(ENG_PROG_FE, ENG_PROG_FE_LEN, g, c, L, eng_io{nullptr, fbuf, nullptr, cnt});
@@ -288,7 +299,179 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, 
   const bool ok = eng_eq_canon(v, L.k == 0 ? fp_one() : fp_zero());
   const uint64_t m = __ballot(ok);
   const bool all = ((m >> (12 * L.g)) & 0xFFFull) == 0xFFFull;
-  if (L.valid && L.k == 0 && !all && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_PAIRING;
+  if (L.valid && L.k == 0 && !all && (!only || only[L.i]) && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_PAIRING;
+}
+
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
+                                                      uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ n1inv,
+                                                      uint8_t* __restrict__ status) {
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_FE * ENG_SLOT_WORDS];
+  eng_fe_block(blockIdx.x, cnt, r0, consts, fbuf, n1inv, status, nullptr, lds);
+}
+
+// ---------------------------------------------------------------- Karabina FE
+// Per chunk: k_eng_fe_seg(0), then for each of the five exponentiations by
+// |x|: k_eng_kb_chain -> k_eng_kb_norm -> k_eng_inv -> k_eng_kb_dec ->
+// k_eng_fe_seg(e); finally k_eng_fe_fb re-runs the listed blocks with a
+// flagged item (f1 = 0 at a stored value: practically never) on prog_fe.
+//
+// State planes (gen_engine.py PL_*: t, t2, the exponentiation input m, the
+// six stored m^(2^s)) in fbuf's wave-blocked layout with ENG_KB_PLANES planes:
+// [block of 5 rounds][plane][limb][g * 12 + component].
+__device__ __forceinline__ size_t kb_off(size_t i, int plane, int comp) {
+  const size_t blk = i / ENG_ROUNDS_PER_BLOCK;
+  const int g = (int)(i - blk * ENG_ROUNDS_PER_BLOCK);
+  return (blk * ENG_KB_PLANES + plane) * FP_LIMBS * ENG_WAVE_WORDS + g * 12 + comp;
+}
+__device__ __forceinline__ fp2 kb_ld2(const uint32_t* xbuf, size_t i, int plane, int comp) {
+  return fp2{ld_blk(xbuf, kb_off(i, plane, comp)), ld_blk(xbuf, kb_off(i, plane, comp + 1))};
+}
+
+// Segment [off, off + len) of ENG_PROG_FEK (gen_engine.py prog_fe_kb) on the
+// 12-lane engine.  first: read f and 1/N1 as k_eng_fe does, clear the items'
+// flags and the fallback list; last: R == 1 -> verdict for unflagged items,
+// and the block joins the fallback list fb = [count, blocks...] if any of
+// its items is flagged.
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe_seg(int off, int len, bool first, bool last, size_t cnt,
+                                                          size_t r0, const uint32_t* __restrict__ consts,
+                                                          const uint32_t* __restrict__ fbuf,
+                                                          const uint32_t* __restrict__ n1inv, uint32_t* __restrict__ xbuf,
+                                                          uint8_t* __restrict__ flags, uint32_t* __restrict__ fb,
+                                                          uint8_t* __restrict__ status) {
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_FE * ENG_SLOT_WORDS];
+  uint32_t* c = lds;
+  eng_load_consts(c, consts);
+  const eng_lane L = eng_lane_id(cnt);
+  uint32_t* g = lds + ENG_GBASE_FE[L.g] * ENG_SLOT_WORDS;
+  if (first) {
+    eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k)));
+    if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
+    if (L.valid && L.k == 0) flags[L.i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) fb[0] = 0;
+  }
+  asm volatile("" ::: "memory");
+  eng_io io{nullptr, nullptr, nullptr, cnt};
+  io.xbuf = xbuf;
+  eng_exec<false, false, 2, true>(ENG_PROG_FEK + off, len, g, c, L, io);
+  if (last) {
+    const fp v = eng_ld(g + (ENG_E_R + L.k) * ENG_SLOT_WORDS);
+    const bool ok = eng_eq_canon(v, L.k == 0 ? fp_one() : fp_zero());
+    const uint64_t m = __ballot(ok);
+    const bool all = ((m >> (12 * L.g)) & 0xFFFull) == 0xFFFull;
+    const bool flagged = L.valid && flags[L.i];
+    if (L.valid && L.k == 0 && !all && !flagged && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_PAIRING;
+    if (__ballot(flagged) != 0 && threadIdx.x == 0) fb[1 + atomicAdd(fb, 1u)] = blockIdx.x;
+  }
+}
+
+// The Granger-Scott fallback over the listed blocks (fb = [count, blocks...]).
+constexpr unsigned ENG_FB_GRID = 64;
+__global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe_fb(size_t cnt, size_t r0, const uint32_t* __restrict__ consts,
+                                                         uint32_t* __restrict__ fbuf,
+                                                         const uint32_t* __restrict__ n1inv,
+                                                         uint8_t* __restrict__ status,
+                                                         const uint8_t* __restrict__ flags,
+                                                         const uint32_t* __restrict__ fb) {
+  __shared__ uint32_t lds[ENG_LDS_SLOTS_FE * ENG_SLOT_WORDS];
+  const uint32_t n = fb[0];
+  for (uint32_t q = blockIdx.x; q < n; q += gridDim.x) {
+    eng_fe_block(fb[1 + q], cnt, r0, consts, fbuf, n1inv, status, flags, lds);
+    __syncthreads();
+  }
+}
+
+static_assert(ENG_KB_COMP[0] == 2 && ENG_KB_COMP[3] == 5 && ENG_KB_COMP[4] == 8 && ENG_KB_COMP[7] == 11,
+              "kb_comp: compressed coordinates f1, f2, f4, f5");
+__device__ __forceinline__ int kb_comp(int k) { return k < 4 ? k + 2 : k + 4; }
+__device__ __forceinline__ int kb_snap(int j) {
+  static_assert(ENG_KB_NSNAP == 6 && ENG_KB_SNAP[0] == 16 && ENG_KB_SNAP[1] == 48 && ENG_KB_SNAP[2] == 57 &&
+                    ENG_KB_SNAP[3] == 60 && ENG_KB_SNAP[4] == 62 && ENG_KB_SNAP[5] == 63,
+                "kb_snap: the set bits of |x| below the top one");
+  return j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+}
+
+// The compressed chain of one exponentiation: 8 lanes per item (8 items per
+// wave, all 64 lanes busy), lane k owning component kb_comp(k) of (f1, f2, f4,
+// f5); 63 compressed squarings of m (plane M) with m^(2^s) stored to plane
+// X0 + j after s = kb_snap(j) squarings.  LDS: 16 slots per item (state, LIN sums).
+#ifndef DG_KB_CHAIN_OCC
+#define DG_KB_CHAIN_OCC 3
+#endif
+__global__ void __launch_bounds__(64, DG_KB_CHAIN_OCC) k_eng_kb_chain(size_t cnt, uint32_t* __restrict__ xbuf) {
+  __shared__ uint32_t lds[8 * ENG_KB_SLOTS * ENG_SLOT_WORDS];
+  const int lane = threadIdx.x & 63, grp = lane >> 3, k = lane & 7;
+  const size_t gi = (size_t)blockIdx.x * 8 + grp;
+  const bool valid = gi < cnt;
+  const size_t i = valid ? gi : cnt - 1;
+  uint32_t* g = lds + grp * ENG_KB_SLOTS * ENG_SLOT_WORDS;
+  const int comp = kb_comp(k);
+  fp own = ld_blk(xbuf, kb_off(i, ENG_KB_PL_M, comp));
+  eng_st(g + k * ENG_SLOT_WORDS, own);
+  asm volatile("" ::: "memory");
+  own = eng_cyc_fast<true, 8>(g, k, own);
+  int s = 1;
+#pragma unroll 1
+  for (int j = 0; j < ENG_KB_NSNAP; ++j) {
+    const int sj = kb_snap(j);
+#pragma unroll 1
+    for (; s < sj; ++s) own = eng_cyc_fast<false, 8>(g, k, own);
+    if (valid) st_blk(xbuf, kb_off(i, ENG_KB_PL_X0 + j, comp), own);
+  }
+}
+
+// Per item: the product P of the six stored values' Norm(4 f1) -> pbuf
+// ([limb][cnt]; k_eng_inv inverts it in place).  A zero norm (f1 = 0) flags
+// the item; 1 stands in for it.
+__global__ void __launch_bounds__(256) k_eng_kb_norm(size_t cnt, const uint32_t* __restrict__ xbuf,
+                                                     uint32_t* __restrict__ pbuf, uint8_t* __restrict__ flags) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt) return;
+  fp acc = fp_one();
+  bool zero = false;
+#pragma unroll 1
+  for (int j = 0; j < ENG_KB_NSNAP; ++j) {
+    fp v = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
+    if (fp_is_zero(v)) {
+      v = fp_one();
+      zero = true;
+    }
+    acc = j ? fp_mul(acc, v) : v;
+  }
+  if (zero) flags[i] = 1;
+  st_soa(pbuf, cnt, i, acc);
+}
+
+// Per item: the six inverted norms from 1/P (pbuf) by Montgomery's trick in
+// registers, then the decompression of each stored value: f0 and f3
+// (engine.cuh eng_kb_decompress).  Flagged items are skipped.
+#ifndef DG_KB_DEC_OCC
+#define DG_KB_DEC_OCC 1
+#endif
+__global__ void __launch_bounds__(256, DG_KB_DEC_OCC) k_eng_kb_dec(size_t cnt, uint32_t* __restrict__ xbuf,
+                                                    const uint32_t* __restrict__ pbuf,
+                                                    const uint8_t* __restrict__ flags) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt || flags[i]) return;
+  fp pre[ENG_KB_NSNAP];
+#pragma unroll
+  for (int j = 0; j < ENG_KB_NSNAP; ++j) {
+    const fp v = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
+    pre[j] = j ? fp_mul(pre[j - 1], v) : v;
+  }
+  fp x = ld_soa(pbuf, cnt, i);  // 1 / (N_0 ... N_5); after value j: 1 / (N_0 ... N_(j-1))
+#pragma unroll
+  for (int j = ENG_KB_NSNAP - 1; j >= 0; --j) {
+    const int pl = ENG_KB_PL_X0 + j;
+    const fp2 f1 = kb_ld2(xbuf, i, pl, 2);
+    const fp ninv = j ? fp_mul(x, pre[j - 1]) : x;
+    if (j) x = fp_mul(x, eng_kb_norm(f1));
+    fp2 f0, f3;
+    eng_kb_decompress(f1, kb_ld2(xbuf, i, pl, 4), kb_ld2(xbuf, i, pl, 8), kb_ld2(xbuf, i, pl, 10), ninv, f0, f3);
+    st_blk(xbuf, kb_off(i, pl, 0), f0.c0);
+    st_blk(xbuf, kb_off(i, pl, 1), f0.c1);
+    st_blk(xbuf, kb_off(i, pl, 6), f3.c0);
+    st_blk(xbuf, kb_off(i, pl, 7), f3.c1);
+  }
 }
 
 }  // namespace dgpu
@@ -352,7 +535,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller_fixed(size_t n, siz
   eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
   asm volatile("" ::: "memory");
   eng_exec<true, false, 1>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, io);
-  if (L.valid) st_blk(fbuf, eng_blk_off(2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
+  if (L.valid) st_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 
 }  // namespace dgpu

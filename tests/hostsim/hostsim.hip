@@ -409,7 +409,7 @@ struct HostGroup {
   uint32_t s[64 * ENG_SLOT_WORDS];
   uint32_t c[ENG_NCONST * ENG_SLOT_WORDS];
   std::vector<fp> lines = std::vector<fp>(68 * 12);
-  fp fbuf[24];
+  fp fbuf[12 * ENG_KB_PLANES];   // k_eng_fe's two planes, or the Karabina FE's planes
   fp n1;
   int step = 0;
   bool cyc_ready = false;   // eng_exec's cyc_lin_ready
@@ -418,6 +418,7 @@ struct HostGroup {
 };
 
 bool g_cyc_fast = false;
+bool g_fe_kb = false;     // the Karabina FE (k_eng_fe_seg / k_eng_kb_*) instead of prog_fe
 bool g_compiled = false;   // compiled ops (engine_compiled.h) instead of the interpreter
 
 // eng_cyc_fast for the 12 lanes (read all, then write all); `lin`: run the
@@ -501,6 +502,73 @@ void host_consts(HostGroup& G, const g1a& pk) {
   put(ENG_C_PSI + 3, cy.c1);
 }
 
+// The 8-lane compressed squaring (k_eng_kb_chain: eng_cyc_fast<., 8> over
+// ENG_CYC8_PAR) for one item: all lanes read, then all write.  own: each
+// lane's output of the previous squaring (its post operand when !lin).
+void host_kb_square(uint32_t* s, bool lin, fp own[8]) {
+  fp outs[8], fused[8];
+  if (lin) {
+    for (int k = 0; k < 8; ++k) outs[k] = eng_cyc_lin(s, ENG_CYC8_PAR[k]);
+    for (int k = 0; k < 8; ++k) eng_st(s + (ENG_CYC8_PAR[k][0] & 0xFFFFu), outs[k]);
+  }
+  for (int k = 0; k < 8; ++k) outs[k] = eng_cyc_prod<ENG_CYC8_XF>(s, ENG_CYC8_PAR[k], lin ? nullptr : &own[k]);
+  for (int k = 0; k < 8; ++k) fused[k] = eng_cyc_fused_lin(outs[k], outs[k ^ 1], k);
+  for (int k = 0; k < 8; ++k) {
+    eng_st(s + (ENG_CYC8_PAR[k][5] >> 16), outs[k]);
+    eng_st(s + ENG_CYC8_PAR[k][7], fused[k]);
+    own[k] = outs[k];
+  }
+}
+
+// Fill a group's slots with normalized garbage (a fresh kernel's LDS): a
+// program segment that read a slot it had not written would change the result.
+void host_scramble(HostGroup& G, uint64_t x) {
+  for (int i = 0; i < 64 * ENG_SLOT_WORDS; ++i) {
+    x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+    G.s[i] = (i % ENG_SLOT_WORDS) == FP_LIMBS - 1 ? (uint32_t)(x % FP_P[FP_LIMBS - 1]) : (uint32_t)(x & FP_MASK);
+  }
+}
+
+// The Karabina FE of one item on the host, kernel by kernel (pairing_engine.cuh
+// eng_fe_kb sequence): segments of ENG_PROG_FEK, the compressed chain per
+// exponentiation, the norms' inversion and the decompression.  R ends in G's
+// slots ENG_E_R.  Returns false if the item would be flagged (f1 = 0).
+bool host_fe_kb(HostGroup& G, const fp f[12], const fp& n1inv) {
+  auto seg = [&](int j) {
+    host_exec(G, ENG_PROG_FEK + ENG_PROG_FEK_OFF[j], ENG_PROG_FEK_OFF[j + 1] - ENG_PROG_FEK_OFF[j]);
+  };
+  host_scramble(G, 0x1234567);
+  for (int k = 0; k < 12; ++k) G.set(ENG_E_F + k, f[k]);
+  G.set(ENG_E_N1I, n1inv);
+  seg(0);
+  for (int e = 1; e <= 5; ++e) {
+    uint32_t ks[ENG_KB_SLOTS * ENG_SLOT_WORDS];
+    memset(ks, 0, sizeof ks);
+    fp own[8];
+    for (int k = 0; k < 8; ++k) {
+      own[k] = G.fbuf[12 * ENG_KB_PL_M + ENG_KB_COMP[k]];
+      eng_st(ks + k * ENG_SLOT_WORDS, own[k]);
+    }
+    host_kb_square(ks, true, own);
+    int s = 1;
+    for (int j = 0; j < ENG_KB_NSNAP; ++j) {
+      for (; s < ENG_KB_SNAP[j]; ++s) host_kb_square(ks, false, own);
+      for (int k = 0; k < 8; ++k) G.fbuf[12 * (ENG_KB_PL_X0 + j) + ENG_KB_COMP[k]] = own[k];
+    }
+    for (int j = 0; j < ENG_KB_NSNAP; ++j) {
+      fp* x = G.fbuf + 12 * (ENG_KB_PL_X0 + j);
+      const fp nrm = eng_kb_norm(fp2{x[2], x[3]});
+      if (fp_is_zero(nrm)) return false;
+      fp2 f0, f3;
+      eng_kb_decompress(fp2{x[2], x[3]}, fp2{x[4], x[5]}, fp2{x[8], x[9]}, fp2{x[10], x[11]}, fp_inv(nrm), f0, f3);
+      x[0] = f0.c0, x[1] = f0.c1, x[6] = f3.c0, x[7] = f3.c1;
+    }
+    host_scramble(G, 0x9E3779B9ull * (uint64_t)e + 1);
+    seg(e);
+  }
+  return true;
+}
+
 // x == 0 mod p for a slot value (< 2.01p)
 bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 }  // namespace
@@ -510,6 +578,7 @@ bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 // the point is pair 1's Q (pair 0 a dummy copy).  Returns 1 in G2, 0 not,
 // -1 undecodable.
 extern "C" void hs_eng_set_cyc_fast(int on) { g_cyc_fast = on != 0; }
+extern "C" void hs_eng_set_fe_kb(int on) { g_fe_kb = on != 0; }
 extern "C" void hs_eng_set_compiled(int on) { g_compiled = on != 0; }
 
 // every compiled op vs the interpreter on the same random slots: 0 iff all
@@ -645,9 +714,13 @@ extern "C" int hs_eng_pairing(const uint8_t* pk48, const uint8_t* msg32, const u
   fp f[12];
   for (int k = 0; k < 12; ++k) f[k] = G.get(ENG_M_F + k);
   const fp n1inv = fp_inv(G.n1);
-  for (int k = 0; k < 12; ++k) G.set(ENG_E_F + k, f[k]);
-  G.set(ENG_E_N1I, n1inv);
-  host_exec(G, ENG_PROG_FE, ENG_PROG_FE_LEN);
+  if (g_fe_kb) {
+    if (!host_fe_kb(G, f, n1inv)) return -3;
+  } else {
+    for (int k = 0; k < 12; ++k) G.set(ENG_E_F + k, f[k]);
+    G.set(ENG_E_N1I, n1inv);
+    host_exec(G, ENG_PROG_FE, ENG_PROG_FE_LEN);
+  }
   bool one = true;
   for (int k = 0; k < 12; ++k) {
     fp v = fp_csub_p(fp_csub_p(G.get(ENG_E_R + k)));

@@ -162,6 +162,7 @@ def run_pairing_model(ops, pk, q1, q2):
     fe = G.ProgramRunner(m)
     fe.run(G.prog_fe())
     res = _read(m, G.E_R)
+    run_pairing_model.n1inv = n1inv
     return res, f, res == [(1, 0)] + [(0, 0)] * 5
 
 
@@ -179,6 +180,92 @@ def test_full_pairing_flow(ops, kind):
     # exact GT value: FE(f_model) = FE(oracle product)^-1 (the model skips the conjugation)
     fo = B.f12_mul(B.miller_loop(pk, h), B.miller_loop(B.g1_neg(B.G1_GEN), sig))
     assert _to_tower(res) == B.f12_conj(B.final_exponentiation(fo))
+
+
+def run_fe_kb_model(ops, c, f, n1inv):
+    """The Karabina FE flow (gen_engine.prog_fe_kb, KbChainModel,
+    kb_decompress): segment 0, then per exponentiation the 8-lane compressed
+    chain from plane M storing m^(2^s) at KB_SNAP, their decompression, and
+    the next segment.  Every segment starts from a fresh group (a new kernel);
+    only the HBM planes carry state.  Returns R in w-basis, or None if an
+    item would be flagged (f1 = 0 at a stored value)."""
+    rows, _ = G.cyc8_params(ops)
+    segs = G.prog_fe_kb()
+    fbuf = {}
+
+    def segment(prog, setup=None):
+        m = G.Model(ops, P, c)
+        if setup:
+            setup(m)
+        r = G.ProgramRunner(m)
+        r.fbuf = fbuf
+        r.run(prog)
+        return m
+
+    def setup0(m):
+        _load(m, G.E_F, f)
+        m.s[G.E_N1I] = n1inv
+
+    m = segment(segs[0], setup0)
+    for e in range(1, 6):
+        ch = G.KbChainModel(rows, P)
+        for i, comp in enumerate(G.KB_COMP):
+            ch.s[i] = fbuf[12 * G.PL_M + comp]
+        snaps = {}
+        for s in range(1, 64):
+            ch.square(lin=(s == 1))
+            if s in G.KB_SNAP:
+                snaps[s] = list(ch.s[:8])
+        for j, s in enumerate(G.KB_SNAP):
+            x = G.kb_decompress(snaps[s], P)
+            if x is None:
+                return None
+            for k, (a, b) in enumerate(x):
+                fbuf[12 * (G.PL_X0 + j) + 2 * k], fbuf[12 * (G.PL_X0 + j) + 2 * k + 1] = a, b
+        m = segment(segs[e])
+    return _read(m, G.E_R)
+
+
+@pytest.mark.parametrize("kind", ["valid", "wrong_msg"])
+def test_fe_karabina_flow(ops, kind):
+    """The Karabina FE gives exactly the Granger-Scott program's FE(f), on a
+    valid and an invalid pairing check; the chain's compressed coordinates
+    equal the oracle's powers m^(2^s)."""
+    sk = D.derive_secret(9)
+    pk = B.g1_mul(B.G1_GEN, sk)
+    msg = b"\x03" * 32
+    h = B.hash_to_g2(msg)
+    sig = B.g2_mul(h, sk)
+    if kind == "wrong_msg":
+        h = B.hash_to_g2(b"\x04" * 32)
+    res, f, ok = run_pairing_model(ops, pk, h, sig)
+    kb = run_fe_kb_model(ops, _consts(pk), f, run_pairing_model.n1inv)
+    assert kb is not None
+    assert kb == res
+    assert (kb == [(1, 0)] + [(0, 0)] * 5) == (kind == "valid")
+
+
+def test_karabina_chain_rows_and_decompression(ops):
+    """KbChainModel over cyc8_params equals the oracle's squarings of a
+    cyclotomic element on the compressed coordinates, and kb_decompress
+    recovers the full element."""
+    rng = random.Random(4)
+    a = _to_tower(_rand_f12(rng))
+    g = B.f12_mul(B.f12_conj(a), B.f12_inv(a))
+    g = B.f12_mul(B.f12_pow(g, P * P), g)
+    rows, _ = G.cyc8_params(ops)
+    ch = G.KbChainModel(rows, P)
+    w = _from_tower(g)
+    flat = [c for pair in w for c in pair]
+    for i, comp in enumerate(G.KB_COMP):
+        ch.s[i] = flat[comp]
+    cur = g
+    for s in range(1, 20):
+        ch.square(lin=(s == 1))
+        cur = B.f12_sqr(cur)
+        wf = [c for pair in _from_tower(cur) for c in pair]
+        assert ch.s[:8] == [wf[comp] for comp in G.KB_COMP]
+    assert G.kb_decompress(ch.s[:8], P) == _from_tower(cur)
 
 
 @pytest.mark.parametrize("in_g2", [True, False])

@@ -207,6 +207,27 @@ def test_engine_fast_cyc_matches_interpreter(hostsim):
     assert outs[0] == outs[1]
 
 
+def test_engine_karabina_fe_matches_granger_scott(hostsim):
+    """The Karabina FE as the device runs it (8-lane compressed chain over
+    ENG_CYC8_PAR, eng_kb_norm / eng_kb_decompress, the ENG_PROG_FEK segments,
+    each segment starting from scrambled slots) gives the same GT value words
+    as the Granger-Scott program, on valid and invalid pairing checks."""
+    sk = D.derive_secret(14)
+    pk = B.g1_mul(B.G1_GEN, sk)
+    pk48 = B.g1_compress(pk)
+    for msg, other in ((b"\x0b" * 32, None), (b"\x0c" * 32, b"\x0d" * 32), (b"\x0e" * 32, None)):
+        sig = B.g2_compress(B.g2_mul(B.hash_to_g2(other or msg), sk))
+        outs = []
+        for kb in (0, 1):
+            hostsim.hs_eng_set_fe_kb(kb)
+            out = buf(576)
+            rc = hostsim.hs_eng_pairing(pk48, msg, sig, out)
+            assert rc == (1 if other is None else 0)
+            outs.append(out.raw)
+        hostsim.hs_eng_set_fe_kb(0)
+        assert outs[0] == outs[1]
+
+
 def test_engine_compiled_ops_match_interpreter(hostsim):
     """The compiled (straight-line) hot ops (engine_compiled.h) give the same
     output words as the interpreter on random slots, and the full pairing

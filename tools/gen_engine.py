@@ -826,43 +826,54 @@ def cyc_fast_params(ops, name="E_CYC"):
     assert len(op.subs) == 2
     lin, prod = op.subs
     assert len(lin) == LANES and len(prod) == LANES
+    return _cyc_rows(lin, prod, lin, prod, {})
+
+
+def _cyc_rows(lin, prod, lin_all, prod_all, remap):
+    """Rows of eng_cyc_fast for the lanes `prod` (lane k computes prod[k] and
+    the LIN record lin[k]); slots are renumbered by `remap` (identity where
+    absent); lin_all / prod_all: the op's full sub-ops (partner and fused-LIN
+    lookups)."""
     slot = SLOT_WORDS
     rows = []
+    nl = len(prod)
+    assert len(lin) == nl
     assert len({r.cm for r in prod}) == 1 and len({abs(r.post[0][1]) for r in prod}) == 1
-    for k in range(LANES):
+    for k in range(nl):
         lr, pr = lin[k], prod[k]
         assert not lr.terms and len(lr.post) == 2 and lr.post[0][1] == 1 and abs(lr.post[1][1]) == 1
         assert lr.dst is not None and lr.exp is None and pr.dst is not None and pr.exp is None
         assert 2 <= len(pr.terms) <= 3 and len(pr.post) == 1 and -128 <= pr.cm < 128
         (x, _), (y, dy) = lr.post
+        sl = lambda s: remap.get(s, s)  # noqa: E731
         terms = sorted(pr.terms, key=lambda t: (t[2] < 0) + (t[3] == 2))
-        w = [lr.dst * slot | (x * slot) << 16, y * slot | (1 if dy < 0 else 0) << 16]
+        w = [sl(lr.dst) * slot | (sl(x) * slot) << 16, sl(y) * slot | (1 if dy < 0 else 0) << 16]
         flags = 0
         for t in range(3):
             if t < len(terms):
                 a, b, sg, cf = terms[t]
                 assert a < 64 and b < 64
-                w.append(a * slot | (b * slot) << 16)
+                w.append(sl(a) * slot | (sl(b) * slot) << 16)
                 flags |= (sg < 0) << (2 * t) | (cf == 2) << (2 * t + 1)
             else:
                 w.append(0)
         (ps, d), = pr.post
         assert ps < 64 and -128 <= d < 128
         assert ps == pr.dst   # the post operand is the lane's own slot (engine.cuh eng_cyc_chain keeps it in registers)
-        w.append(ps * slot | (pr.dst * slot) << 16)
+        w.append(sl(ps) * slot | (sl(pr.dst) * slot) << 16)
         flags |= len(terms) << 8 | (pr.cm & 0xFF) << 16 | (d & 0xFF) << 24
         # fused LIN: this lane holds coefficient half pr.dst; partner k ^ 1 the other half
         assert prod[k ^ 1].dst == pr.dst ^ 1
         re, im = pr.dst & ~1, pr.dst | 1
         want = [(re, 1), (im, 1 if pr.dst == re else -1)]
-        fused = [r.dst for r in lin if r.post == want]
+        fused = [r.dst for r in lin_all if r.post == want]
         assert len(fused) == 1, (k, want)
-        w += [flags, fused[0] * slot]
+        w += [flags, sl(fused[0]) * slot]
         rows.append(w)
     # bounds: LIN outputs x + y < 4.02p, x - y + 8p < 10.02p (normalized, unreduced);
     # every product sum < 2048 p^2 (redc output < 1.06p), <= 4 terms (no column normalization)
     tmp = {}
-    for r in lin:
+    for r in lin_all:
         tmp[r.dst] = 4.02 if r.post[1][1] > 0 else 10.02
     for r in prod:
         tot = 0.0
@@ -872,6 +883,151 @@ def cyc_fast_params(ops, name="E_CYC"):
             tot += cf * ba * (8.0 if sg < 0 else bb)
         assert tot < 2048 and len(r.terms) <= 4, (r.dst, tot)
     return rows
+
+
+# ---------------------------------------------------------------- Karabina final exponentiation
+# The hard part's five exponentiations by |x| (315 of the FE's cyclotomic
+# squarings) run on COMPRESSED elements (Karabina 2010): of the Granger-Scott
+# formulas (op_cyclo_sqr) the outputs f1, f2, f4, f5 depend only on f1, f2,
+# f4, f5 -- eight Fp instead of twelve.  The compressed chain runs in its own
+# kernel with 8 lanes per item (8 items per wave64, no idle lane; the 12-lane
+# groups run 5 items on 60 lanes), squaring m itself 63 times and storing
+# m^(2^s) for the six set bits s of |x|; decompression
+#   f3 = (xi f5^2 + 3 f2^2 - 2 f4) / (4 f1),  f0 = xi (2 f3^2 + f1 f5 - 3 f4 f2) + 1
+# needs one inversion per stored value, batched over the chunk (Montgomery's
+# trick, k_eng_kb_inv); the 12-lane program segments multiply the six values
+# (m^|x|) and run the glue between exponentiations.  An item with f1 = 0 at a
+# stored value (probability ~2^-762, or m = 1) is flagged and re-run through
+# the Granger-Scott program (prog_fe).
+KB_SNAP = (16, 48, 57, 60, 62, 63)     # m^(2^s) stored after s squarings: sum of 2^s = |x|
+KB_COMP = (2, 3, 4, 5, 8, 9, 10, 11)   # compressed coordinates (f1, f2, f4, f5) as w-basis components (re, im)
+KB_SLOTS = 16                          # chain kernel slots per item: 8 state + 8 LIN sums (pairs B, C)
+PL_T, PL_T2, PL_M, PL_X0 = 0, 1, 2, 3  # planes of the Karabina FE state: t, t2, exponentiation input, stored values
+KB_PLANES = PL_X0 + len(KB_SNAP)
+assert sum(1 << s for s in KB_SNAP) == 0xD201000000010000
+
+
+def cyc8_params(ops, name="E_CYC"):
+    """eng_cyc_fast rows of the 8-lane compressed squaring: E_CYC's records
+    for the outputs f1, f2, f4, f5 (lane k computes component KB_COMP[k]) and
+    the LIN sums of the Fp4 pairs B = (f1, f4), C = (f2, f5), renumbered into
+    the chain kernel's 16 slots (state k at slot k, sums at 8..15).  Lane k's
+    LIN record is the one it forms in the fused epilogue."""
+    op = {o.name: o for o in ops}[name]
+    lin, prod = op.subs
+    remap = {E_R + c: i for i, c in enumerate(KB_COMP)}
+    remap.update({E_CT + 4 + t: 8 + t for t in range(8)})
+    by_dst = {r.dst: r for r in prod}
+    prod8 = [by_dst[E_R + c] for c in KB_COMP]
+    lin8 = []
+    for r in prod8:
+        re, im = r.dst & ~1, r.dst | 1
+        want = [(re, 1), (im, 1 if r.dst == re else -1)]
+        lr = [x for x in lin if x.post == want]
+        assert len(lr) == 1
+        lin8.append(lr[0])
+    # closed: the eight outputs read only the eight state slots and the pairs B, C sums
+    for r in prod8 + lin8:
+        refs = [r.dst] + [t[0] for t in r.terms] + [t[1] for t in r.terms] + [s for s, _ in r.post]
+        assert all(s in remap for s in refs), r.dst
+    rows = _cyc_rows(lin8, prod8, lin, prod, remap)
+    xf = 0
+    for r in prod8:
+        for t, (_, _, sg, cf) in enumerate(sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2))):
+            xf |= (sg < 0) << t | (cf == 2) << (16 + t)
+    return rows, xf
+
+
+def prog_fe_kb():
+    """The Karabina FE as seven 12-lane program segments (k_eng_fe_seg):
+    segment 0 is prog_fe's easy part and stores t = m (planes T and M);
+    segment e = 1..5 follows exponentiation e's compressed chain: the product
+    of its six decompressed values (planes X0..X5) is m^|x|, conjugated m^x,
+    then the glue of prog_fe up to the next exponentiation's input (plane M).
+    Segment 5 ends with R = FE(f)."""
+    run = lambda *names: [("run", n) for n in names]  # noqa: E731
+    seg0 = run("E_XIF", "E_NRM", "E_XIN2", "E_T012", "E_XIT", "E_D", "E_NINV_d", "E_NINV", "E_XINI",
+               "E_SQRC", "E_MULN", "E_FROB2A", "E_XIA", "E_MUL")
+    seg0 += [("st12", E_R, 12 * PL_T), ("st12", E_R, 12 * PL_M)]
+    segs = [seg0]
+    for e in range(1, 6):
+        p = [("ld12", E_R, 12 * PL_X0)]
+        for j in range(1, len(KB_SNAP)):
+            p += [("ld12", E_A, 12 * (PL_X0 + j))] + run("E_XIA", "E_MUL")
+        p += run("E_CONJ")                                          # R = m^x
+        if e in (1, 2):                                             # t0 = t^x conj(t), t1 = t0^x conj(t0)
+            p += [("ld12", E_A, 12 * PL_M)] + run("E_XIA", "E_MULCJ") + [("st12", E_R, 12 * PL_M)]
+        elif e == 3:                                                # t2 = t1^x t1^p
+            p += [("ld12", E_A, 12 * PL_M)] + run("E_FROB1", "E_XIA", "E_MUL")
+            p += [("st12", E_R, 12 * PL_M), ("st12", E_R, 12 * PL_T2)]
+        elif e == 4:                                                # t2^x
+            p += [("st12", E_R, 12 * PL_M)]
+        else:                                                       # t3 = t2^(x^2) t2^(p^2) conj(t2), times t^3
+            p += [("ld12", E_A, 12 * PL_T2)] + run("E_FROB2", "E_XIA", "E_MUL")
+            p += [("ld12", E_A, 12 * PL_T2)] + run("E_XIA", "E_MULCJ")
+            p += [("ld12", E_A, 12 * PL_T)] + run("E_XIA", "E_MUL", "E_CYCA", "E_XIA", "E_MUL")
+        segs.append(p)
+    return segs
+
+
+class KbChainModel:
+    """The 8-lane compressed squaring (engine.cuh eng_cyc_fast over
+    ENG_CYC8_PAR) over Python ints mod p: the rows' semantics, TEST
+    INFRASTRUCTURE (tests/test_engine_model.py)."""
+
+    def __init__(self, rows, p):
+        self.rows, self.p = rows, p
+        self.s = [0] * KB_SLOTS
+
+    def _get(self, w):
+        return self.s[w // SLOT_WORDS]
+
+    def square(self, lin):
+        p, rows = self.p, self.rows
+        if lin:
+            outs = []
+            for w in rows:
+                x, y = self._get(w[0] >> 16), self._get(w[1] & 0xFFFF)
+                outs.append((w[0] & 0xFFFF, (x - y) if (w[1] >> 16) else (x + y)))
+            for d, v in outs:
+                self.s[d // SLOT_WORDS] = v % p
+        outs = []
+        for w in rows:
+            fl = w[6]
+            acc = 0
+            for t in range((fl >> 8) & 3):
+                a, b = self._get(w[2 + t] & 0xFFFF), self._get(w[2 + t] >> 16)
+                sg = -1 if (fl >> (2 * t)) & 1 else 1
+                cf = 2 if (fl >> (2 * t + 1)) & 1 else 1
+                acc += sg * cf * a * b
+            cm = ((fl >> 16) & 0xFF) - (256 if (fl >> 23) & 1 else 0)
+            d = ((fl >> 24) & 0xFF) - (256 if (fl >> 31) & 1 else 0)
+            outs.append((w[5] >> 16, (cm * acc + d * self._get(w[5] & 0xFFFF)) % p))
+        for dd, v in outs:
+            self.s[dd // SLOT_WORDS] = v
+        # fused LIN epilogue: lane k forms own + partner (re lane) / partner - own... (im lane)
+        for k, w in enumerate(rows):
+            own, par = outs[k][1], outs[k ^ 1][1]
+            self.s[w[7] // SLOT_WORDS] = ((par - own) if (k & 1) else (own + par)) % p
+
+
+def kb_decompress(v, p):
+    """(f1, f2, f4, f5) (8 ints, KB_COMP order) -> the 12 w-basis components;
+    None when f1 = 0 (the flagged case)."""
+    f1, f2, f4, f5 = (v[0], v[1]), (v[2], v[3]), (v[4], v[5]), (v[6], v[7])
+    mul = lambda a, b: ((a[0] * b[0] - a[1] * b[1]) % p, (a[0] * b[1] + a[1] * b[0]) % p)  # noqa: E731
+    xi = lambda a: ((a[0] - a[1]) % p, (a[0] + a[1]) % p)  # noqa: E731
+    lin = lambda *ts: (sum(c * a[0] for c, a in ts) % p, sum(c * a[1] for c, a in ts) % p)  # noqa: E731
+    d = lin((4, f1))
+    nd = (d[0] * d[0] + d[1] * d[1]) % p
+    if nd == 0:
+        return None
+    ninv = pow(nd, p - 2, p)
+    dinv = (d[0] * ninv % p, (-d[1]) * ninv % p)
+    n = lin((1, xi(mul(f5, f5))), (3, mul(f2, f2)), (-2, f4))
+    f3 = mul(n, dinv)
+    f0 = lin((1, xi(lin((2, mul(f3, f3)), (1, mul(f1, f5)), (-3, mul(f4, f2))))), (1, (1, 0)))
+    return [f0, f1, f2, f3, f4, f5]
 
 
 # ---------------------------------------------------------------- compiled ops (engine_compiled.h)
@@ -1072,7 +1228,28 @@ def emit(path):
     for w in rows:
         lines.append("  {" + ", ".join(f"0x{x:08x}u" for x in w) + "},")
     lines.append("};")
+    rows8, xf8 = cyc8_params(ops)
+    lines.append("// Karabina FE (tools/gen_engine.py cyc8_params, prog_fe_kb): the 8-lane compressed squaring")
+    lines.append(f"constexpr int ENG_KB_SLOTS = {KB_SLOTS}, ENG_KB_NSNAP = {len(KB_SNAP)}, ENG_KB_PLANES = {KB_PLANES};")
+    lines.append(f"constexpr int ENG_KB_PL_T = {PL_T}, ENG_KB_PL_T2 = {PL_T2}, ENG_KB_PL_M = {PL_M}, ENG_KB_PL_X0 = {PL_X0};")
+    lines.append(f"constexpr int ENG_KB_SNAP[{len(KB_SNAP)}] = {{{', '.join(map(str, KB_SNAP))}}};")
+    lines.append(f"constexpr int ENG_KB_COMP[8] = {{{', '.join(map(str, KB_COMP))}}};")
+    lines.append(f"constexpr uint32_t ENG_CYC8_XF = 0x{xf8:x}u;")
+    lines.append(f"alignas(16) ENG_TABLE_QUAL uint32_t ENG_CYC8_PAR[8][8] = {{")
+    for w in rows8:
+        lines.append("  {" + ", ".join(f"0x{x:08x}u" for x in w) + "},")
+    lines.append("};")
     op_index = {op.name: i for i, op in enumerate(ops)}
+    segs = [encode_prog(s, op_index) for s in prog_fe_kb()]
+    offs = [0]
+    for s in segs:
+        offs.append(offs[-1] + len(s))
+    lines.append(f"constexpr int ENG_PROG_FEK_OFF[{len(offs)}] = {{{', '.join(map(str, offs))}}};")
+    allk = [w for s in segs for w in s]
+    lines.append(f"ENG_TABLE_QUAL uint32_t ENG_PROG_FEK[{len(allk)}] = {{")
+    for i in range(0, len(allk), 12):
+        lines.append("  " + ", ".join(f"0x{w:08x}u" for w in allk[i:i + 12]) + ",")
+    lines.append("};")
     lines.append(f"constexpr uint32_t ENG_OPC_RUN = {OPC['run']}, ENG_OPC_STEP = {OPC['step']}, ENG_OPC_LDLINE = {OPC['ldline']}, "
                  f"ENG_OPC_LD12 = {OPC['ld12']}, ENG_OPC_ST12 = {OPC['st12']};")
     for pname, prog in (("LINES", prog_lines()), ("MILLER", prog_miller()), ("FE", prog_fe())):

@@ -164,6 +164,12 @@ def recover_work(t, slices=5):
     slice_mads = t * (m("g2_dbl") + 6 * m("g2_add_affine")) + 64 * m("g2_dbl") + 17 * t * m("g2_add")
     g1 = 64 * m("g1_dbl") + (17 * t + 1) * m("g1_add_affine")
     return {"recover_msm": {"mads": slices * slice_mads}, "recover_rlc_g1": {"mads": g1}}
+# the Karabina FE's stages (libdrand_gpu eng_fe_kb_locked): the 12-lane
+# program segments (+ the flagged-block fallback), the 8-lane compressed
+# chains, the norms' inversion and the decompression
+KB_STAGE_WORK = {"eng_fe": "k_eng_fe_seg", "eng_fe_chain": "k_eng_kb_chain", "eng_fe_kbinv": "k_eng_kb_inv"}
+
+
 # stage -> kernel symbol for the traffic lookup
 STAGE_KERNEL = {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
                 "eng_lines_fixed": "k_eng_lines_fixed", "hash_to_g2": "hash_to_g2", "decode_g2": "k_decode_g2_sigs",
@@ -195,7 +201,9 @@ def roofline_for(stage_ms, items, pipeline="g2", stage_items=None, extra_work=No
     overrides it per stage."""
     if not stage_ms or not items:
         return None
-    wmap = STAGE_WORK[pipeline]
+    wmap = dict(STAGE_WORK[pipeline])
+    if "eng_fe_chain" in stage_ms:  # Karabina FE (default; DGPU_FE=gs runs k_eng_fe alone under "eng_fe")
+        wmap.update(KB_STAGE_WORK)
     work = dict(hash_work(), **engine_work())
     work.update(extra_work or {})
     have = {s: t for s, t in stage_ms.items() if s in wmap and wmap[s] in work and t > 0}
@@ -216,7 +224,8 @@ def roofline_for(stage_ms, items, pipeline="g2", stage_items=None, extra_work=No
                            "profiles/op_counts.json")}
     out["stage_frac"] = {s: stage_items.get(s, items) * work[wmap[s]]["mads"] / (t * 1e-3) / PEAK_MAD_U64_PER_S
                          for s, t in have.items()}
-    traffic, src = traffic_for(STAGE_KERNEL.get(name, key), it)
+    kb = "eng_fe_chain" in stage_ms and name in KB_STAGE_WORK
+    traffic, src = traffic_for(key if kb else STAGE_KERNEL.get(name, key), it)
     if traffic is not None:
         out["traffic"] = traffic
         out["traffic_unit"] = "bytes over the launches (PMC FETCH_SIZE+WRITE_SIZE, %s)" % src

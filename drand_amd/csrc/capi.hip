@@ -86,9 +86,9 @@ constexpr size_t ENG_CHUNK = 524288;
 constexpr size_t ENG_CHUNK_MIN = 16384;
 // Karabina FE state per round and lane: the planes (t, t2, m, six stored
 // values), the product of the six norms + its prefix products (k_eng_inv),
-// the flag and the fallback list entry
+// the six excluded products, the flag and the fallback list entry
 constexpr size_t ENG_KB_XWORDS = (size_t)ENG_KB_PLANES * 12 * FP_LIMBS;
-constexpr size_t ENG_KB_BYTES_PER_ROUND = ENG_KB_XWORDS * 4 + 2 * (size_t)FP_LIMBS * 4 + 1 + 4;
+constexpr size_t ENG_KB_BYTES_PER_ROUND = ENG_KB_XWORDS * 4 + (2 + (size_t)ENG_KB_NSNAP) * FP_LIMBS * 4 + 1 + 4;
 // engine bytes per round and lane: line buffer + f planes + N1 + Karabina state
 constexpr size_t ENG_BYTES_PER_ROUND =
     (size_t)ENG_LINE_STEPS * FP_LIMBS * 12 * 4 + 2 * FP_LIMBS * 12 * 4 + FP_LIMBS * 4 + ENG_KB_BYTES_PER_ROUND;
@@ -174,6 +174,7 @@ struct dgpu_ctx {
   DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1, l2_kb;
   bool fe_gs = false;            // DGPU_FE=gs: the Granger-Scott FE kernel instead of the Karabina chain (A/B)
   size_t kb_inv_chain = 16;      // DGPU_KB_INV_CHAIN: norms per k_eng_inv thread in the Karabina FE (A/B)
+  size_t kb_test_flag = 0;       // DGPU_KB_TEST_FLAG=k (tests): flag every k-th item so the fallback runs
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
@@ -606,14 +607,18 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
 // 2b): segment 0 (easy part), then per exponentiation by |x| the 8-lane
 // compressed chain, the batched inversion of its six stored values' norms,
 // their decompression and the next 12-lane segment; last, the Granger-Scott
-// kernel for flagged items only.  kb: ENG_KB_BYTES_PER_ROUND x cap bytes.
-int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap, size_t r0, uint32_t* f,
+// kernel for the listed blocks with a flagged item.  capb: the chunk capacity
+// rounded up to whole blocks of 5 rounds (>= cnt); kb: ENG_KB_BYTES_PER_ROUND
+// x capb bytes.
+int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t capb, size_t r0, uint32_t* f,
                      const uint32_t* n1inv, uint8_t* kb, uint8_t* st, hipStream_t s) {
-  uint32_t* xbuf = (uint32_t*)kb;  // cap is a multiple of 5: whole blocks
-  uint32_t* pbuf = xbuf + ENG_KB_XWORDS * cap;
-  uint32_t* pre = pbuf + (size_t)FP_LIMBS * cap;
-  uint32_t* fb = pre + (size_t)FP_LIMBS * cap;
-  uint8_t* flags = (uint8_t*)(fb + cap);
+  if (capb % ENG_ROUNDS_PER_BLOCK || cnt > capb) return set_err(DGPU_EINVAL, "karabina FE: bad chunk capacity");
+  uint32_t* xbuf = (uint32_t*)kb;  // [capb / 5 blocks][ENG_KB_PLANES][limb][60]
+  uint32_t* pbuf = xbuf + ENG_KB_XWORDS * capb;
+  uint32_t* pre = pbuf + (size_t)FP_LIMBS * capb;
+  uint32_t* ebuf = pre + (size_t)FP_LIMBS * capb;
+  uint32_t* fb = ebuf + (size_t)ENG_KB_NSNAP * FP_LIMBS * capb;
+  uint8_t* flags = (uint8_t*)(fb + capb);
   const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
   const size_t inv_threads = std::max<size_t>(1, (cnt + c->kb_inv_chain - 1) / c->kb_inv_chain);
   constexpr int nseg = (int)(sizeof(ENG_PROG_FEK_OFF) / sizeof(ENG_PROG_FEK_OFF[0])) - 1;
@@ -624,13 +629,13 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
       hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_fe_kbinv");
-      hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, (const uint32_t*)xbuf, pbuf,
-                         flags);
+      hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
+                         pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
       HIP_TRY(hipGetLastError());
       hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
       HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, (const uint32_t*)pbuf,
-                         (const uint8_t*)flags);
+      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
+                         (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
       HIP_TRY(hipGetLastError());
     }
     mark(c, s, "eng_fe");
@@ -663,7 +668,8 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
   DevBuf* b_kb = L ? L->kb : &c->eng_kb;
   const bool need_lines = !(fixed_table && c->fused_fixed);
   int rc;
-  if (!c->fe_gs && (rc = b_kb->ensure(cap * ENG_KB_BYTES_PER_ROUND))) return rc;
+  // the Karabina planes are wave-blocked: whole blocks of 5 rounds (cap may be n, not a multiple of 5)
+  if (!c->fe_gs && (rc = b_kb->ensure(cap_blk * ENG_ROUNDS_PER_BLOCK * ENG_KB_BYTES_PER_ROUND))) return rc;
   if (need_lines && (rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
   if ((rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
   if ((rc = b_n1->ensure(cap * FP_LIMBS * 4))) return rc;
@@ -707,7 +713,8 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
       mark(c, s, "eng_fe");
       hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
       HIP_TRY(hipGetLastError());
-    } else if ((rc = eng_fe_kb_locked(c, consts, cnt, cap, r0, f, n1, (uint8_t*)b_kb->p, st, s))) {
+    } else if ((rc = eng_fe_kb_locked(c, consts, cnt, cap_blk * ENG_ROUNDS_PER_BLOCK, r0, f, n1, (uint8_t*)b_kb->p,
+                                      st, s))) {
       return rc;
     }
   }
@@ -1015,6 +1022,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (fev && !strcmp(fev, "gs")) c->fe_gs = true;
   const char* kic = getenv("DGPU_KB_INV_CHAIN");
   if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
+  const char* ktf = getenv("DGPU_KB_TEST_FLAG");
+  if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);

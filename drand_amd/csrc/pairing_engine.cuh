@@ -419,59 +419,72 @@ __global__ void __launch_bounds__(64, DG_KB_CHAIN_OCC) k_eng_kb_chain(size_t cnt
   }
 }
 
-// Per item: the product P of the six stored values' Norm(4 f1) -> pbuf
-// ([limb][cnt]; k_eng_inv inverts it in place).  A zero norm (f1 = 0) flags
-// the item; 1 stands in for it.
-__global__ void __launch_bounds__(256) k_eng_kb_norm(size_t cnt, const uint32_t* __restrict__ xbuf,
-                                                     uint32_t* __restrict__ pbuf, uint8_t* __restrict__ flags) {
+// Per item: the norms N_j = Norm(4 f1) of the six stored values, their
+// product P -> pbuf ([limb][cnt]; k_eng_inv inverts it in place) and the
+// excluded products E_j = prod_(k != j) N_k -> ebuf ([j][limb][cnt]), so
+// that 1 / N_j = E_j / P.  A zero norm (f1 = 0) flags the item (unless it
+// has already failed: its verdict stands); 1 stands in for it.  flag_every
+// (test mode, DGPU_KB_TEST_FLAG): also flag every item i with
+// i % flag_every == 0, so the fallback runs.
+__global__ void __launch_bounds__(256) k_eng_kb_norm(size_t cnt, size_t r0, const uint32_t* __restrict__ xbuf,
+                                                     uint32_t* __restrict__ pbuf, uint32_t* __restrict__ ebuf,
+                                                     uint8_t* __restrict__ flags, const uint8_t* __restrict__ status,
+                                                     size_t flag_every) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cnt) return;
-  fp acc = fp_one();
-  bool zero = false;
-#pragma unroll 1
+  fp nrm[ENG_KB_NSNAP];
+  bool zero = flag_every && i % flag_every == 0;
+#pragma unroll
   for (int j = 0; j < ENG_KB_NSNAP; ++j) {
-    fp v = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
-    if (fp_is_zero(v)) {
-      v = fp_one();
+    nrm[j] = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
+    if (fp_is_zero(nrm[j])) {
+      nrm[j] = fp_one();
       zero = true;
     }
-    acc = j ? fp_mul(acc, v) : v;
   }
-  if (zero) flags[i] = 1;
+  // prefixes into ebuf, then each E_j = prefix_(j-1) * suffix_(j+1)
+  fp acc = nrm[0];
+#pragma unroll
+  for (int j = 1; j < ENG_KB_NSNAP; ++j) {
+    st_soa(ebuf + (size_t)j * FP_LIMBS * cnt, cnt, i, acc);
+    acc = fp_mul(acc, nrm[j]);
+  }
   st_soa(pbuf, cnt, i, acc);
+  acc = nrm[ENG_KB_NSNAP - 1];
+#pragma unroll
+  for (int j = ENG_KB_NSNAP - 2; j >= 0; --j) {
+    const fp e = j ? fp_mul(ld_soa(ebuf + (size_t)j * FP_LIMBS * cnt, cnt, i), acc) : acc;
+    st_soa(ebuf + (size_t)j * FP_LIMBS * cnt, cnt, i, e);
+    acc = fp_mul(acc, nrm[j]);
+  }
+  if (zero && status[r0 + i] == ST_OK) flags[i] = 1;
 }
 
-// Per item: the six inverted norms from 1/P (pbuf) by Montgomery's trick in
-// registers, then the decompression of each stored value: f0 and f3
-// (engine.cuh eng_kb_decompress).  Flagged items are skipped.
+// Decompression, one thread per stored value j of item i (element e = j cnt
+// + i): 1 / N_j = E_j / P (ebuf, pbuf after k_eng_inv), then f0 and f3 of
+// plane X0 + j (engine.cuh eng_kb_decompress).  Flagged items are skipped.
+// 2 waves/SIMD (13 spilled VGPRs) measured faster than 1 (r03k: the FE's
+// inversion + decompression stages 47.3 vs 60.9 ms per 2M rounds).
 #ifndef DG_KB_DEC_OCC
-#define DG_KB_DEC_OCC 1
+#define DG_KB_DEC_OCC 2
 #endif
 __global__ void __launch_bounds__(256, DG_KB_DEC_OCC) k_eng_kb_dec(size_t cnt, uint32_t* __restrict__ xbuf,
-                                                    const uint32_t* __restrict__ pbuf,
-                                                    const uint8_t* __restrict__ flags) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cnt || flags[i]) return;
-  fp pre[ENG_KB_NSNAP];
-#pragma unroll
-  for (int j = 0; j < ENG_KB_NSNAP; ++j) {
-    const fp v = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
-    pre[j] = j ? fp_mul(pre[j - 1], v) : v;
-  }
-  fp x = ld_soa(pbuf, cnt, i);  // 1 / (N_0 ... N_5); after value j: 1 / (N_0 ... N_(j-1))
-#pragma unroll
-  for (int j = ENG_KB_NSNAP - 1; j >= 0; --j) {
-    const int pl = ENG_KB_PL_X0 + j;
-    const fp2 f1 = kb_ld2(xbuf, i, pl, 2);
-    const fp ninv = j ? fp_mul(x, pre[j - 1]) : x;
-    if (j) x = fp_mul(x, eng_kb_norm(f1));
-    fp2 f0, f3;
-    eng_kb_decompress(f1, kb_ld2(xbuf, i, pl, 4), kb_ld2(xbuf, i, pl, 8), kb_ld2(xbuf, i, pl, 10), ninv, f0, f3);
-    st_blk(xbuf, kb_off(i, pl, 0), f0.c0);
-    st_blk(xbuf, kb_off(i, pl, 1), f0.c1);
-    st_blk(xbuf, kb_off(i, pl, 6), f3.c0);
-    st_blk(xbuf, kb_off(i, pl, 7), f3.c1);
-  }
+                                                                   const uint32_t* __restrict__ pbuf,
+                                                                   const uint32_t* __restrict__ ebuf,
+                                                                   const uint8_t* __restrict__ flags) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)ENG_KB_NSNAP * cnt) return;
+  const size_t j = e / cnt, i = e - j * cnt;
+  if (flags[i]) return;
+  const int pl = ENG_KB_PL_X0 + (int)j;
+  const fp ninv = fp_mul(ld_soa(pbuf, cnt, i), ld_soa(ebuf + j * FP_LIMBS * cnt, cnt, i));
+  fp2 f0, f3;
+  eng_kb_decompress(kb_ld2(xbuf, i, pl, 2), kb_ld2(xbuf, i, pl, 4), kb_ld2(xbuf, i, pl, 8), kb_ld2(xbuf, i, pl, 10),
+                    ninv, f0, f3);
+  st_blk(xbuf, kb_off(i, pl, 0), f0.c0);
+  st_blk(xbuf, kb_off(i, pl, 1), f0.c1);
+  st_blk(xbuf, kb_off(i, pl, 6), f3.c0);
+  st_blk(xbuf, kb_off(i, pl, 7), f3.c1);
 }
 
 }  // namespace dgpu

@@ -184,45 +184,73 @@ def test_rlc_mode_large_chain(chained):
     assert np.array_equal(per == 0, expect)
 
 
+def _verify_with_env(c, env, mode=None):
+    """Verify chain c on a fresh context opened under the environment `env`
+    (the library reads its A/B and test knobs at dgpu_open); returns reasons."""
+    import os
+    from drand_amd import _lib
+    n = len(c.rounds)
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ctx = _lib.Context(0)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        lib = ctx.lib
+        _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, c.pk, len(c.pk)))
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        reason = np.zeros(n, dtype=np.uint8)
+        _lib.check(lib.dgpu_verify_batch(ctx.handle, _lib.SCHEME_CHAINED, n, _lib.ptr(c.rounds),
+                                         _lib.ptr(c.sigs), c.sigs.shape[1], _lib.ptr(c.sig_len),
+                                         _lib.ptr(c.prev), c.prev.shape[1], _lib.ptr(c.prev_len),
+                                         _lib.MODE_PER_ROUND if mode is None else mode, 0, _lib.ptr(bits),
+                                         _lib.ptr(reason)))
+        assert np.array_equal(np.unpackbits(bits, bitorder="little")[:n].astype(bool), reason == 0)
+        return reason
+    finally:
+        ctx.close()
+
+
+def test_karabina_fe_equals_granger_scott_and_fallback():
+    """The Karabina FE (default) against the Granger-Scott kernel (DGPU_FE=gs)
+    and against the Karabina path with every 7th item of each chunk forced
+    onto the fallback list (DGPU_KB_TEST_FLAG=7: flagged as if f1 = 0, its FE
+    re-run on prog_fe by k_eng_fe_fb) -- the fallback otherwise practically
+    never runs.  20,011 rounds (a ragged last block), 1% corrupted: identical
+    reasons, equal to the construction."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 20011
+    c = make_chain(21, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 21, rate=1e-2)
+    kb = _verify_with_env(c, {})
+    gs = _verify_with_env(c, {"DGPU_FE": "gs"})
+    fb = _verify_with_env(c, {"DGPU_KB_TEST_FLAG": "7"})
+    assert kb.tolist() == gs.tolist() == fb.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(kb == 0, expect)
+
+
 def test_two_lane_per_round_large_chain():
     """A batch spanning two engine chunks runs on two lanes (streams, half the
     batch each, capi.hip verify_device_locked): 2*131072 + 1001 rounds (odd
     split), 0.1% corrupted -- reasons equal the one-lane context's
     (DGPU_LANES=1, 64Ki-round engine chunks: five chunks) and the
     construction."""
-    import os
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
     n = 2 * 131072 + 1001
     c = make_chain(13, n, _lib.SCHEME_CHAINED, seg_len=64)
     bad = corrupt(c, 13, rate=1e-3)
 
-    def run(env):
-        saved = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
-        try:
-            ctx = _lib.Context(0)
-        finally:
-            for k, v in saved.items():
-                if v is None:
-                    del os.environ[k]
-                else:
-                    os.environ[k] = v
-        try:
-            lib = ctx.lib
-            _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, c.pk, len(c.pk)))
-            bits = np.zeros((n + 7) // 8, dtype=np.uint8)
-            reason = np.zeros(n, dtype=np.uint8)
-            _lib.check(lib.dgpu_verify_batch(ctx.handle, _lib.SCHEME_CHAINED, n, _lib.ptr(c.rounds),
-                                             _lib.ptr(c.sigs), c.sigs.shape[1], _lib.ptr(c.sig_len),
-                                             _lib.ptr(c.prev), c.prev.shape[1], _lib.ptr(c.prev_len),
-                                             _lib.MODE_PER_ROUND, 0, _lib.ptr(bits), _lib.ptr(reason)))
-            assert np.array_equal(np.unpackbits(bits, bitorder="little")[:n].astype(bool), reason == 0)
-            return reason
-        finally:
-            ctx.close()
-
-    two, one = run({"DGPU_LANES": "2"}), run({"DGPU_LANES": "1", "DGPU_ENG_CHUNK": "65536"})
+    two = _verify_with_env(c, {"DGPU_LANES": "2"})
+    one = _verify_with_env(c, {"DGPU_LANES": "1", "DGPU_ENG_CHUNK": "65536"})
     assert two.tolist() == one.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False

@@ -51,6 +51,34 @@ def main():
         # exponentiation per 64 items (~475 multiplications) amortized
         "k_eng_inv": {"mads": 3 * 392 + 475 * 392 // 64},
     }
+    # Karabina FE: the 12-lane program segments, the 8-lane
+    # compressed chains (63 squarings of the E_CYC records for f1, f2, f4, f5,
+    # five exponentiations), and the per-thread decompression side: norms of
+    # the six stored values (k_eng_kb_norm: 2 sqr each, 5 mul), their product's
+    # inversion (k_eng_inv: 3 mul + an inversion, 82 mul + 380 sqr, per
+    # KB_INV_CHAIN items), the per-value inverses and eng_kb_decompress
+    # (k_eng_kb_dec: 12 sqr + 5 mul forward, 2 mul + 2 sqr per value after the
+    # first backward, 17 mul per decompression)
+    segs = G.prog_fe_kb()
+    seg_work = program_work(ops, [ins for sg in segs for ins in sg])
+    cyc = {o.name: o for o in ops}["E_CYC"].subs[1]
+    comp = {G.E_R + c for c in G.KB_COMP}
+    sq_terms = sum(len(r.terms) for r in cyc if r.dst in comp)
+    sq_redc = sum(1 for r in cyc if r.dst in comp and r.terms)
+    n_exp, n_sq = 5, 63
+    chain = {"squarings": n_exp * n_sq, "product_terms": n_exp * n_sq * sq_terms,
+             "reductions": n_exp * n_sq * sq_redc, "mads": n_exp * n_sq * (sq_terms + sq_redc) * MADS_PER_PRODUCT}
+    MUL, SQR = 392, 301
+    KB_INV_CHAIN = 16
+    ns = len(G.KB_SNAP)
+    norm = 2 * ns * SQR + (ns - 1) * MUL
+    inv = 3 * MUL + (82 * MUL + 380 * SQR) // KB_INV_CHAIN
+    dec = 2 * ns * SQR + (ns - 1) * MUL + (ns - 1) * (2 * MUL + 2 * SQR) + ns * 17 * MUL
+    kern["k_eng_fe_seg"] = seg_work
+    kern["k_eng_kb_chain"] = chain
+    kern["k_eng_kb_inv"] = {"mads": n_exp * (norm + inv + dec), "per_exponentiation": {
+        "k_eng_kb_norm": norm, "k_eng_inv": inv, "k_eng_kb_dec": dec}}
+    kern["k_eng_fe_karabina"] = {"mads": seg_work["mads"] + chain["mads"] + kern["k_eng_kb_inv"]["mads"]}
     # on-G1 schemes: the Miller program with every line formed at its LDLINE
     # from the key's fixed table, 8 of the 12 exports scaled by one Fp
     # multiplication (a P coordinate): 68 line steps x 8 x 392 mads more
@@ -62,7 +90,10 @@ def main():
     out = {
         "unit": "per item (one two-pair pairing check); mads = 32x32->64 v_mad_u64_u32 products the algorithm performs",
         "kernels": kern,
-        "pairing_total_mads": sum(kern[k]["mads"] for k in ("k_eng_lines", "k_eng_miller", "k_eng_inv", "k_eng_fe")),
+        "pairing_total_mads": sum(kern[k]["mads"] for k in ("k_eng_lines", "k_eng_miller", "k_eng_inv",
+                                                             "k_eng_fe_karabina")),
+        "pairing_total_mads_granger_scott_fe": sum(kern[k]["mads"] for k in ("k_eng_lines", "k_eng_miller",
+                                                                              "k_eng_inv", "k_eng_fe")),
     }
     path = os.path.join(os.path.dirname(HERE), "profiles", "engine_work.json")
     with open(path, "w") as f:

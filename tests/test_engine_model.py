@@ -69,7 +69,7 @@ def _read(m, base):
 def test_tables_emit_and_bounds(ops, tmp_path):
     G.check_bounds(ops)
     out, nsl = G.emit(str(tmp_path / "t.h"))
-    assert nsl["MILLER"] <= 34 and nsl["FE"] <= 48 and nsl["LINES"] <= 52
+    assert nsl["MILLER"] <= 36 and nsl["FE"] <= 48 and nsl["LINES"] <= 52
     # the committed header is what the generator produces
     with open(os.path.join(ROOT, "drand_amd", "csrc", "engine_tables.h")) as f:
         assert f.read() == open(tmp_path / "t.h").read()

@@ -114,10 +114,16 @@ def op_xi_copy(name, src_base, dst_base, ks):
     return pack(name, recs)
 
 
-def op_sqr12(name, F, XF, conj=False):
-    """F <- F^2 (conj: F <- conj(F)^2 = conj(F^2)), in place; XF = xi*F[1..5]."""
+def op_sqr12(name, F, XF, conj=False, XF0=None):
+    """F <- F^2 (conj: F <- conj(F)^2 = conj(F^2)), in place; XF = xi*F[1..5],
+    XF0 (optional) = xi*F[0].  The xi-copy of a coefficient a + bu is
+    (a - b) + (a + b)u, so a square's real part a^2 - b^2 is ONE product of its
+    xi-copy's halves: the squares f_i^2 (i = 0, 1, 2, no wrap) take 1 term
+    instead of 2, and no output needs more than 7 (8 before)."""
     f = fp12(F)
     xf = {k: fp2(XF + 2 * (k - 1)) for k in range(1, 6)}
+    if XF0 is not None:
+        xf[0] = fp2(XF0)
     recs = []
     for k in range(6):
         re, im = [], []
@@ -127,7 +133,10 @@ def op_sqr12(name, F, XF, conj=False):
                     continue
                 wrap = i + j >= 6
                 y = xf[j] if wrap else f[j]
-                if i == j and not wrap:
+                if i == j and not wrap and i in xf:
+                    r = [T(xf[i][0], xf[i][1])]       # (a - b)(a + b)
+                    m = [T(f[i][0], f[i][1], 1, 2)]   # 2ab
+                elif i == j and not wrap:
                     r, m = sqr_terms(f[i])
                 elif i == j:
                     r, m = mul_terms(f[i], y)
@@ -532,6 +541,7 @@ def lines_subgroup_op():
 
 # ---------------------------------------------------------------- k_miller slots
 M_F, M_X, M_L1, M_L2 = 0, 12, 22, 28      # F (12), xi-copies (10), line 1 (6), line 2 (6)
+M_XF0 = 34                                # xi-copy of F's w^0 coefficient (the squaring's f0^2)
 M_N, M_XN2, M_T, M_XT, M_D, M_N1 = 22, 12, 14, 28, 20, 12  # norm epilogue (after the loop)
 
 # ---------------------------------------------------------------- k_fe slots
@@ -547,8 +557,9 @@ def build_ops():
     ops.append(lines_add_op())
     ops.append(lines_subgroup_op())
     # k_miller
-    ops.append(op_xi_copy("M_XIF", M_F, M_X, [1, 2, 3, 4, 5]))
-    ops.append(op_sqr12("M_SQR", M_F, M_X))
+    ops.append(pack("M_XIF", op_xi_copy("_a", M_F, M_X, [1, 2, 3, 4, 5]).subs[0] +
+                    op_xi_copy("_b", M_F, M_XF0, [0]).subs[0]))
+    ops.append(op_sqr12("M_SQR", M_F, M_X, XF0=M_XF0))
     # xi l2, xi l3 for both lines: L1 (l0, l2, l3) at 22, L2 at 28 -> X 12..15 and 16..19
     ops.append(pack("M_XIL", op_xi_copy("_a", M_L1, M_X, [1, 2]).subs[0] + op_xi_copy("_b", M_L2, M_X + 4, [1, 2]).subs[0]))
     ops.append(op_line_mul("M_LM1", M_F, M_L1, M_X))
@@ -1150,7 +1161,7 @@ def check_bounds(ops):
 # [24, 65, 113, 161, 202], FE [24, 71, 117, 164, 210] with the hard part's
 # blocks reordered), but those measured slower (profiles/r02/r02s_group_bases_ab.json:
 # lines +3%, Miller +2%), so the layout stays packed.
-GROUP_BASES = {k: [N_CONST + g * n for g in range(5)] for k, n in (("LINES", 50), ("MILLER", 34), ("FE", 46))}
+GROUP_BASES = {k: [N_CONST + g * n for g in range(5)] for k, n in (("LINES", 50), ("MILLER", 36), ("FE", 46))}
 
 
 def emit(path):

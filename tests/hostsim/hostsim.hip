@@ -461,6 +461,14 @@ void host_run_op(HostGroup& G, int op) {
         else G.n1 = outs[k];
       }
     }
+    const uint32_t fz = (ntw >> 21) & 0xFFu;  // fused epilogue (engine.cuh eng_fuse_epilogue)
+    if (fz) {
+      for (int k = 0; k < ENG_LANES; ++k) {
+        const uint32_t w = ENG_FUSE_TAB[fz - 1][k], mode = w >> 16;
+        if (mode) G.set((int)(w & 0xFFFFu), mode == 1 ? eng_cyc_sum(outs[k], outs[k ^ 1], false)
+                                                      : eng_cyc_sum(outs[k ^ 1], outs[k], true));
+      }
+    }
   }
 }
 

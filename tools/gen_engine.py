@@ -90,12 +90,32 @@ def fp12(base):
 
 
 # ---------------------------------------------------------------- op builders
+# Fused epilogue of a sub-op (FUSE_SUM / FUSE_DIFF per lane): after the
+# sub-op's outputs are stored, lane k forms from its own output and its DPP
+# partner's (lane k ^ 1, the other half of the same Fp2 value) own + partner
+# (SUM, the re lane: re + im) or partner - own + 8p (DIFF, the im lane:
+# re - im), normalized and NOT reduced (< 4.02p / < 10.02p), into slot dst --
+# the a +- b sums a later squaring's one-product real part (a+b)(a-b) needs.
+FUSE_SUM, FUSE_DIFF = 1, 2
+FUSE_BOUND = {FUSE_SUM: 4.02, FUSE_DIFF: 10.02}
+
+
 class Op:
-    def __init__(self, name, subs):
+    def __init__(self, name, subs, fuse=None):
         self.name = name
         self.subs = subs  # list of list[Rec] (<= 12 each)
         for s in subs:
             assert len(s) <= LANES, (name, len(s))
+        # {sub index: [(dst slot, FUSE_*) or None per lane]}
+        self.fuse = fuse or {}
+        for si, lanes in self.fuse.items():
+            sub = subs[si]
+            for k, f in enumerate(lanes):
+                if f is None:
+                    continue
+                # the partner lane holds the other half of the same Fp2 output
+                assert sub[k].dst is not None and sub[k ^ 1].dst == sub[k].dst ^ 1, (name, si, k)
+                assert f[1] == (FUSE_SUM if sub[k].dst % 2 == 0 else FUSE_DIFF), (name, si, k)
 
 
 def pack(name, recs):
@@ -394,6 +414,7 @@ def op_cyclo_sqr(name, R, TMP):
 # PubPoly.Eval(i) in threshold recovery); pair 1's (-g1) is a block constant.
 LINE_PAIR_SLOTS = 24
 L_NXP0, L_YP0 = 48, 49
+L_YS = 16      # per pair: YS, YD, ZS, ZD = Y.re +- Y.im, Z.re +- Z.im (live from a step's last sub-op to the next S2)
 
 
 def _pb(p, off):
@@ -420,9 +441,12 @@ def lines_dbl_op():
         fp2_out(S1, X2, *sqr_terms(X))
         fp2_out(S1, XY, *mul_terms(X, Y))
         fp2_out(S1, YZ, *mul_terms(Y, Z))
-        # S2: t0 = Y^2 -> X slot, t1 = Z^2 -> Y slot; l2 = 3 X2 (-xP) (export)
-        fp2_out(S2, X, *sqr_terms(Y))
-        fp2_out(S2, Y, *sqr_terms(Z))
+        # S2: t0 = Y^2 -> X slot, t1 = Z^2 -> Y slot; l2 = 3 X2 (-xP) (export).
+        # The squares' real parts are one product (a+b)(a-b) of the sums the
+        # previous step's last sub-op (or LINIT) left in YS, YD, ZS, ZD
+        YS, YD, ZS, ZD = _pb(p, L_YS), _pb(p, L_YS + 1), _pb(p, L_YS + 2), _pb(p, L_YS + 3)
+        fp2_out(S2, X, [T(YS, YD)], [T(Y[0], Y[1], 1, 2)])
+        fp2_out(S2, Y, [T(ZS, ZD)], [T(Z[0], Z[1], 1, 2)])
         S2.append(Rec(exp=6 * p + 2, cm=3, terms=[T(X2[0], nxp)]))
         S2.append(Rec(exp=6 * p + 3, cm=3, terms=[T(X2[1], nxp)]))
         t0, t1 = X, Y
@@ -452,7 +476,7 @@ def lines_dbl_op():
         fp2_out(S5, X, *mul_terms(XY, U, coef=2))
         fp2_out(S5, Y, [T(VP, VM), T(WP, W12M, -1)], [T(V[0], V[1], 1, 2), T(W[0], W12[1], -1, 2)])
         fp2_out(S5, Z, *mul_terms(t0, YZ), cm=8)
-    return Op("LDBL", [S1, S2, S3, S4, S4b, S5])
+    return Op("LDBL", [S1, S2, S3, S4, S4b, S5], fuse={5: _yz_fuse()})
 
 
 def lines_add_op():
@@ -503,7 +527,31 @@ def lines_add_op():
         c, d = mul_terms(Y, E, sign=-1)
         fp2_out(S6, Y, a + c, b + d)
         fp2_out(S6, Z, *mul_terms(Z, E))
-    return Op("LADD", [S1, S2, S3, S4, S5, S6])
+    return Op("LADD", [S1, S2, S3, S4, S5, S6], fuse={5: _yz_fuse()})
+
+
+def _yz_fuse():
+    """The fused epilogue of the sub-op that writes (X, Y, Z) of both pairs
+    (lanes 6p + 0..5 = X, Y, Z re/im): Y and Z's a+-b sums for the next
+    doubling's S2."""
+    lanes = [None] * LANES
+    for p in range(2):
+        for c, base in ((1, L_YS), (2, L_YS + 2)):   # Y, Z
+            lanes[6 * p + 2 * c] = (_pb(p, base), FUSE_SUM)
+            lanes[6 * p + 2 * c + 1] = (_pb(p, base + 1), FUSE_DIFF)
+    return lanes
+
+
+def lines_init_op():
+    """LINIT: the sums YS, YD, ZS, ZD of the initial T = (xQ, yQ, 1) for both
+    pairs (afterwards each step's last sub-op forms them, _yz_fuse)."""
+    recs = []
+    for p in range(2):
+        Y, Z = fp2(_pb(p, 2)), fp2(_pb(p, 4))
+        for src, base in ((Y, L_YS), (Z, L_YS + 2)):
+            recs.append(Rec(dst=_pb(p, base), post=[(src[0], 1), (src[1], 1)]))
+            recs.append(Rec(dst=_pb(p, base + 1), post=[(src[0], 1), (src[1], -1)]))
+    return pack("LINIT", recs)
 
 
 # After the loop T of pair 1 is [|x|] sigma (the ladder of |x| = 0xd201000000010000,
@@ -556,6 +604,7 @@ def build_ops():
     ops.append(lines_dbl_op())
     ops.append(lines_add_op())
     ops.append(lines_subgroup_op())
+    ops.append(lines_init_op())
     # k_miller
     ops.append(pack("M_XIF", op_xi_copy("_a", M_F, M_X, [1, 2, 3, 4, 5]).subs[0] +
                     op_xi_copy("_b", M_F, M_XF0, [0]).subs[0]))
@@ -610,7 +659,7 @@ BITS = [(0xD201000000010000 >> i) & 1 for i in range(62, -1, -1)]
 
 
 def prog_lines():
-    prog = []
+    prog = [("run", "LINIT")]
     for b in BITS:
         prog += [("run", "LDBL"), ("step",)]
         if b:
@@ -776,18 +825,33 @@ def slot_ref(s):
     return (s * SLOT_WORDS) if s < 64 else (((s - 64) * SLOT_WORDS) | 0x400)
 
 
+def fuse_tables(ops):
+    """Per fused sub-op (in op order): 12 lane words dst | FUSE_* << 16
+    (0xFFFF: no epilogue on that lane).  Returns (tables, {(op, sub): 1-based index})."""
+    tabs, idx = [], {}
+    for op in ops:
+        for si in sorted(op.fuse):
+            lanes = op.fuse[si] + [None] * (LANES - len(op.fuse[si]))
+            tabs.append([0xFFFF if f is None else f[0] | f[1] << 16 for f in lanes])
+            idx[(op.name, si)] = len(tabs)
+    return tabs, idx
+
+
 def encode(ops):
     words = []
     op_tab = []
     sub_tab = []
+    _, fidx = fuse_tables(ops)
+    assert len(fidx) < 256
     for op in ops:
         op_tab.append((len(sub_tab), len(op.subs)))
-        for sub in op.subs:
+        for si, sub in enumerate(op.subs):
             nt = max([len(r.terms) for r in sub] + [0])
             assert nt <= MAX_TERMS, (op.name, nt)
             ntp = (nt + 3) & ~3   # records are 16-byte aligned: header + terms padded to 4 words
             uses_c = any(x >= 64 for r in sub for t in r.terms for x in t[:2]) or any(x >= 64 for r in sub for x, _ in r.post)
-            sub_tab.append((len(words), nt | norm_schedule(sub) << 8 | uses_c << 20))
+            fz = fidx.get((op.name, si), 0)
+            sub_tab.append((len(words), nt | norm_schedule(sub) << 8 | uses_c << 20 | fz << 21))
             for k in range(LANES):
                 r = sub[k] if k < len(sub) else None
                 if r is None:
@@ -1102,6 +1166,9 @@ def emit_compiled(ops, sub_tab, path):
                 out.append("    if ((h0 & 0xFFu) != 0xFFu) eng_st(g + (h0 & 0xFFu) * ENG_SLOT_WORDS, o);")
             if has_exp:
                 out.append("    if (((h0 >> 8) & 0xFFu) != 0xFFu) sink((h0 >> 8) & 0xFFu, o);")
+            fz = (ntw >> 21) & 0xFF
+            if fz:
+                out.append(f"    eng_fuse_epilogue(g, o, ENG_FUSE_TAB[{fz - 1}][k], k);")
             out.append("    asm volatile(\"\" ::: \"memory\");")
             out.append("  }")
         out.append("}")
@@ -1135,15 +1202,30 @@ def emit_compiled(ops, sub_tab, path):
         f.write("\n".join(out) + "\n")
 
 
+def fused_reads(op):
+    """{sub index: {slot: bound in p}}: the sub-ops that read a fused
+    epilogue's unreduced sums (LDBL's S2 reads the a+-b sums of Y and Z)."""
+    wide = {}
+    if op.name == "LDBL":
+        wide[1] = {}
+        for p in range(2):
+            for j in range(4):
+                wide[1][_pb(p, L_YS + j)] = FUSE_BOUND[FUSE_SUM if j % 2 == 0 else FUSE_DIFF]
+    return wide
+
+
 def check_bounds(ops):
     """Static bounds the device arithmetic relies on (see engine.cuh):
-    slot values < 2.01p; product sum < 2048 p^2 so redc < 1.8p; the post
-    linear combination stays < 2^392."""
+    slot values < 2.01p (fused-epilogue sums: fused_reads); product sum
+    < 2048 p^2 so redc < 1.8p; the post linear combination stays < 2^392."""
     for op in ops:
-        for sub in op.subs:
+        wide = fused_reads(op)
+        for si, sub in enumerate(op.subs):
+            bnd = lambda s: wide.get(si, {}).get(s, 2.01)  # noqa: E731
             for r in sub:
-                # negated operands are 8p - b (FP_SUBK), < 8p
-                prod = sum(cf * 2.01 * (8.0 if sg < 0 else 2.01) for _, _, sg, cf in r.terms)
+                # negated operands are 8p - b (FP_SUBK), < 8p: b < 7.99p
+                assert all(not (sg < 0 and bnd(b) >= 7.99) for _, b, sg, _ in r.terms), op.name
+                prod = sum(cf * bnd(a) * (8.0 if sg < 0 else bnd(b)) for a, b, sg, cf in r.terms)
                 assert prod < 2048, (op.name, prod)
                 # redc output < 1.8p; negative multipliers act on 8p - x
                 lin = abs(r.cm) * (8.0 if r.cm < 0 else 1.8) + sum(abs(d) * (8.0 if d < 0 else 2.01) for _, d in r.post)
@@ -1235,6 +1317,13 @@ def emit(path):
         for t, (_, _, sg, cf) in enumerate(sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2))):
             xf |= (sg < 0) << t | (cf == 2) << (16 + t)
     lines.append(f"constexpr uint32_t ENG_CYC_XF = 0x{xf:x}u;")
+    ftabs, _ = fuse_tables(ops)
+    lines.append("// fused epilogues (tools/gen_engine.py fuse_tables): per fused sub-op, lane word dst | mode << 16")
+    lines.append(f"constexpr int ENG_NFUSE = {len(ftabs)};")
+    lines.append(f"ENG_TABLE_QUAL uint32_t ENG_FUSE_TAB[{max(1, len(ftabs))}][{LANES}] = {{")
+    for t in ftabs:
+        lines.append("  {" + ", ".join(f"0x{x:08x}u" for x in t) + "},")
+    lines.append("};")
     lines.append(f"alignas(16) ENG_TABLE_QUAL uint32_t ENG_CYC_PAR[{LANES}][8] = {{")
     for w in rows:
         lines.append("  {" + ", ".join(f"0x{x:08x}u" for x in w) + "},")
@@ -1309,6 +1398,10 @@ class Model:
                     self.s[r.dst] = v
                 if r.exp is not None:
                     self.exports[r.exp] = v
+            for k, f in enumerate(self.ops[name].fuse.get(self.ops[name].subs.index(sub), [])):
+                if f is not None:
+                    own, par = outs[k][1], outs[k ^ 1][1]
+                    self.s[f[0]] = (own + par) % p if f[1] == FUSE_SUM else (par - own) % p
 
 
 if __name__ == "__main__":

@@ -429,9 +429,12 @@ def lines_dbl_op():
       X4 = 2 XY u,  Y4 = v^2 - 12 w^2,  Z4 = 8 t0 YZ
       l0 = t0 - w,  l2 = 3 X^2 (-xP),  l3 = 2 YZ yP
     Y4 = (v0 + v1)(v0 - v1) - (w0 + w1)(12w0 - 12w1) + (2 v0 v1 - 2 w0 12w1) u
-    over the sums of a LIN pass (S4b), so no lane of S5 needs more than two
-    products (the sub-op costs its busiest lane)."""
-    S1, S2, S3, S4, S4b, S5 = [], [], [], [], [], []
+    over sums that S3's and S4's fused epilogues form (round 2 ran a LIN
+    sub-op, S4b, for them), so no lane of S5 needs more than two products
+    (the sub-op costs its busiest lane); likewise S2's squares take one
+    product each over the sums of Y and Z that S5's epilogue (or LADD's, or
+    LINIT) leaves in YS, YD, ZS, ZD.  Five sub-ops."""
+    S1, S2, S3, S4, S5 = [], [], [], [], []
     for p in range(2):
         X, Y, Z = fp2(_pb(p, 0)), fp2(_pb(p, 2)), fp2(_pb(p, 4))
         X2, XY, YZ = fp2(_pb(p, 10)), fp2(_pb(p, 12)), fp2(_pb(p, 14))
@@ -465,18 +468,22 @@ def lines_dbl_op():
         S4.append(Rec(exp=6 * p + 4, cm=2, terms=[T(YZ[0], yp)]))
         S4.append(Rec(exp=6 * p + 5, cm=2, terms=[T(YZ[1], yp)]))
         W12 = Y
-        # S4b (LIN): vp = v0 + v1, vm = v0 - v1 (X2's slots, dead after S2), wp = w0 + w1,
-        # w12m = 12 w0 - 12 w1 (22, 23)
+        # the sums vp = v0 + v1, vm = v0 - v1 (X2's slots, dead after S2) and
+        # wp = w0 + w1 (22) come from S3's fused epilogue, w12m = 12 w0 - 12 w1
+        # (23) from S4's (unreduced: w12m is S5's a operand, wp the negated b)
         VP, VM, WP, W12M = _pb(p, 10), _pb(p, 11), _pb(p, 22), _pb(p, 23)
-        S4b.append(Rec(dst=VP, post=[(V[0], 1), (V[1], 1)]))
-        S4b.append(Rec(dst=VM, post=[(V[0], 1), (V[1], -1)]))
-        S4b.append(Rec(dst=WP, post=[(W[0], 1), (W[1], 1)]))
-        S4b.append(Rec(dst=W12M, post=[(W12[0], 1), (W12[1], -1)]))
         # S5: X4 = 2 XY u -> X, Y4 = v^2 - w w12 -> Y, Z4 = 8 t0 YZ -> Z
         fp2_out(S5, X, *mul_terms(XY, U, coef=2))
-        fp2_out(S5, Y, [T(VP, VM), T(WP, W12M, -1)], [T(V[0], V[1], 1, 2), T(W[0], W12[1], -1, 2)])
+        fp2_out(S5, Y, [T(VP, VM), T(W12M, WP, -1)], [T(V[0], V[1], 1, 2), T(W[0], W12[1], -1, 2)])
         fp2_out(S5, Z, *mul_terms(t0, YZ), cm=8)
-    return Op("LDBL", [S1, S2, S3, S4, S4b, S5], fuse={5: _yz_fuse()})
+    # S3 lanes 6p + (0..5) = W, U, V (re, im); S4 lanes 6p + (2, 3) = w12
+    f3, f4 = [None] * LANES, [None] * LANES
+    for p in range(2):
+        f3[6 * p + 0] = (_pb(p, 22), FUSE_SUM)      # wp
+        f3[6 * p + 4] = (_pb(p, 10), FUSE_SUM)      # vp
+        f3[6 * p + 5] = (_pb(p, 11), FUSE_DIFF)     # vm
+        f4[6 * p + 3] = (_pb(p, 23), FUSE_DIFF)     # w12m
+    return Op("LDBL", [S1, S2, S3, S4, S5], fuse={2: f3, 3: f4, 4: _yz_fuse()})
 
 
 def lines_add_op():
@@ -1211,6 +1218,10 @@ def fused_reads(op):
         for p in range(2):
             for j in range(4):
                 wide[1][_pb(p, L_YS + j)] = FUSE_BOUND[FUSE_SUM if j % 2 == 0 else FUSE_DIFF]
+        wide[4] = {}
+        for p in range(2):
+            for off, mode in ((10, FUSE_SUM), (11, FUSE_DIFF), (22, FUSE_SUM), (23, FUSE_DIFF)):
+                wide[4][_pb(p, off)] = FUSE_BOUND[mode]
     return wide
 
 

@@ -619,7 +619,16 @@ def build_ops():
     # xi l2, xi l3 for both lines: L1 (l0, l2, l3) at 22, L2 at 28 -> X 12..15 and 16..19
     ops.append(pack("M_XIL", op_xi_copy("_a", M_L1, M_X, [1, 2]).subs[0] + op_xi_copy("_b", M_L2, M_X + 4, [1, 2]).subs[0]))
     ops.append(op_line_mul("M_LM1", M_F, M_L1, M_X))
-    ops.append(op_line_mul("M_LM2", M_F, M_L2, M_X + 4))
+    lm2 = op_line_mul("M_LM2", M_F, M_L2, M_X + 4)
+    # its fused epilogue leaves xi f = (re - im, re + im) of every coefficient
+    # for the next step's M_SQR (the loop's M_XIF pass, round 2, is gone):
+    # the re lane's re + im is the copy's im half, the im lane's re - im its re half
+    lanes = [None] * LANES
+    for k in range(6):
+        xr = M_XF0 if k == 0 else M_X + 2 * (k - 1)
+        lanes[2 * k] = (xr + 1, FUSE_SUM)
+        lanes[2 * k + 1] = (xr, FUSE_DIFF)
+    ops.append(Op("M_LM2", lm2.subs, fuse={0: lanes}))
     ops.append(op_norm6("M_NRM", M_F, M_X, M_N))
     ops.append(op_xi_copy("M_XIN2", M_N, M_XN2, [2]))
     ops.append(op_fp6_inv_t("M_T012", M_N, M_XN2, M_T))
@@ -678,8 +687,8 @@ def prog_miller():
     prog = []
     line = [("ldline", M_L1), ("run", "M_XIL"), ("run", "M_LM1"), ("run", "M_LM2")]
     for j, b in enumerate(BITS):
-        if j:
-            prog += [("run", "M_XIF"), ("run", "M_SQR")]
+        if j:   # M_SQR's xi-copies of f: the previous M_LM2's fused epilogue
+            prog += [("run", "M_SQR")]
         prog += line
         if b:
             prog += line
@@ -795,9 +804,12 @@ def _slot_limb_max(bound_p=2.01):
     return [(1 << 28) - 1] * 13 + [top]
 
 
-def norm_schedule(sub):
-    """Bit t set: normalize after term t (encoded term order)."""
-    amax = _slot_limb_max()
+def norm_schedule(sub, wide=None):
+    """Bit t set: normalize after term t (encoded term order).  wide: {slot:
+    bound in p} of operands above the slot bound (fused_reads)."""
+    amax0 = _slot_limb_max()
+    wide = wide or {}
+    amax_of = lambda s: _slot_limb_max(wide[s]) if s in wide else amax0  # noqa: E731
     subk = _subk_limbs()
     LIM, LIM_REDC = (1 << 64) - 1, (1 << 64) - (1 << 60)
     lanes = [sorted(r.terms, key=lambda x: (x[2] < 0) + (x[3] == 2)) for r in sub]
@@ -810,8 +822,9 @@ def norm_schedule(sub):
         for terms in lanes:
             g = [0] * 28
             if t < len(terms):
-                _, _, sg, cf = terms[t]
-                bmax = [(subk[j] if sg < 0 else amax[j]) << (cf - 1) for j in range(14)]
+                a, b, sg, cf = terms[t]
+                amax, bm = amax_of(a), amax_of(b)
+                bmax = [(subk[j] if sg < 0 else bm[j]) << (cf - 1) for j in range(14)]
                 for i in range(14):
                     for j in range(14):
                         g[i + j] += amax[i] * bmax[j]
@@ -858,7 +871,8 @@ def encode(ops):
             ntp = (nt + 3) & ~3   # records are 16-byte aligned: header + terms padded to 4 words
             uses_c = any(x >= 64 for r in sub for t in r.terms for x in t[:2]) or any(x >= 64 for r in sub for x, _ in r.post)
             fz = fidx.get((op.name, si), 0)
-            sub_tab.append((len(words), nt | norm_schedule(sub) << 8 | uses_c << 20 | fz << 21))
+            ns = norm_schedule(sub, fused_reads(op).get(si))
+            sub_tab.append((len(words), nt | ns << 8 | uses_c << 20 | fz << 21))
             for k in range(LANES):
                 r = sub[k] if k < len(sub) else None
                 if r is None:
@@ -1222,6 +1236,12 @@ def fused_reads(op):
         for p in range(2):
             for off, mode in ((10, FUSE_SUM), (11, FUSE_DIFF), (22, FUSE_SUM), (23, FUSE_DIFF)):
                 wide[4][_pb(p, off)] = FUSE_BOUND[mode]
+    if op.name == "M_SQR":   # the xi-copies (re - im, re + im) of f from M_LM2's epilogue
+        wide[0] = {}
+        for k in range(6):
+            xr = M_XF0 if k == 0 else M_X + 2 * (k - 1)
+            wide[0][xr] = FUSE_BOUND[FUSE_DIFF]
+            wide[0][xr + 1] = FUSE_BOUND[FUSE_SUM]
     return wide
 
 

@@ -170,8 +170,15 @@ def recover_work(t, slices=5):
 KB_STAGE_WORK = {"eng_fe": "k_eng_fe_seg", "eng_fe_chain": "k_eng_kb_chain", "eng_fe_kbinv": "k_eng_kb_inv"}
 
 
+# the T-steps run per thread (k_lines_thr) unless DGPU_LINES=engine selects
+# the 12-lane engine program (k_eng_lines)
+if os.environ.get("DGPU_LINES") != "engine":
+    for _p in ("g2", "recover"):
+        STAGE_WORK[_p]["eng_lines"] = "k_lines_thr"
+
+
 # stage -> kernel symbol for the traffic lookup
-STAGE_KERNEL = {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
+STAGE_KERNEL = {"eng_lines": STAGE_WORK["g2"]["eng_lines"], "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv", "eng_fe": "k_eng_fe",
                 "eng_lines_fixed": "k_eng_lines_fixed", "hash_to_g2": "hash_to_g2", "decode_g2": "k_decode_g2_sigs",
                 "hash_to_g1": "k_hash_to_g1_beacons", "decode_g1": "k_decode_g1_sigs",
                 "rlc_leaves_tree": "k_rlc_leaves"}

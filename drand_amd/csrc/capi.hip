@@ -19,6 +19,7 @@
 #include "../../include/drand_gpu.h"
 #include "kernels.cuh"
 #include "pairing_engine.cuh"
+#include "lines_thread.cuh"
 #include "recover.cuh"
 #include "g1sig.cuh"
 #include "rlc_msm.cuh"
@@ -177,6 +178,7 @@ struct dgpu_ctx {
   size_t kb_test_flag = 0;       // DGPU_KB_TEST_FLAG=k (tests): flag every k-th item so the fallback runs
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
+  bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
@@ -697,7 +699,11 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                            fixed_table, lines);
       } else {
         mark(c, s, "eng_lines");
-        hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, r0, cnt, h, h_stride, h_idx, sg,
+        if (c->lines_thread)
+          hipLaunchKernelGGL(k_lines_thr, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, n, r0, cnt, h, h_stride, h_idx,
+                             sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
+        else
+          hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, r0, cnt, h, h_stride, h_idx, sg,
                            pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
       }
       HIP_TRY(hipGetLastError());
@@ -1006,6 +1012,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
   const char* ec = getenv("DGPU_ENG_CHUNK");
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
+  const char* lnv = getenv("DGPU_LINES");
+  if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");

@@ -1,0 +1,160 @@
+// Per-thread T-steps of the two Miller loops: one thread per (round, pair),
+// the G2 point T in registers, 68 steps of line coefficients written to the
+// engine's blocked line buffer (pairing_engine.cuh: [b][step][limb][g][6p+e]),
+// where k_eng_miller consumes them.  Same contract as k_eng_lines (which stays
+// for the on-G1 fixed-line table): pairs (pk, H_i) and (-g1, S_i), and the
+// fused G2 membership test of S_i on pair 1's final T = [|x|] S_i.
+//
+// Why per thread: the T-steps carry no Fp12 state, so a thread holds one pair's
+// point (6 Fp) and runs the step formulas with every Fp product on its own
+// lanes -- no LDS slot round trips or per-sub-op waits of the 12-lane engine.
+//
+// Reference: chain/verify.go:44 -> kyber bls.Verify -> kilic Engine
+// (miller loop line evaluations, R).  Line convention as pairing.cuh
+// miller_dbl_step / miller_add_step: l = c0 + c2 w^2 + c3 w^3 with c2 linear in
+// -xP and c3 in yP; each line may carry any Fp2 scale (killed by the final
+// exponentiation), so the doubling below runs a 4x-scaled T with no halvings.
+#pragma once
+#include "pairing.cuh"
+
+namespace dgpu {
+
+// Doubling with its tangent line, homogeneous projective T (x = X/Z, y = Y/Z),
+// E': y^2 = x^3 + b', b' = 4 xi.  With t0 = Y^2, t2 = 3 b' Z^2 = 12 xi Z^2,
+// t3 = 3 t2:
+//   X' = 2XY (t0 - t3), Y' = (t0 + t3)^2 - 12 t2^2, Z' = 4 t0 (2YZ)
+//   (4x the classical (XY/2 (t0 - t3), ((t0 + t3)/2)^2 - 3 t2^2, t0 2YZ)),
+//   line: c0 = t0 - t2, c2 = 3 X^2 (-xP), c3 = 2YZ yP.
+// 2XY and 2YZ as (X + Y)^2 - X^2 - Y^2 and (Y + Z)^2 - Y^2 - Z^2.
+// Bounds (units of p; CI = normalized, < 2.01p; fp_mul outputs < 1.01p here):
+//   X + Y, Y + Z carried (< 4.02p) into fp2_sqr; t2 = 12 (xi Z^2) from the
+//   carried lazy xi Z^2 (< 10.01p, limbs < 2^28 so 12x < 2^32) reduced to CI;
+//   t3 = 3 t2 carried (< 6.03p); t0 + t3 carried (< 7.04p: fp2_sqr's
+//   second coefficient < 7.99p); t0 + 8p - t3 carried (< 9.04p) into fp2_mul;
+//   12 t2^2 carried (< 12.1p, fp2_sub32's bound 31.9p); 4 t0 carried (< 4.04p).
+DG_FN line3 lt_dbl(g2p& T, const fp& nxp, const fp& yp) {
+  const fp2 t0 = fp2_sqr(T.y);
+  const fp2 t1 = fp2_sqr(T.z);
+  const fp2 x2 = fp2_sqr(T.x);
+  const fp2 yz2 = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(T.y, T.z))), fp2_add_lz(t0, t1));
+  const fp2 xy2 = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(T.x, T.y))), fp2_add_lz(x2, t0));
+  const fp2 xt1 = fp2_carry(fp2{fp_sub_lz(t1.c0, t1.c1), fp_add_lz(t1.c0, t1.c1)});
+  const fp2 t2 = fp2{fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c0)), fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c1))};
+  const fp2 t3 = fp2_carry(fp2_add_lz(fp2_add_lz(t2, t2), t2));
+  line3 l;
+  l.c0 = fp2_sub(t0, t2);
+  l.c2 = fp2_mul_fp(fp2_carry(fp2_add_lz(fp2_add_lz(x2, x2), x2)), nxp);
+  l.c3 = fp2_mul_fp(yz2, yp);
+  const fp2 t2sq = fp2_sqr(t2);
+  T.x = fp2_mul(xy2, fp2_carry(fp2{fp_sub_lz(t0.c0, t3.c0), fp_sub_lz(t0.c1, t3.c1)}));
+  T.y = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(t0, t3))), fp2_carry(fp2_mulk_lz(t2sq, 12)));
+  T.z = fp2_mul(fp2_carry(fp2_mulk_lz(t0, 4)), yz2);
+  return l;
+}
+
+// Mixed addition T + Q (Q affine) with its chord line (pairing.cuh
+// miller_add_step's formulas; 5 of the 68 steps).
+DG_FN line3 lt_add(g2p& T, const g2a& Q, const fp& nxp, const fp& yp) {
+  const fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
+  const fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  const fp2 C = fp2_sqr(theta);
+  const fp2 D = fp2_sqr(lam);
+  const fp2 E = fp2_mul(lam, D);
+  const fp2 F = fp2_mul(T.z, C);
+  const fp2 G = fp2_mul(T.x, D);
+  const fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
+  line3 l;
+  l.c0 = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y));
+  l.c2 = fp2_mul_fp(theta, nxp);
+  l.c3 = fp2_mul_fp(lam, yp);
+  const fp2 ye = fp2_mul(T.y, E);
+  T.x = fp2_mul(lam, H);
+  T.y = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), ye);
+  T.z = fp2_mul(T.z, E);
+  return l;
+}
+
+// One pair's 68 T-steps (63 doublings, additions at the 5 lower set bits of
+// |x|), sink(step, line) per step; returns the final T = [|x|] Q.
+template <class Sink>
+DG_FN g2p lt_pair(const g2a& Q, const fp& nxp, const fp& yp, Sink&& sink) {
+  g2p T{Q.x, Q.y, fp2_one()};
+  int step = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    sink(step++, lt_dbl(T, nxp, yp));
+    if ((BLS_X_ABS >> i) & 1ull) sink(step++, lt_add(T, Q, nxp, yp));
+  }
+  return T;
+}
+
+// psi(S) == -T for T = [|x|] S (homogeneous): X = x_psi Z, Y = -y_psi Z, Z != 0
+// (Scott's G2 membership test, as the engine's LSUB op).
+DG_FN bool lt_in_g2(const g2p& T, const g2a& S) {
+  const g2a ps = g2a_psi(S);
+  return !fp2_is_zero(T.z) && fp2_is_zero(fp2_sub(T.x, fp2_mul(ps.x, T.z))) &&
+         fp2_is_zero(fp2_add(T.y, fp2_mul(ps.y, T.z)));
+}
+
+#ifndef DG_NO_KERNELS
+}  // namespace dgpu
+#include "pairing_engine.cuh"
+namespace dgpu {
+
+#ifndef DG_LINES_OCC
+#define DG_LINES_OCC 2
+#endif
+// Thread t: chunk-local round i = t / 2, pair p = t % 2.  Arguments as
+// k_eng_lines (pairing_engine.cuh); consts: the engine constant block (pair
+// points (-x, y) in slots ENG_C_NXP0..ENG_C_YP1).  Each step's 6 exports of
+// the pair are 6 consecutive words per limb plane, written as 3 dwordx2.
+__global__ void __launch_bounds__(256, DG_LINES_OCC) k_lines_thr(size_t n, size_t r0, size_t cnt,
+                                                                 const uint32_t* __restrict__ h_pts, size_t h_stride,
+                                                                 const uint32_t* __restrict__ h_idx,
+                                                                 const uint32_t* __restrict__ sig_pts,
+                                                                 const uint32_t* __restrict__ pk_items,
+                                                                 const uint32_t* __restrict__ consts,
+                                                                 uint32_t* __restrict__ lines,
+                                                                 uint8_t* __restrict__ status) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = t >> 1;
+  const int p = (int)(t & 1);
+  if (i >= cnt) return;
+  const size_t r = r0 + i;
+  const uint32_t* qb = p ? sig_pts : h_pts;
+  const size_t qs = p ? n : h_stride;
+  const size_t qi = p ? r : (h_idx ? (size_t)h_idx[r] : r);
+  g2a Q;
+  Q.x.c0 = ld_soa(qb, qs, qi);
+  Q.x.c1 = ld_soa(qb + (size_t)FP_LIMBS * qs, qs, qi);
+  Q.y.c0 = ld_soa(qb + (size_t)2 * FP_LIMBS * qs, qs, qi);
+  Q.y.c1 = ld_soa(qb + (size_t)3 * FP_LIMBS * qs, qs, qi);
+  fp nxp, yp;
+  if (p == 0 && pk_items) {
+    nxp = ld_soa(pk_items, n, r);
+    yp = ld_soa(pk_items + (size_t)FP_LIMBS * n, n, r);
+  } else {
+    const int s0 = (p ? ENG_C_NXP1 : ENG_C_NXP0) - 64;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      nxp.l[l] = consts[s0 * ENG_SLOT_WORDS + l];
+      yp.l[l] = consts[(s0 + 1) * ENG_SLOT_WORDS + l];
+    }
+  }
+  const size_t blk = i / ENG_ROUNDS_PER_BLOCK;
+  uint32_t* base = lines + eng_blk_off(blk, ENG_LINE_STEPS, 0, (int)(i % ENG_ROUNDS_PER_BLOCK), 6 * p);
+  const g2p T = lt_pair(Q, nxp, yp, [&](int step, const line3& l) {
+    uint32_t* b = base + (size_t)step * FP_LIMBS * ENG_WAVE_WORDS;
+#pragma unroll
+    for (int k = 0; k < FP_LIMBS; ++k) {
+      uint2* w = reinterpret_cast<uint2*>(b + k * ENG_WAVE_WORDS);
+      w[0] = make_uint2(l.c0.c0.l[k], l.c0.c1.l[k]);
+      w[1] = make_uint2(l.c2.c0.l[k], l.c2.c1.l[k]);
+      w[2] = make_uint2(l.c3.c0.l[k], l.c3.c1.l[k]);
+    }
+  });
+  if (status && p == 1 && !lt_in_g2(T, Q) && status[r] == ST_OK) status[r] = ST_SUBGROUP;
+}
+#endif
+
+}  // namespace dgpu

@@ -8,6 +8,7 @@
 #include "../../drand_amd/csrc/pairing.cuh"
 #define DG_NO_KERNELS
 #include "../../drand_amd/csrc/g1sig.cuh"
+#include "../../drand_amd/csrc/lines_thread.cuh"
 
 using namespace dgpu;
 
@@ -43,6 +44,24 @@ int hs_count_stages(const uint8_t* pk48, const uint8_t* prev, uint32_t prev_len,
   bool ok = fp12_is_one(final_exponentiation(f));
   out[6] = dg_count_mul; out[7] = dg_count_sqr;
   return ok ? 0 : 3;
+#else
+  return -100;
+#endif
+}
+
+// Fp mul/sqr counts of k_lines_thr per round (DG_COUNT_OPS builds): both
+// pairs' 68 T-steps (lines_thread.cuh lt_pair) and the fused membership test.
+int hs_count_lines_thr(const uint8_t* sig96, unsigned long long* out) {
+#ifdef DG_COUNT_OPS
+  g2a s;
+  if (g2_decompress(&s, sig96, false) != DEC_OK) return -1;
+  const g2a h{C_G2_X, C_G2_Y};
+  dg_count_mul = dg_count_sqr = 0;
+  lt_pair(h, fp_neg(C_G1_X), C_G1_Y, [](int, const line3&) {});
+  const g2p T = lt_pair(s, fp_neg(C_G1_X), C_G1_NEG_Y, [](int, const line3&) {});
+  const bool in = lt_in_g2(T, s);
+  out[0] = dg_count_mul; out[1] = dg_count_sqr;
+  return in ? 0 : -2;
 #else
   return -100;
 #endif
@@ -587,6 +606,8 @@ bool host_slot_zero(const fp& x) { return fp_is_zero(x); }
 // -1 undecodable.
 extern "C" void hs_eng_set_cyc_fast(int on) { g_cyc_fast = on != 0; }
 extern "C" void hs_eng_set_fe_kb(int on) { g_fe_kb = on != 0; }
+bool g_lines_thread = false;  // T-steps from lines_thread.cuh lt_pair (k_lines_thr) instead of the LINES program
+extern "C" void hs_eng_set_lines_thread(int on) { g_lines_thread = on != 0; }
 extern "C" void hs_eng_set_compiled(int on) { g_compiled = on != 0; }
 
 // every compiled op vs the interpreter on the same random slots: 0 iff all
@@ -680,6 +701,10 @@ extern "C" int hs_eng_subgroup(const uint8_t* sig96) {
   G.set(ENG_L_NXP0, fp_neg(C_G1_X));
   G.set(ENG_L_YP0, C_G1_Y);
   G.step = 0;
+  if (g_lines_thread) {
+    const g2p T = lt_pair(s, fp_neg(C_G1_X), C_G1_NEG_Y, [](int, const line3&) {});
+    return lt_in_g2(T, s) ? 1 : 0;
+  }
   host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
   const bool d0 = host_slot_zero(G.get(ENG_L_SUB_D1)) && host_slot_zero(G.get(ENG_L_SUB_D1 + 1)) &&
                   host_slot_zero(G.get(ENG_L_SUB_D2)) && host_slot_zero(G.get(ENG_L_SUB_D2 + 1));
@@ -715,7 +740,16 @@ extern "C" int hs_eng_pairing(const uint8_t* pk48, const uint8_t* msg32, const u
   G.set(ENG_L_NXP0, fp_neg(pk.x));
   G.set(ENG_L_YP0, pk.y);
   G.step = 0;
-  host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
+  if (g_lines_thread) {
+    const fp nx[2] = {fp_neg(pk.x), fp_neg(C_G1_X)}, yv[2] = {pk.y, C_G1_NEG_Y};
+    for (int p = 0; p < 2; ++p)
+      lt_pair(q[p], nx[p], yv[p], [&](int step, const line3& l) {
+        const fp v[6] = {l.c0.c0, l.c0.c1, l.c2.c0, l.c2.c1, l.c3.c0, l.c3.c1};
+        for (int e = 0; e < 6; ++e) G.lines[step * 12 + 6 * p + e] = v[e];
+      });
+  } else {
+    host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
+  }
   for (int k = 0; k < 12; ++k) G.set(ENG_M_F + k, k == 0 ? fp_one() : fp_zero());
   G.step = 0;
   host_exec(G, ENG_PROG_MILLER, ENG_PROG_MILLER_LEN);

@@ -237,6 +237,26 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     assert np.array_equal(kb == 0, expect)
 
 
+def test_thread_lines_equal_engine_lines():
+    """The per-thread T-steps (k_lines_thr, default) against the 12-lane
+    engine's lines program (DGPU_LINES=engine): 20,011 rounds (ragged last
+    block), 1% corrupted -- identical reasons (x-bit flips that stay on the
+    curve exercise the fused membership test: REASON_SUBGROUP from both),
+    equal to the construction."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 20011
+    c = make_chain(23, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 23, rate=1e-2)
+    thr = _verify_with_env(c, {})
+    eng = _verify_with_env(c, {"DGPU_LINES": "engine"})
+    assert thr.tolist() == eng.tolist()
+    assert (thr == _lib.REASON_SUBGROUP).any()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(thr == 0, expect)
+
+
 def test_two_lane_per_round_large_chain():
     """A batch spanning two engine chunks runs on two lanes (streams, half the
     batch each, capi.hip verify_device_locked): 2*131072 + 1001 rounds (odd

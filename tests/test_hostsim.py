@@ -293,3 +293,38 @@ def test_engine_fused_subgroup_check(hostsim):
         q = B.iso_map_g2(B.map_to_curve_sswu_g2((rnd.randrange(P), rnd.randrange(P))))
         assert not B.g2_in_subgroup(q)
         assert hostsim.hs_eng_subgroup(B.g2_compress(q)) == 0
+
+
+def test_thread_lines_match_oracle_and_engine(hostsim):
+    """The per-thread T-steps (lines_thread.cuh lt_pair, k_lines_thr) feeding
+    the engine's Miller and FE programs give the oracle's exact GT value on
+    valid and invalid checks (each line may differ from the engine's by an Fp2
+    scale, which the final exponentiation removes), and their fused membership
+    test gives the oracle's verdicts."""
+    sk = D.derive_secret(15)
+    pk = B.g1_mul(B.G1_GEN, sk)
+    pk48 = B.g1_compress(pk)
+    try:
+        for msg, other in ((b"\x21" * 32, None), (b"\x22" * 32, b"\x23" * 32)):
+            sig_pt = B.g2_mul(B.hash_to_g2(other or msg), sk)
+            outs = []
+            for on in (0, 1):
+                hostsim.hs_eng_set_lines_thread(on)
+                out = buf(576)
+                assert hostsim.hs_eng_pairing(pk48, msg, B.g2_compress(sig_pt), out) == (1 if other is None else 0)
+                outs.append(out.raw)
+            assert outs[0] == outs[1]
+            fo = B.f12_mul(B.miller_loop(pk, B.hash_to_g2(msg)), B.miller_loop(B.g1_neg(B.G1_GEN), sig_pt))
+            exp = B.f12_conj(B.final_exponentiation(fo))
+            w = [exp[0][0], exp[1][0], exp[0][1], exp[1][1], exp[0][2], exp[1][2]]
+            assert [ib(outs[1][48 * k:48 * k + 48]) for k in range(12)] == [c % P for pair in w for c in pair]
+        hostsim.hs_eng_set_lines_thread(1)
+        g = load_golden("chain_chained_s1.json")
+        for r in g["rounds"][:2]:
+            assert hostsim.hs_eng_subgroup(bytes.fromhex(r["sig"])) == 1
+        rnd = random.Random(10)
+        for _ in range(2):
+            q = B.iso_map_g2(B.map_to_curve_sswu_g2((rnd.randrange(P), rnd.randrange(P))))
+            assert hostsim.hs_eng_subgroup(B.g2_compress(q)) == 0
+    finally:
+        hostsim.hs_eng_set_lines_thread(0)

@@ -44,6 +44,9 @@ def main():
     for i, name in enumerate(["k_h2c_field", "k_h2c_sswu", "k_h2c_finish", "k_decode_g2_sigs"]):
         mul, sqr = kout[2 * i], kout[2 * i + 1]
         kernels[name] = {"fp_mul": mul, "fp_sqr": sqr, "mads": MADS_MUL * mul + MADS_SQR * sqr}
+    lo = (ctypes.c_ulonglong * 2)()
+    assert L.hs_count_lines_thr(bytes.fromhex(r["sig"]), lo) == 0
+    kernels["k_lines_thr"] = {"fp_mul": lo[0], "fp_sqr": lo[1], "mads": MADS_MUL * lo[0] + MADS_SQR * lo[1]}
     h = [kernels[k] for k in ("k_h2c_field", "k_h2c_sswu", "k_h2c_finish")]
     # bench.py's stage "hash_to_g2" = the three hash kernels' launches summed
     kernels["hash_to_g2"] = {k: sum(x[k] for x in h) for k in ("fp_mul", "fp_sqr", "mads")}

@@ -25,19 +25,27 @@ namespace dgpu {
 //   X' = 2XY (t0 - t3), Y' = (t0 + t3)^2 - 12 t2^2, Z' = 4 t0 (2YZ)
 //   (4x the classical (XY/2 (t0 - t3), ((t0 + t3)/2)^2 - 3 t2^2, t0 2YZ)),
 //   line: c0 = t0 - t2, c2 = 3 X^2 (-xP), c3 = 2YZ yP.
-// 2XY and 2YZ as (X + Y)^2 - X^2 - Y^2 and (Y + Z)^2 - Y^2 - Z^2.
+// 2XY and 2YZ as (X + Y)^2 - X^2 - Y^2 and (Y + Z)^2 - Y^2 - Z^2, left
+// unreduced (lt_sub32_nr: they only feed products).
 // Bounds (units of p; CI = normalized, < 2.01p; fp_mul outputs < 1.01p here):
 //   X + Y, Y + Z carried (< 4.02p) into fp2_sqr; t2 = 12 (xi Z^2) from the
 //   carried lazy xi Z^2 (< 10.01p, limbs < 2^28 so 12x < 2^32) reduced to CI;
 //   t3 = 3 t2 carried (< 6.03p); t0 + t3 carried (< 7.04p: fp2_sqr's
 //   second coefficient < 7.99p); t0 + 8p - t3 carried (< 9.04p) into fp2_mul;
 //   12 t2^2 carried (< 12.1p, fp2_sub32's bound 31.9p); 4 t0 carried (< 4.04p).
+// a - b + 32p normalized, not reduced (< 33.2p: top limb < 2^23): only ever a
+// multiplication operand (fp2_mul / fp2_mul_fp: sums < 2^29 per limb, value
+// products < 70p x 4.1p).
+DG_FN fp2 lt_sub32_nr(const fp2& a, const fp2& b) {
+  return fp2{fp_norm(fp_sub2_lz(a.c0, b.c0)), fp_norm(fp_sub2_lz(a.c1, b.c1))};
+}
+
 DG_FN line3 lt_dbl(g2p& T, const fp& nxp, const fp& yp) {
   const fp2 t0 = fp2_sqr(T.y);
   const fp2 t1 = fp2_sqr(T.z);
   const fp2 x2 = fp2_sqr(T.x);
-  const fp2 yz2 = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(T.y, T.z))), fp2_add_lz(t0, t1));
-  const fp2 xy2 = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(T.x, T.y))), fp2_add_lz(x2, t0));
+  const fp2 yz2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.y, T.z))), fp2_add_lz(t0, t1));
+  const fp2 xy2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.x, T.y))), fp2_add_lz(x2, t0));
   const fp2 xt1 = fp2_carry(fp2{fp_sub_lz(t1.c0, t1.c1), fp_add_lz(t1.c0, t1.c1)});
   const fp2 t2 = fp2{fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c0)), fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c1))};
   const fp2 t3 = fp2_carry(fp2_add_lz(fp2_add_lz(t2, t2), t2));

@@ -175,6 +175,9 @@ KB_STAGE_WORK = {"eng_fe": "k_eng_fe_seg", "eng_fe_chain": "k_eng_kb_chain", "en
 if os.environ.get("DGPU_LINES") != "engine":
     for _p in ("g2", "recover"):
         STAGE_WORK[_p]["eng_lines"] = "k_lines_thr"
+# likewise the compressed chains (k_kb_chain_thr; DGPU_KB_CHAIN=lanes: k_eng_kb_chain)
+if os.environ.get("DGPU_KB_CHAIN") != "lanes":
+    KB_STAGE_WORK["eng_fe_chain"] = "k_kb_chain_thr"
 
 
 # stage -> kernel symbol for the traffic lookup

@@ -20,6 +20,7 @@
 #include "kernels.cuh"
 #include "pairing_engine.cuh"
 #include "lines_thread.cuh"
+#include "kb_thread.cuh"
 #include "recover.cuh"
 #include "g1sig.cuh"
 #include "rlc_msm.cuh"
@@ -178,6 +179,7 @@ struct dgpu_ctx {
   size_t kb_test_flag = 0;       // DGPU_KB_TEST_FLAG=k (tests): flag every k-th item so the fallback runs
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
+  bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
@@ -628,7 +630,10 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
   for (int seg = 0; seg < nseg; ++seg) {
     if (seg > 0) {
       mark(c, s, "eng_fe_chain");
-      hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
+      if (c->kb_thread)
+        hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
+      else
+        hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_fe_kbinv");
       hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
@@ -1012,6 +1017,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
   const char* ec = getenv("DGPU_ENG_CHUNK");
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
+  const char* kcv = getenv("DGPU_KB_CHAIN");
+  if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
   const char* lnv = getenv("DGPU_LINES");
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* gl = getenv("DGPU_G1_LINES");

@@ -1,0 +1,121 @@
+// Per-thread Karabina chain: one thread per round squares the compressed
+// element (f1, f2, f4, f5) of the exponentiation input m 63 times and stores
+// m^(2^s) at the six set bits s of |x| -- the same contract as the 8-lane
+// k_eng_kb_chain (pairing_engine.cuh), whose planes and layout it reads and
+// writes.  The compressed state is 8 Fp, so it stays in one thread's
+// registers and every product runs on the thread's own lanes.
+//
+// Compressed squaring (Granger-Scott, tower.cuh fp12_cyclo_sqr, restricted to
+// the closed outputs; Karabina 2010): with B = (f1, f4), C = (f2, f5) in
+// Fp4 = Fp2[s]/(s^2 - xi),
+//   B^2 = (f1^2 + xi f4^2, 2 f1 f4),  C^2 = (f2^2 + xi f5^2, 2 f2 f5)
+//   f1' = 3 xi (2 f2 f5) + 2 f1,  f4' = 3 (f2^2 + xi f5^2) - 2 f4,
+//   f2' = 3 (f1^2 + xi f4^2) - 2 f2,  f5' = 3 (2 f1 f4) + 2 f5.
+// Six Fp2 squarings (2 f1 f4 = (f1 + f4)^2 - f1^2 - f4^2): 12 Fp products.
+// Reference: the final exponentiation of kilic/bls12-381 (R), via
+// chain/verify.go:44 -> kyber bls.Verify; tools/gen_engine.py KbChainModel.
+#pragma once
+#include "tower.cuh"
+
+namespace dgpu {
+
+// Lazy steps (units of p; inputs CI: normalized, < 2.01p; fp2_sqr outputs
+// < 1.01p):
+//   f1 + f4, f2 + f5 carried (< 4.02p) into fp2_sqr;
+//   x^2 + xi y^2 = (X.re + Y.re + 8p - Y.im, X.im + Y.re + Y.im) carried
+//   (< 11.1p, limbs < 2^28), tripled (< 33.3p, limbs < 2^29.6), minus 2 f
+//   through fp_sub2_lz (+32p) -> < 65.3p, normalized and reduced to CI;
+//   2ab = (a + b)^2 - (a^2 + b^2) through fp_sub2_lz carried (< 33.1p),
+//   tripled plus 2 f (< 103.4p) -> CI; the xi-twisted one reduced to CI first
+//   (xi needs its subtrahend < 7.99p), xi applied lazily and carried
+//   (< 10.01p), tripled plus 2 f1 (< 34.1p) -> CI.
+DG_FN fp kb_t_out(const fp& x3, const fp& f, bool minus) {
+  fp t = fp_add_lz(fp_add_lz(x3, x3), x3);
+  return fp_reduce(fp_norm(minus ? fp_sub2_lz(t, fp_add_lz(f, f)) : fp_add_lz(t, fp_add_lz(f, f))));
+}
+DG_FN fp2 kb_t_qsum(const fp2& xx, const fp2& yy) {  // xx + xi yy, carried
+  return fp2{fp_norm(fp_add_lz(xx.c0, fp_sub_lz(yy.c0, yy.c1))), fp_norm(fp_add_lz(xx.c1, fp_add_lz(yy.c0, yy.c1)))};
+}
+DG_FN fp2 kb_t_cross(const fp2& ss, const fp2& xx, const fp2& yy) {  // ss - xx - yy, carried
+  return fp2{fp_norm(fp_sub2_lz(ss.c0, fp_add_lz(xx.c0, yy.c0))), fp_norm(fp_sub2_lz(ss.c1, fp_add_lz(xx.c1, yy.c1)))};
+}
+
+DG_FN void kb_sqr_thr(fp2& f1, fp2& f2, fp2& f4, fp2& f5) {
+  // C side: f1' and f4' (they need the old f1, f4, which the B side squares)
+  fp2 n1, n4;
+  {
+    const fp2 c2 = fp2_sqr(f2), c5 = fp2_sqr(f5);
+    const fp2 c25 = fp2_sqr(fp2_carry(fp2_add_lz(f2, f5)));
+    const fp2 q = kb_t_qsum(c2, c5);
+    n4 = fp2{kb_t_out(q.c0, f4.c0, true), kb_t_out(q.c1, f4.c1, true)};
+    const fp2 x = kb_t_cross(c25, c2, c5);
+    const fp2 xr{fp_reduce(x.c0), fp_reduce(x.c1)};
+    const fp2 xx{fp_norm(fp_sub_lz(xr.c0, xr.c1)), fp_norm(fp_add_lz(xr.c0, xr.c1))};  // xi (2 f2 f5)
+    n1 = fp2{kb_t_out(xx.c0, f1.c0, false), kb_t_out(xx.c1, f1.c1, false)};
+  }
+  // B side: f2' and f5'
+  const fp2 a1 = fp2_sqr(f1), a4 = fp2_sqr(f4);
+  const fp2 a14 = fp2_sqr(fp2_carry(fp2_add_lz(f1, f4)));
+  const fp2 q = kb_t_qsum(a1, a4);
+  f2 = fp2{kb_t_out(q.c0, f2.c0, true), kb_t_out(q.c1, f2.c1, true)};
+  const fp2 x = kb_t_cross(a14, a1, a4);
+  f5 = fp2{kb_t_out(x.c0, f5.c0, false), kb_t_out(x.c1, f5.c1, false)};
+  f1 = n1;
+  f4 = n4;
+}
+
+// 63 compressed squarings of (f1, f2, f4, f5); snap(j, f1, f2, f4, f5) after
+// s = 16, 48, 57, 60, 62, 63 of them (sum of 2^s = |x|).
+template <class Snap>
+DG_FN void kb_chain_thr(fp2 f1, fp2 f2, fp2 f4, fp2 f5, Snap&& snap) {
+  int s = 0;
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    const int sj = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+#pragma unroll 1
+    for (; s < sj; ++s) kb_sqr_thr(f1, f2, f4, f5);
+    snap(j, f1, f2, f4, f5);
+  }
+}
+
+}  // namespace dgpu
+
+#ifndef DG_NO_KERNELS
+#include "pairing_engine.cuh"
+namespace dgpu {
+
+#ifndef DG_KB_THR_OCC
+#define DG_KB_THR_OCC 2
+#endif
+// Thread = round i of the chunk: m from plane M, the six stored values to
+// planes X0.. (components 2..5, 8..11: f1, f2, f4, f5), dwordx2 per Fp2 limb.
+__global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt, uint32_t* __restrict__ xbuf) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt) return;
+  auto ld = [&](int plane, int comp) {
+    const uint32_t* b = xbuf + kb_off(i, plane, comp);
+    fp2 v;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      const uint2 w = *reinterpret_cast<const uint2*>(b + l * ENG_WAVE_WORDS);
+      v.c0.l[l] = w.x, v.c1.l[l] = w.y;
+    }
+    return v;
+  };
+  auto st = [&](int plane, int comp, const fp2& v) {
+    uint32_t* b = xbuf + kb_off(i, plane, comp);
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) *reinterpret_cast<uint2*>(b + l * ENG_WAVE_WORDS) = make_uint2(v.c0.l[l], v.c1.l[l]);
+  };
+  kb_chain_thr(ld(ENG_KB_PL_M, 2), ld(ENG_KB_PL_M, 4), ld(ENG_KB_PL_M, 8), ld(ENG_KB_PL_M, 10),
+               [&](int j, const fp2& f1, const fp2& f2, const fp2& f4, const fp2& f5) {
+                 const int pl = ENG_KB_PL_X0 + j;
+                 st(pl, 2, f1);
+                 st(pl, 4, f2);
+                 st(pl, 8, f4);
+                 st(pl, 10, f5);
+               });
+}
+
+}  // namespace dgpu
+#endif

@@ -9,6 +9,7 @@
 #define DG_NO_KERNELS
 #include "../../drand_amd/csrc/g1sig.cuh"
 #include "../../drand_amd/csrc/lines_thread.cuh"
+#include "../../drand_amd/csrc/kb_thread.cuh"
 
 using namespace dgpu;
 
@@ -62,6 +63,19 @@ int hs_count_lines_thr(const uint8_t* sig96, unsigned long long* out) {
   const bool in = lt_in_g2(T, s);
   out[0] = dg_count_mul; out[1] = dg_count_sqr;
   return in ? 0 : -2;
+#else
+  return -100;
+#endif
+}
+
+// Fp mul/sqr counts of k_kb_chain_thr per exponentiation (DG_COUNT_OPS builds).
+int hs_count_kb_chain_thr(unsigned long long* out) {
+#ifdef DG_COUNT_OPS
+  const fp2 a{fp_one(), fp_one()};
+  dg_count_mul = dg_count_sqr = 0;
+  kb_chain_thr(a, a, a, a, [](int, const fp2&, const fp2&, const fp2&, const fp2&) {});
+  out[0] = dg_count_mul; out[1] = dg_count_sqr;
+  return 0;
 #else
   return -100;
 #endif
@@ -437,6 +451,7 @@ struct HostGroup {
 };
 
 bool g_cyc_fast = false;
+bool g_kb_thread = false;  // the per-thread compressed chain (kb_thread.cuh) instead of the 8-lane rows
 bool g_fe_kb = false;     // the Karabina FE (k_eng_fe_seg / k_eng_kb_*) instead of prog_fe
 bool g_compiled = false;   // compiled ops (engine_compiled.h) instead of the interpreter
 
@@ -569,18 +584,28 @@ bool host_fe_kb(HostGroup& G, const fp f[12], const fp& n1inv) {
   G.set(ENG_E_N1I, n1inv);
   seg(0);
   for (int e = 1; e <= 5; ++e) {
-    uint32_t ks[ENG_KB_SLOTS * ENG_SLOT_WORDS];
-    memset(ks, 0, sizeof ks);
-    fp own[8];
-    for (int k = 0; k < 8; ++k) {
-      own[k] = G.fbuf[12 * ENG_KB_PL_M + ENG_KB_COMP[k]];
-      eng_st(ks + k * ENG_SLOT_WORDS, own[k]);
-    }
-    host_kb_square(ks, true, own);
-    int s = 1;
-    for (int j = 0; j < ENG_KB_NSNAP; ++j) {
-      for (; s < ENG_KB_SNAP[j]; ++s) host_kb_square(ks, false, own);
-      for (int k = 0; k < 8; ++k) G.fbuf[12 * (ENG_KB_PL_X0 + j) + ENG_KB_COMP[k]] = own[k];
+    if (g_kb_thread) {  // kb_thread.cuh (k_kb_chain_thr)
+      const fp* m = G.fbuf + 12 * ENG_KB_PL_M;
+      kb_chain_thr(fp2{m[2], m[3]}, fp2{m[4], m[5]}, fp2{m[8], m[9]}, fp2{m[10], m[11]},
+                   [&](int j, const fp2& f1, const fp2& f2, const fp2& f4, const fp2& f5) {
+                     fp* x = G.fbuf + 12 * (ENG_KB_PL_X0 + j);
+                     x[2] = f1.c0, x[3] = f1.c1, x[4] = f2.c0, x[5] = f2.c1;
+                     x[8] = f4.c0, x[9] = f4.c1, x[10] = f5.c0, x[11] = f5.c1;
+                   });
+    } else {
+      uint32_t ks[ENG_KB_SLOTS * ENG_SLOT_WORDS];
+      memset(ks, 0, sizeof ks);
+      fp own[8];
+      for (int k = 0; k < 8; ++k) {
+        own[k] = G.fbuf[12 * ENG_KB_PL_M + ENG_KB_COMP[k]];
+        eng_st(ks + k * ENG_SLOT_WORDS, own[k]);
+      }
+      host_kb_square(ks, true, own);
+      int s = 1;
+      for (int j = 0; j < ENG_KB_NSNAP; ++j) {
+        for (; s < ENG_KB_SNAP[j]; ++s) host_kb_square(ks, false, own);
+        for (int k = 0; k < 8; ++k) G.fbuf[12 * (ENG_KB_PL_X0 + j) + ENG_KB_COMP[k]] = own[k];
+      }
     }
     for (int j = 0; j < ENG_KB_NSNAP; ++j) {
       fp* x = G.fbuf + 12 * (ENG_KB_PL_X0 + j);
@@ -608,6 +633,7 @@ extern "C" void hs_eng_set_cyc_fast(int on) { g_cyc_fast = on != 0; }
 extern "C" void hs_eng_set_fe_kb(int on) { g_fe_kb = on != 0; }
 bool g_lines_thread = false;  // T-steps from lines_thread.cuh lt_pair (k_lines_thr) instead of the LINES program
 extern "C" void hs_eng_set_lines_thread(int on) { g_lines_thread = on != 0; }
+extern "C" void hs_eng_set_kb_thread(int on) { g_kb_thread = on != 0; }
 extern "C" void hs_eng_set_compiled(int on) { g_compiled = on != 0; }
 
 // every compiled op vs the interpreter on the same random slots: 0 iff all

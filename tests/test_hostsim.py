@@ -328,3 +328,30 @@ def test_thread_lines_match_oracle_and_engine(hostsim):
             assert hostsim.hs_eng_subgroup(B.g2_compress(q)) == 0
     finally:
         hostsim.hs_eng_set_lines_thread(0)
+
+
+def test_thread_kb_chain_matches_lane_chain(hostsim):
+    """The per-thread compressed chain (kb_thread.cuh kb_chain_thr,
+    k_kb_chain_thr) in the Karabina FE gives the same GT value words as the
+    8-lane chain rows, and the oracle's, on valid and invalid checks."""
+    sk = D.derive_secret(16)
+    pk = B.g1_mul(B.G1_GEN, sk)
+    pk48 = B.g1_compress(pk)
+    hostsim.hs_eng_set_fe_kb(1)
+    try:
+        for msg, other in ((b"\x31" * 32, None), (b"\x32" * 32, b"\x33" * 32)):
+            sig_pt = B.g2_mul(B.hash_to_g2(other or msg), sk)
+            outs = []
+            for on in (0, 1):
+                hostsim.hs_eng_set_kb_thread(on)
+                out = buf(576)
+                assert hostsim.hs_eng_pairing(pk48, msg, B.g2_compress(sig_pt), out) == (1 if other is None else 0)
+                outs.append(out.raw)
+            assert outs[0] == outs[1]
+            fo = B.f12_mul(B.miller_loop(pk, B.hash_to_g2(msg)), B.miller_loop(B.g1_neg(B.G1_GEN), sig_pt))
+            exp = B.f12_conj(B.final_exponentiation(fo))
+            w = [exp[0][0], exp[1][0], exp[0][1], exp[1][1], exp[0][2], exp[1][2]]
+            assert [ib(outs[1][48 * k:48 * k + 48]) for k in range(12)] == [c % P for pair in w for c in pair]
+    finally:
+        hostsim.hs_eng_set_kb_thread(0)
+        hostsim.hs_eng_set_fe_kb(0)

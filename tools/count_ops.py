@@ -47,6 +47,10 @@ def main():
     lo = (ctypes.c_ulonglong * 2)()
     assert L.hs_count_lines_thr(bytes.fromhex(r["sig"]), lo) == 0
     kernels["k_lines_thr"] = {"fp_mul": lo[0], "fp_sqr": lo[1], "mads": MADS_MUL * lo[0] + MADS_SQR * lo[1]}
+    # the FE's five per-thread compressed chains (bench stage eng_fe_chain)
+    assert L.hs_count_kb_chain_thr(lo) == 0
+    kernels["k_kb_chain_thr"] = {"fp_mul": 5 * lo[0], "fp_sqr": 5 * lo[1],
+                                 "mads": 5 * (MADS_MUL * lo[0] + MADS_SQR * lo[1])}
     h = [kernels[k] for k in ("k_h2c_field", "k_h2c_sswu", "k_h2c_finish")]
     # bench.py's stage "hash_to_g2" = the three hash kernels' launches summed
     kernels["hash_to_g2"] = {k: sum(x[k] for x in h) for k in ("fp_mul", "fp_sqr", "mads")}

@@ -212,7 +212,9 @@ def roofline_for(stage_ms, items, pipeline="g2", stage_items=None, extra_work=No
     if not stage_ms or not items:
         return None
     wmap = dict(STAGE_WORK[pipeline])
-    if "eng_fe_chain" in stage_ms:  # Karabina FE (default; DGPU_FE=gs runs k_eng_fe alone under "eng_fe")
+    # Karabina FE (default; DGPU_FE=gs runs k_eng_fe alone under "eng_fe"), on
+    # the pipelines whose engine stages run once per item (not RLC's node checks)
+    if "eng_fe_chain" in stage_ms and "eng_fe" in wmap:
         wmap.update(KB_STAGE_WORK)
     work = dict(hash_work(), **engine_work())
     work.update(extra_work or {})

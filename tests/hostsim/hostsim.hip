@@ -639,7 +639,7 @@ extern "C" void hs_eng_set_compiled(int on) { g_compiled = on != 0; }
 // every compiled op vs the interpreter on the same random slots: 0 iff all
 // outputs (slots and exports) are identical words
 extern "C" int hs_eng_compiled_compare(uint64_t seed) {
-  static const int ops[] = {OP_LDBL, OP_LADD, OP_M_XIF, OP_M_SQR, OP_M_XIL, OP_E_MUL, OP_E_MULCJ, OP_E_XIA};
+  static const int ops[] = {OP_LDBL, OP_LADD, OP_M_XIF, OP_M_SQR, OP_M_LM1, OP_M_LM2, OP_E_MUL, OP_E_MULCJ, OP_E_XIA};
   int n = 0;
   for (int op : ops) {
     HostGroup A;
@@ -665,7 +665,7 @@ extern "C" int hs_eng_compiled_compare(uint64_t seed) {
       if (memcmp(&A.lines[i], &B.lines[i], sizeof(fp)) != 0) return 200 + op;
     ++n;
   }
-  return n == 8 ? 0 : -1;
+  return n == (int)(sizeof ops / sizeof ops[0]) ? 0 : -1;
 }
 
 // canonical residue of a normalized value < 2^392

@@ -89,7 +89,7 @@ def test_sqr_and_line_mul(ops):
     for j, v in enumerate((l0, l2, l3)):
         m.s[G.M_L1 + 2 * j], m.s[G.M_L1 + 2 * j + 1] = v
         m.s[G.M_L2 + 2 * j], m.s[G.M_L2 + 2 * j + 1] = v
-    m.run("M_XIL")
+    m.run("M_XIF")   # xi-copies of f; M_LM1's epilogue leaves those of f l for M_LM2
     m.run("M_LM1")
     line = _to_tower([l0, (0, 0), l2, l3, (0, 0), (0, 0)])
     exp = B.f12_mul(_to_tower(f), line)

@@ -170,17 +170,25 @@ def op_sqr12(name, F, XF, conj=False, XF0=None):
     return pack(name, recs)
 
 
-def op_line_mul(name, F, L, XL):
-    """F <- F * (l0 + l2 w^2 + l3 w^3); L = (l0, l2, l3) at L..L+5, XL = (xi l2, xi l3)."""
+def op_line_mul(name, F, L, XL=None, XF=None):
+    """F <- F * (l0 + l2 w^2 + l3 w^3); L = (l0, l2, l3) at L..L+5.  The
+    terms that wrap past w^6 carry a factor xi: with XL = (xi l2, xi l3) they
+    read the line's xi-copies, with XF = {k: xi f_k} (k = 3, 4, 5) the
+    coefficient's (round 3: from the previous op's fused epilogue, no per-line
+    xi pass)."""
     f = fp12(F)
     l0, l2, l3 = fp2(L), fp2(L + 2), fp2(L + 4)
-    xl2, xl3 = fp2(XL), fp2(XL + 2)
+    xl = {2: fp2(XL), 3: fp2(XL + 2)} if XL is not None else None
     recs = []
     for k in range(6):
         re, im = [], []
-        for src, coeff, xcoeff, sh in ((k, l0, l0, 0), ((k - 2) % 6, l2, xl2, 2), ((k - 3) % 6, l3, xl3, 3)):
-            y = xcoeff if k < sh else coeff
-            r, m = mul_terms(f[src], y)
+        for src, coeff, sh in ((k, l0, 0), ((k - 2) % 6, l2, 2), ((k - 3) % 6, l3, 3)):
+            if k >= sh:
+                r, m = mul_terms(f[src], coeff)
+            elif xl is not None:
+                r, m = mul_terms(f[src], xl[sh])
+            else:
+                r, m = mul_terms(fp2(XF[src]), coeff)
             re += r
             im += m
         recs.append(Rec(dst=f[k][0], terms=re))
@@ -615,20 +623,23 @@ def build_ops():
     # k_miller
     ops.append(pack("M_XIF", op_xi_copy("_a", M_F, M_X, [1, 2, 3, 4, 5]).subs[0] +
                     op_xi_copy("_b", M_F, M_XF0, [0]).subs[0]))
-    ops.append(op_sqr12("M_SQR", M_F, M_X, XF0=M_XF0))
-    # xi l2, xi l3 for both lines: L1 (l0, l2, l3) at 22, L2 at 28 -> X 12..15 and 16..19
-    ops.append(pack("M_XIL", op_xi_copy("_a", M_L1, M_X, [1, 2]).subs[0] + op_xi_copy("_b", M_L2, M_X + 4, [1, 2]).subs[0]))
-    ops.append(op_line_mul("M_LM1", M_F, M_L1, M_X))
-    lm2 = op_line_mul("M_LM2", M_F, M_L2, M_X + 4)
-    # its fused epilogue leaves xi f = (re - im, re + im) of every coefficient
-    # for the next step's M_SQR (the loop's M_XIF pass, round 2, is gone):
-    # the re lane's re + im is the copy's im half, the im lane's re - im its re half
-    lanes = [None] * LANES
-    for k in range(6):
-        xr = M_XF0 if k == 0 else M_X + 2 * (k - 1)
-        lanes[2 * k] = (xr + 1, FUSE_SUM)
-        lanes[2 * k + 1] = (xr, FUSE_DIFF)
-    ops.append(Op("M_LM2", lm2.subs, fuse={0: lanes}))
+    # Fused epilogues leave xi f = (re - im, re + im) of coefficients for the
+    # next op (the re lane's re + im is the copy's im half, the im lane's
+    # re - im its re half): M_LM2 -> all six, for the next step's M_SQR (the
+    # loop's M_XIF pass of round 2 is gone); M_SQR and M_LM1 -> f3, f4, f5,
+    # the factors of the line products' wrapped terms (xi f_k) l_j, so no
+    # per-line xi-copy pass (M_XIL, to r03aa) either.
+    def xi_lanes(ks):
+        lanes = [None] * LANES
+        for k in ks:
+            xr = M_XF0 if k == 0 else M_X + 2 * (k - 1)
+            lanes[2 * k] = (xr + 1, FUSE_SUM)
+            lanes[2 * k + 1] = (xr, FUSE_DIFF)
+        return lanes
+    xf_wrap = {k: M_X + 2 * (k - 1) for k in (3, 4, 5)}
+    ops.append(Op("M_SQR", op_sqr12("M_SQR", M_F, M_X, XF0=M_XF0).subs, fuse={0: xi_lanes((3, 4, 5))}))
+    ops.append(Op("M_LM1", op_line_mul("M_LM1", M_F, M_L1, XF=xf_wrap).subs, fuse={0: xi_lanes((3, 4, 5))}))
+    ops.append(Op("M_LM2", op_line_mul("M_LM2", M_F, M_L2, XF=xf_wrap).subs, fuse={0: xi_lanes(range(6))}))
     ops.append(op_norm6("M_NRM", M_F, M_X, M_N))
     ops.append(op_xi_copy("M_XIN2", M_N, M_XN2, [2]))
     ops.append(op_fp6_inv_t("M_T012", M_N, M_XN2, M_T))
@@ -684,8 +695,9 @@ def prog_lines():
 
 
 def prog_miller():
-    prog = []
-    line = [("ldline", M_L1), ("run", "M_XIL"), ("run", "M_LM1"), ("run", "M_LM2")]
+    # M_XIF once: xi-copies of f = 1 for the first step's line products
+    prog = [("run", "M_XIF")]
+    line = [("ldline", M_L1), ("run", "M_LM1"), ("run", "M_LM2")]
     for j, b in enumerate(BITS):
         if j:   # M_SQR's xi-copies of f: the previous M_LM2's fused epilogue
             prog += [("run", "M_SQR")]
@@ -1132,7 +1144,7 @@ def kb_decompress(v, p):
 # eng_exec includes the op (0 lines, 1 miller, 2 fe).
 # (M_LM1 / M_LM2 compile without spills since eng_sub_c fences each term's
 # products; without the fence k_eng_miller spilled 179 VGPRs)
-COMPILED = {"LDBL": 0, "LADD": 0, "M_XIF": 1, "M_SQR": 1, "M_XIL": 1, "M_LM1": 1, "M_LM2": 1,
+COMPILED = {"LDBL": 0, "LADD": 0, "M_XIF": 1, "M_SQR": 1, "M_LM1": 1, "M_LM2": 1,
             "E_MUL": 2, "E_MULCJ": 2, "E_XIA": 2}
 
 
@@ -1236,9 +1248,9 @@ def fused_reads(op):
         for p in range(2):
             for off, mode in ((10, FUSE_SUM), (11, FUSE_DIFF), (22, FUSE_SUM), (23, FUSE_DIFF)):
                 wide[4][_pb(p, off)] = FUSE_BOUND[mode]
-    if op.name == "M_SQR":   # the xi-copies (re - im, re + im) of f from M_LM2's epilogue
+    if op.name in ("M_SQR", "M_LM1", "M_LM2"):   # xi-copies (re - im, re + im) of f from fused epilogues
         wide[0] = {}
-        for k in range(6):
+        for k in (range(6) if op.name == "M_SQR" else (3, 4, 5)):
             xr = M_XF0 if k == 0 else M_X + 2 * (k - 1)
             wide[0][xr] = FUSE_BOUND[FUSE_DIFF]
             wide[0][xr + 1] = FUSE_BOUND[FUSE_SUM]

@@ -85,7 +85,11 @@ const char *dgpu_last_error(void);
  * Read once here: DGPU_LANES=1 keeps large per-round G2 batches on one stream
  * (default: two streams over the batch halves; verdicts are identical), and
  * DGPU_G1_LINES=buffer runs the on-G1 fixed-Q lines through a line buffer
- * (default: formed inside the Miller kernel; verdicts are identical). */
+ * (default: formed inside the Miller kernel; verdicts are identical);
+ * DGPU_LINES=engine and DGPU_KB_CHAIN=lanes run the Miller loops' T-steps and
+ * the final exponentiation's compressed chains on the 12- / 8-lane engine
+ * instead of one thread per item (default; verdicts are identical);
+ * DGPU_FE=gs runs the Granger-Scott final exponentiation (A/B). */
 int dgpu_open(int device, dgpu_ctx **out);
 void dgpu_close(dgpu_ctx *ctx);
 

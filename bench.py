@@ -15,7 +15,8 @@ The default run also measures every other BASELINE.json configuration at its
 stated size, each with its own verdict check, roofline and CPU baseline:
   rlc            configs[2]: RLC batch verify of the same resident chain
   configs3       configs[3]: 10M-round pedersen-bls-unchained and
-                 bls-unchained-on-g1 chains, per-round verify
+                 bls-unchained-on-g1 chains, per-round verify and the
+                 per-GPU RLC fold (G2 / G1 bucket-MSM roots) of each
   recover        configs[4]: threshold recovery, n=32, t=17, 100k rounds
   multi_abi      the product multi-GPU boundary (dgpu_verify_multi: one
                  process drives all N GPUs, host records, RCCL gathers), run
@@ -143,7 +144,11 @@ STAGE_WORK = {
            "decode_g1": "k_decode_g1_sigs", "h_affine": "k_g1_batch_affine"},
     # RLC: the per-round stages only (node checks are data-dependent: 1 at 0% corruption)
     "rlc": {"rlc_hash_to_g2_raw": "rlc_hash_to_g2_raw", "decode_g2": "k_decode_g2_sigs+subgroup",
-            "rlc_leaves_tree": "rlc_leaves_tree"},
+            "rlc_affine": "k_g2_batch_affine", "rlc_root_msm": "rlc_root_msm", "rlc_leaves_tree": "rlc_leaves_tree"},
+    # RLC for the G1-signature schemes (configs[3]'s per-GPU fold)
+    "rlc_g1": {"rlc_hash_to_g1_raw": "rlc_hash_to_g1_raw", "decode_g1": "k_decode_g1_sigs",
+               "rlc_affine": "k_g1_batch_affine", "rlc_root_msm": "rlc_root_msm_g1",
+               "rlc_leaves_tree": "rlc_leaves_tree_g1"},
     # recovery (batched check): per round, one pairing check and the MSMs
     "recover": {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv",
                 "eng_fe": "k_eng_fe", "recover_msm": "recover_msm", "recover_rlc_g1": "recover_rlc_g1"},
@@ -251,12 +256,12 @@ def stage_times(lib, ctx, step, passes=1):
     _lib.check(lib.dgpu_set_profiling(ctx.handle, 1))
     for _ in range(passes):
         step()
-    ms = (ctypes.c_float * 32)()
-    names = (ctypes.c_char_p * 32)()
-    ns = lib.dgpu_stage_times(ctx.handle, ms, 32, names)
-    _lib.check(lib.dgpu_set_profiling(ctx.handle, 0))
+    try:
+        out = _lib.stage_times(ctx)
+    finally:
+        _lib.check(lib.dgpu_set_profiling(ctx.handle, 0))
     torch.cuda.synchronize()
-    return {names[i].decode(): float(ms[i]) for i in range(max(ns, 0))}
+    return out
 
 
 def timed(step, steps, world, dev, after=None):
@@ -527,7 +532,8 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
            "verdict_mismatches": int((verdicts != expect).sum()), "corrupted_rounds_total": len(bad),
            "chain_gen_s": t_gen, "scheme": scheme, "rounds_total": n_total, "rounds_per_gpu": n}
     g1 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
-    pipeline = "rlc" if mode == "rlc" else ("g1" if g1 else "g2")
+    rlc_pipe = "rlc_g1" if g1 else "rlc"
+    pipeline = rlc_pipe if mode == "rlc" else ("g1" if g1 else "g2")
     if rank == 0:
         res["roofline"] = roofline_for(stage_ms, n, pipeline)
 
@@ -551,7 +557,7 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
     # configs[2] beside the metric: RLC batch verification (one multi-Miller
     # loop + one final exponentiation per checked node, root first, exact
     # per-round verdicts by bisection) over the same resident chain
-    if rlc and mode == "per-round" and not g1:
+    if rlc and mode == "per-round":
         step_rlc = lambda: step_mode(_lib.MODE_RLC, seed + 1)  # noqa: E731
         step_rlc()
         rlc_ms = stage_times(lib, ctx, step_rlc)
@@ -560,9 +566,13 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
                              after=lambda: gather_verdict_bits(d_bits, n, n_total, world, rank))
         res["rlc"] = {"value": n_total * rlc_steps / t_rlc, "unit": "rounds/s", "ms_per_step": t_rlc / rlc_steps * 1e3,
                       "steps": rlc_steps, "verdict_mismatches": int((v_rlc != expect).sum()), "stage_ms": rlc_ms,
-                      "roofline": roofline_for(rlc_ms, n, "rlc") if rank == 0 else None,
-                      "workload": "configs[2] on the same chain: RLC batch verify, root first, per-round verdicts by "
-                                  "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)"}
+                      "roofline": roofline_for(rlc_ms, n, rlc_pipe) if rank == 0 else None,
+                      "workload": ("configs[3] per-GPU fold on the same chain: RLC batch verify of G1 signatures "
+                                   "(G1 bucket-MSM root, one 2-pair check on the key's fixed-Q lines), root first, "
+                                   "per-round verdicts by bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)"
+                                   if g1 else
+                                   "configs[2] on the same chain: RLC batch verify, root first, per-round verdicts by "
+                                   "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)")}
         log(f"rlc: {res['rlc']['value']:.0f} rounds/s")
 
     if main and rank == 0 and world == 1 and not args.no_ingest:
@@ -579,6 +589,11 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
         except Exception as e:  # reported, never fatal
             res["cpu_baseline"] = {"error": repr(e)}
         log("cpu baseline done")
+        if "rlc" in res and "value" in res["cpu_baseline"]:
+            # the reference has no batch mode: its CPU path verifies every round with
+            # its own pairing whatever the GPU's mode, so the leg's baseline stands
+            res["rlc"]["cpu_baseline"] = dict(res["cpu_baseline"], note="same CPU run as this leg's cpu_baseline "
+                                              "(the reference verifies each round with its own pairing check)")
     del d_rounds, d_sigs, d_sig_len, d_prev, d_prev_len, d_bits, chain
     gc.collect()
     torch.cuda.empty_cache()
@@ -689,7 +704,7 @@ def main_verify(args, world, rank, local):
         legs["configs3"] = {}
         for sch in ("pedersen-bls-unchained", "bls-unchained-on-g1"):
             legs["configs3"][sch] = verify_leg(args, world, rank, local, sch, n_total, args.leg_steps, 1,
-                                               cpu_seconds=args.cpu_seconds / 2)
+                                               rlc=not args.no_rlc, cpu_seconds=args.cpu_seconds / 2)
         # configs[4]: threshold recovery at its stated shape
         legs["recover"] = recover_leg(args, world, rank, local, 100_000, max(args.leg_steps, 3), 1,
                                       args.cpu_seconds / 2)

@@ -117,6 +117,23 @@ def check(rc):
     return rc
 
 
+MAX_STAGES = 32  # DGPU_MAX_STAGES
+
+
+def stage_times(ctx):
+    """dgpu_stage_times of the context's last profiled call: {stage: ms}.
+    Raises on an overflowed event pool; every pipeline's stage count is
+    within DGPU_MAX_STAGES (asserted: the return is the count needed)."""
+    ms = (ctypes.c_float * MAX_STAGES)()
+    names = (ctypes.c_char_p * MAX_STAGES)()
+    ns = ctx.lib.dgpu_stage_times(ctx.handle, ms, MAX_STAGES, names)
+    if ns < 0:
+        check(ns)
+    if ns > MAX_STAGES:
+        raise DrandGPUError(DGPU_EINVAL, f"{ns} stages > DGPU_MAX_STAGES")
+    return {names[i].decode(): float(ms[i]) for i in range(ns)}
+
+
 def shard_range(n, ndev, k):
     """dgpu_shard_range: item range [lo, hi) of device k (host-only bookkeeping)."""
     lib = load()

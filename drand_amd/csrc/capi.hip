@@ -204,6 +204,7 @@ struct dgpu_ctx {
   std::vector<hipEvent_t> ev;
   std::vector<const char*> stage_name;
   int n_ev = 0;
+  bool ev_overflow = false;  // the last call recorded more than STAGE_EVENTS_MAX stage events
 };
 
 namespace {
@@ -221,8 +222,13 @@ struct stream_order {
 
 // Stage markers: mark(c, s, name) records an event that *starts* stage `name`
 // (and ends the previous one); mark(c, s, nullptr) closes the last stage.
+constexpr int STAGE_EVENTS_MAX = 4096;
 void mark(dgpu_ctx* c, hipStream_t s, const char* name = nullptr) {
-  if (!c->profile || c->n_ev >= 1024) return;
+  if (!c->profile) return;
+  if (c->n_ev >= STAGE_EVENTS_MAX) {  // reported by dgpu_stage_times, never dropped silently
+    c->ev_overflow = true;
+    return;
+  }
   if ((size_t)c->n_ev == c->ev.size()) {
     hipEvent_t e = nullptr;
     if (hipEventCreate(&e) != hipSuccess) return;
@@ -384,34 +390,58 @@ struct rlc_trees {
   int top() const { return (int)sz.size() - 1; }
 };
 
+// Word sizes of one signature group's points in the RLC buffers.
+struct rlc_geom {
+  bool g1;
+  int aw, jw;  // affine / Jacobian words per point
+};
+inline rlc_geom rlc_geom_of(bool g1) { return g1 ? rlc_geom{true, G1A_WORDS, G1J_WORDS} : rlc_geom{false, G2A_WORDS, G2J_WORDS}; }
+
 // RLC phase 1: R_i = pre-cofactor H(m_i) (affine, in rlc_tree's tail),
-// sig_i decoded (+ subgroup, required before any combination: soundness).
+// sig_i decoded (+ subgroup, required before any combination: soundness --
+// both groups' cofactors have small prime factors, so a small-order component
+// would survive a random 64-bit combination with noticeable probability).
 // Asynchronous on s.
-uint32_t* rlc_rpts(dgpu_ctx* c, size_t n) {
-  // R_i after the two trees' levels: the layout rlc_tree_locked keeps
+size_t rlc_tree_points(size_t n) {
   size_t total = 0;
   for (size_t v = n;; v = (v + 1) / 2) {
     total += v;
     if (v <= 1) break;
   }
-  return (uint32_t*)c->rlc_tree.p + 2 * total * G2J_WORDS;
+  return total;
+}
+
+uint32_t* rlc_rpts(dgpu_ctx* c, size_t n, int jw) {
+  // R_i after the two trees' levels: the layout rlc_tree_t keeps
+  return (uint32_t*)c->rlc_tree.p + 2 * rlc_tree_points(n) * jw;
 }
 
 int rlc_points_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s) {
   const unsigned B = 256;
   const size_t n = a.n;
-  size_t total = 0;
-  for (size_t v = n;; v = (v + 1) / 2) {
-    total += v;
-    if (v <= 1) break;
-  }
+  const rlc_geom G = rlc_geom_of(sig_on_g1(a.scheme));
   int rc;
-  if ((rc = c->rlc_tree.ensure(2 * total * G2J_WORDS * 4 + n * G2J_WORDS * 4))) return rc;
-  if ((rc = c->sig_pts.ensure(n * G2A_WORDS * 4))) return rc;
-  if ((rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
-  uint32_t* rpts = rlc_rpts(c, n);
+  if ((rc = c->rlc_tree.ensure(2 * rlc_tree_points(n) * G.jw * 4 + n * G.jw * 4))) return rc;
+  if ((rc = c->sig_pts.ensure(n * G.aw * 4)) || (rc = c->h_pre.ensure(n * FP_WORDS * 4))) return rc;
+  uint32_t* rpts = rlc_rpts(c, n, G.jw);
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
   uint8_t* st = (uint8_t*)c->status.p;
+  if (G.g1) {
+    mark(c, s, "rlc_hash_to_g1_raw");
+    hipLaunchKernelGGL(k_hash_to_g1_raw, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.m,
+                       a.scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, rpts, rpts + 2 * FP_WORDS * n);
+    HIP_TRY(hipGetLastError());
+    mark(c, s, "decode_g1");
+    hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len,
+                       a.m, sg, st);
+    HIP_TRY(hipGetLastError());
+    mark(c, s, "rlc_affine");
+    hipLaunchKernelGGL(k_g1_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, rpts,
+                       (const uint32_t*)(rpts + 2 * FP_WORDS * n), (uint32_t*)c->h_pre.p);
+    HIP_TRY(hipGetLastError());
+    return DGPU_OK;
+  }
+  if ((rc = c->h_tmp.ensure(n * (4 + 12) * FP_WORDS * 4))) return rc;
   mark(c, s, "rlc_hash_to_g2_raw");
   {
     // the per-round hash's field and SSWU stages, then Q0 + Q1 without the cofactor
@@ -437,16 +467,18 @@ int rlc_points_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s) {
 }
 
 // RLC root by bucket MSM (rlc_msm.cuh) into root (P then S, stride-1
-// Jacobian).  Asynchronous on s.
-int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root) {
+// Jacobian of the signature group).  Asynchronous on s.
+template <class Gr>
+int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root) {
+  using M = GrMem<Gr>;
   const unsigned B = 256;
   const size_t n = a.n;
   if (n > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "RLC batch too large (%zu)", n);
   int rc;
-  if ((rc = c->msm_aos.ensure(2 * n * MSM_AOS_WORDS * 4)) || (rc = c->msm_flags.ensure(n)) ||
+  if ((rc = c->msm_aos.ensure(2 * n * M::AFF * 4)) || (rc = c->msm_flags.ensure(n)) ||
       (rc = c->msm_counts.ensure(3 * MSM_KEYS * 4)) || (rc = c->msm_list.ensure(MSM_MW * n * 4 + 4)) ||
-      (rc = c->msm_buckets.ensure(MSM_KEYS * G2J_WORDS * 4)) ||
-      (rc = c->msm_runs.ensure(2 * (size_t)MSM_MW * MSM_RUNS * G2J_WORDS * 4)))
+      (rc = c->msm_buckets.ensure(MSM_KEYS * M::JAC * 4)) ||
+      (rc = c->msm_runs.ensure(2 * (size_t)MSM_MW * MSM_RUNS * M::JAC * 4)))
     return rc;
   uint32_t* aos = (uint32_t*)c->msm_aos.p;
   uint8_t* flags = (uint8_t*)c->msm_flags.p;
@@ -455,7 +487,7 @@ int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32
   uint32_t* cursor = offsets + MSM_KEYS;
   uint32_t* list = (uint32_t*)c->msm_list.p;
   mark(c, s, "rlc_root_msm");
-  hipLaunchKernelGGL(k_msm_aos, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)rlc_rpts(c, n),
+  hipLaunchKernelGGL(k_msm_aos<Gr>, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)rlc_rpts(c, n, M::JAC),
                      (const uint32_t*)c->sig_pts.p, (const uint8_t*)c->status.p, aos, flags);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemsetAsync(counts, 0, MSM_KEYS * 4, s));
@@ -467,32 +499,38 @@ int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32
                      list);
   HIP_TRY(hipGetLastError());
   uint32_t* buckets = (uint32_t*)c->msm_buckets.p;
-  hipLaunchKernelGGL(k_msm_bucket, dim3(grid_for(MSM_KEYS, B)), dim3(B), 0, s, n, (const uint32_t*)offsets,
+  hipLaunchKernelGGL(k_msm_bucket<Gr>, dim3(grid_for(MSM_KEYS, B)), dim3(B), 0, s, n, (const uint32_t*)offsets,
                      (const uint32_t*)counts, (const uint32_t*)list, (const uint32_t*)aos, buckets);
   HIP_TRY(hipGetLastError());
   uint32_t* runs = (uint32_t*)c->msm_runs.p;
-  uint32_t* runs2 = runs + (size_t)MSM_MW * MSM_RUNS * G2J_WORDS;
-  hipLaunchKernelGGL(k_msm_window, dim3(grid_for((size_t)MSM_MW * MSM_RUNS, B)), dim3(B), 0, s,
+  uint32_t* runs2 = runs + (size_t)MSM_MW * MSM_RUNS * M::JAC;
+  hipLaunchKernelGGL(k_msm_window<Gr>, dim3(grid_for((size_t)MSM_MW * MSM_RUNS, B)), dim3(B), 0, s,
                      (const uint32_t*)buckets, runs);
   HIP_TRY(hipGetLastError());
   size_t len = MSM_RUNS;
   while (len > 1) {  // pairwise tree per (MSM, window), ping-pong between the two run buffers
     const size_t nl = (len + 1) / 2;
-    hipLaunchKernelGGL(k_g2_sum_level, dim3(grid_for((size_t)MSM_MW * nl, B)), dim3(B), 0, s, MSM_MW, len,
+    hipLaunchKernelGGL(k_sum_level<Gr>, dim3(grid_for((size_t)MSM_MW * nl, B)), dim3(B), 0, s, MSM_MW, len,
                        (const uint32_t*)runs, nl, runs2);
     HIP_TRY(hipGetLastError());
     std::swap(runs, runs2);
     len = nl;
   }
-  hipLaunchKernelGGL(k_msm_root, dim3(1), dim3(64), 0, s, (const uint32_t*)runs, root, root + G2J_WORDS);
+  hipLaunchKernelGGL(k_msm_root<Gr>, dim3(1), dim3(64), 0, s, (const uint32_t*)runs, root, root + M::JAC);
   HIP_TRY(hipGetLastError());
   return DGPU_OK;
+}
+
+int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root) {
+  return sig_on_g1(a.scheme) ? rlc_root_msm_t<G1Ops>(c, a, s, root) : rlc_root_msm_t<G2Ops>(c, a, s, root);
 }
 
 // The segment trees of one RLC batch (leaves P_i = r_i R_i, S_i = r_i sig_i,
 // r_i from the seed and the batch position i; then sums up to the root),
 // built from rlc_points_locked's points.  Asynchronous on s.
-int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+template <class Gr>
+int rlc_tree_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+  using M = GrMem<Gr>;
   const unsigned B = 256;
   const size_t n = a.n;
   T.sz.assign(1, n);
@@ -503,34 +541,40 @@ int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees&
   size_t off = 0;
   for (size_t l = 0; l < T.sz.size(); ++l) {
     T.P[l] = tree + off;
-    off += T.sz[l] * G2J_WORDS;
+    off += T.sz[l] * M::JAC;
     T.S[l] = tree + off;
-    off += T.sz[l] * G2J_WORDS;
+    off += T.sz[l] * M::JAC;
   }
   mark(c, s, "rlc_leaves_tree");
-  hipLaunchKernelGGL(k_rlc_leaves, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed, (const uint32_t*)rlc_rpts(c, n),
-                     (const uint32_t*)c->sig_pts.p, (const uint8_t*)c->status.p, T.P[0], T.S[0]);
+  hipLaunchKernelGGL(k_rlc_leaves<Gr>, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed,
+                     (const uint32_t*)rlc_rpts(c, n, M::JAC), (const uint32_t*)c->sig_pts.p,
+                     (const uint8_t*)c->status.p, T.P[0], T.S[0]);
   HIP_TRY(hipGetLastError());
   for (size_t l = 0; l + 1 < T.sz.size(); ++l) {
-    hipLaunchKernelGGL(k_rlc_level, dim3(grid_for(2 * T.sz[l + 1], B)), dim3(B), 0, s, T.sz[l], T.P[l], T.S[l],
+    hipLaunchKernelGGL(k_rlc_level<Gr>, dim3(grid_for(2 * T.sz[l + 1], B)), dim3(B), 0, s, T.sz[l], T.P[l], T.S[l],
                        T.sz[l + 1], T.P[l + 1], T.S[l + 1]);
     HIP_TRY(hipGetLastError());
   }
   return DGPU_OK;
 }
 
+int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+  return sig_on_g1(a.scheme) ? rlc_tree_t<G1Ops>(c, a, s, T) : rlc_tree_t<G2Ops>(c, a, s, T);
+}
+
 // Check candidate nodes cand of a level (P_lvl, S_lvl, n_level nodes) on the
-// pairing engine: e(pk, h_eff P) e(-g1, S) == 1.  Fail flags stay on the
-// device (d_fail, one byte per candidate); `fail` (optional) receives them on
-// the host (synchronizes the stream).
+// pairing engine: e(pk, h_eff P) e(-g1, S) == 1 (G2 signatures) or
+// e(h_eff P, pk) e(-S, g2) == 1 (G1 signatures: the key's fixed-Q line
+// table).  Fail flags stay on the device (d_fail, one byte per candidate);
+// `fail` (optional) receives them on the host (synchronizes the stream).
 int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32_t>& cand, size_t n_level,
                      const uint32_t* P_lvl, const uint32_t* S_lvl, hipStream_t s, std::vector<uint8_t>* fail) {
   const unsigned B = 256;
   const size_t m = cand.size();
+  const rlc_geom G = rlc_geom_of(key->g2key);
   int rc;
   if ((rc = c->rlc_idx.ensure(m * 4)) || (rc = c->rlc_fail.ensure(m))) return rc;
-  if ((rc = c->rlc_h.ensure(m * G2A_WORDS * 4)) || (rc = c->rlc_s.ensure(m * G2A_WORDS * 4)) ||
-      (rc = c->rlc_st.ensure(m)))
+  if ((rc = c->rlc_h.ensure(m * G.aw * 4)) || (rc = c->rlc_s.ensure(m * G.aw * 4)) || (rc = c->rlc_st.ensure(m)))
     return rc;
   uint32_t* d_idx = (uint32_t*)c->rlc_idx.p;
   uint8_t* d_fail = (uint8_t*)c->rlc_fail.p;
@@ -539,9 +583,16 @@ int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32
   uint32_t* cs = (uint32_t*)c->rlc_s.p;
   uint8_t* cst = (uint8_t*)c->rlc_st.p;
   mark(c, s, "rlc_prep");
-  hipLaunchKernelGGL(k_rlc_prep, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, n_level, P_lvl, S_lvl, ch, cs, cst);
+  if (G.g1)
+    hipLaunchKernelGGL(k_rlc_prep<G1Ops>, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, n_level, P_lvl, S_lvl, ch,
+                       cs, cst);
+  else
+    hipLaunchKernelGGL(k_rlc_prep<G2Ops>, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, n_level, P_lvl, S_lvl, ch,
+                       cs, cst);
   HIP_TRY(hipGetLastError());
-  if ((rc = eng_pairing_locked(c, (const uint32_t*)key->consts.p, m, ch, cs, cst, s))) return rc;
+  if ((rc = eng_pairing_locked(c, (const uint32_t*)key->consts.p, m, ch, cs, cst, s, 0, nullptr, nullptr,
+                               G.g1 ? (const uint32_t*)key->table.p : nullptr)))
+    return rc;
   mark(c, s, "rlc_bisection");
   hipLaunchKernelGGL(k_rlc_fail, dim3(grid_for(m, B)), dim3(B), 0, s, m, cst, d_fail);
   HIP_TRY(hipGetLastError());
@@ -825,8 +876,6 @@ int check_args(const dgpu_ctx* c, const key_entry* key, const verify_args& a) {
     if (a.m.chained && (!a.m.prev_len || (!a.m.prev && a.m.prev_stride)))
       return set_err(DGPU_EINVAL, "chained scheme needs previous signatures");
   }
-  if (sig_on_g1(a.scheme) && a.mode != DGPU_MODE_PER_ROUND)
-    return set_err(DGPU_EUNSUPPORTED, "RLC mode is built for G2 signatures only");
   (void)c;
   return DGPU_OK;
 }
@@ -839,15 +888,16 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   if ((rc = c->status.ensure(n))) return rc;
   uint8_t* st = (uint8_t*)c->status.p;
   c->n_ev = 0;
-  if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
+  c->ev_overflow = false;
   if (a.mode == DGPU_MODE_RLC) {
     // root first, by bucket MSM; the tree of leaves only when it fails
+    const int jw = rlc_geom_of(sig_on_g1(a.scheme)).jw;
     if ((rc = rlc_points_locked(c, a, s))) return rc;
-    if ((rc = c->rlc_root.ensure(2 * G2J_WORDS * 4))) return rc;
+    if ((rc = c->rlc_root.ensure(2 * jw * 4))) return rc;
     uint32_t* root = (uint32_t*)c->rlc_root.p;
     if ((rc = rlc_root_msm_locked(c, a, s, root))) return rc;
     std::vector<uint8_t> fail;
-    if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, root, root + G2J_WORDS, s, &fail))) return rc;
+    if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, root, root + jw, s, &fail))) return rc;
     if (!fail[0] || a.n == 1) {
       if (fail[0]) {  // one round: its leaf is the root
         hipLaunchKernelGGL(k_rlc_mark, dim3(1), dim3(64), 0, s, (size_t)1, (const uint32_t*)c->rlc_idx.p,
@@ -860,6 +910,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
     if ((rc = rlc_tree_locked(c, a, s, T))) return rc;
     return rlc_descend_locked(c, key, T, s, true);
   }
+  if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
   const uint32_t* consts = (const uint32_t*)key->consts.p;
   const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z,     &c->h_pre, &c->h_tmp,
                      &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb};
@@ -1181,12 +1232,15 @@ int dgpu_set_profiling(dgpu_ctx* c, int enable) {
   std::lock_guard<std::mutex> lk(c->mu);
   c->profile = enable != 0;
   c->n_ev = 0;
+  c->ev_overflow = false;
   return DGPU_OK;
 }
 
 int dgpu_stage_times(dgpu_ctx* c, float* ms_out, int max_stages, const char** names_out) {
   if (!c || !ms_out) return set_err(DGPU_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
+  if (c->ev_overflow)
+    return set_err(DGPU_EINVAL, "stage timing: the last call recorded more than %d stage events", STAGE_EVENTS_MAX);
   HIP_TRY(hipSetDevice(c->device));
   std::vector<const char*> names;
   std::vector<float> sums;
@@ -1203,12 +1257,12 @@ int dgpu_stage_times(dgpu_ctx* c, float* ms_out, int max_stages, const char** na
     }
     sums[k] += ms;
   }
-  int n = (int)std::min<size_t>(names.size(), (size_t)std::max(max_stages, 0));
+  const int n = (int)std::min<size_t>(names.size(), (size_t)std::max(max_stages, 0));
   for (int i = 0; i < n; ++i) {
     ms_out[i] = sums[i];
     if (names_out) names_out[i] = names[i];
   }
-  return n;
+  return (int)names.size();  // the count needed (like snprintf): > max_stages means truncated
 }
 
 int dgpu_digest_batch(dgpu_ctx* c, int scheme, size_t n, const uint64_t* rounds, const uint8_t* prev,
@@ -1566,6 +1620,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
                                  uint8_t* d_ok, uint8_t* d_status, hipStream_t s) {
   if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
   c->n_ev = 0;
+  c->ev_overflow = false;
   if (c->recover_exact)
     return recover_exact_locked(c, n_rounds, d_msgs, m, d_parts, stride, d_plen, d_out, d_ok, d_status, s);
   const size_t items = n_rounds * m;

@@ -164,6 +164,25 @@ __global__ void __launch_bounds__(256, 2) k_hash_to_g1_beacons(size_t n, msg_src
   st_fp(z_out, n, i, h.z);
 }
 
+// RLC mode (rlc_msm.cuh): the pre-cofactor hash point R = Q0 + Q1 on E1
+// (Jacobian X, Y into r_out, Z into z_out): h_eff = 1 + |x| is applied once per
+// checked node, by linearity, instead of a 64-step ladder per round.
+__global__ void __launch_bounds__(256, 2) k_hash_to_g1_raw(size_t n, msg_src m, int g1dst,
+                                                         uint32_t* __restrict__ r_out, uint32_t* __restrict__ z_out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t uni[32];
+  if (g1dst)
+    msg_expand<true, 4>(m, i, uni);
+  else
+    msg_expand<false, 4>(m, i, uni);
+  const g1j r = g1_add_body(map_to_curve_sswu_iso11_body(fp_from_be64_words(uni)),
+                            map_to_curve_sswu_iso11_body(fp_from_be64_words(uni + 16)));
+  st_fp(r_out, n, i, r.x);
+  st_fp(r_out + FP_WORDS * n, n, i, r.y);
+  st_fp(z_out, n, i, r.z);
+}
+
 // H(m) in G1 of raw messages of any length, compressed (parity surface:
 // dgpu_hash_to_g1 / dgpu_hash_to_curve)
 __global__ void __launch_bounds__(256) k_hash_to_g1_msgs(size_t n, msg_src m, int g1dst, uint8_t* __restrict__ out48) {

@@ -323,76 +323,9 @@ __device__ __forceinline__ uint64_t rlc_coeff(uint64_t seed, uint64_t idx) {
   return z ? z : 1ull;
 }
 
-// Leaves of the RLC tree: P_i = [a_i] R_i + [b_i] psi(R_i), S_i = [a_i] sig_i +
-// [b_i] psi(sig_i) with (a_i, b_i) the two halves of rlc_coeff (infinity for
-// rounds whose decode verdict is already final).  psi commutes with h_eff and
-// acts as [x] on G2, so h_eff P_i = [r_i] H_i and S_i = [r_i] sig_i with
-// r_i = a_i + b_i x: 2^64 distinct nonzero coefficients mod r (|a_i| < |x|), the
-// same soundness as a uniform 64-bit r_i, at half the doublings.  R_i is affine
-// here (k_g2_batch_affine ran on the pre-cofactor hash points; (0, 0) marks
-// the identity).  2n threads: j < n computes P_j, j >= n computes S_{j-n}.
-// The scalar multiplication is the window form (g2_mul2_win4_affine): every
-// lane runs the same sequence; the NAF ladder (DG_RLC_NAF) ran the union of
-// its lanes' digit-driven additions.
-__global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, uint64_t seed, const uint32_t* __restrict__ r_aff,
-                                                            const uint32_t* __restrict__ sig_pts,
-                                                            const uint8_t* __restrict__ status,
-                                                            uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2 * n) return;
-  const bool sig = j >= n;
-  const size_t i = sig ? j - n : j;
-  g2j acc = g2_infinity();
-  if (status[i] == ST_OK) {
-    const g2a q = ld_g2a(sig ? sig_pts : r_aff, n, i);
-    if (!(fp2_is_zero(q.x) && fp2_is_zero(q.y))) {
-      const uint64_t z = rlc_coeff(seed, i);
-#if defined(DG_RLC_NAF)
-      acc = g2_mul2_naf32_affine<true>(q, q, (uint32_t)z, (uint32_t)(z >> 32));
-#else
-      acc = g2_mul2_win4_affine(q, (uint32_t)z, (uint32_t)(z >> 32));
-#endif
-    }
-  }
-  st_g2j(sig ? s_out : p_out, n, i, acc);
-}
-
-// One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied); 2 n_out
-// threads, the first n_out on the P tree, the rest on the S tree.
-__global__ void __launch_bounds__(256) k_rlc_level(size_t n_in, const uint32_t* __restrict__ p_in,
-                                                    const uint32_t* __restrict__ s_in, size_t n_out,
-                                                    uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * n_out) return;
-  const bool sig = t >= n_out;
-  const size_t j = sig ? t - n_out : t;
-  const uint32_t* in = sig ? s_in : p_in;
-  const size_t a = 2 * j, b = 2 * j + 1;
-  g2j P = ld_g2j(in, n_in, a);
-  if (b < n_in) P = g2_add_body(P, ld_g2j(in, n_in, b));
-  st_g2j(sig ? s_out : p_out, n_out, j, P);
-}
-
-// Candidate nodes for the pairing engine: h[c] = affine h_eff * P, sg[c] =
-// affine S, st[c] = ST_OK when both are finite (the engine then decides),
-// RLC_TRIVIAL when both are infinity (passes), ST_PAIRING when exactly one is
-// (e(Q, .) of a non-trivial prime-order point alone is never 1).
+// Node status of a trivially passing candidate (both points at infinity;
+// rlc_msm.cuh k_rlc_prep).
 constexpr uint8_t RLC_TRIVIAL = 0x80;
-__global__ void __launch_bounds__(64) k_rlc_prep(size_t n_cand, const uint32_t* __restrict__ idx, size_t n_level,
-                                                 const uint32_t* __restrict__ p_lvl,
-                                                 const uint32_t* __restrict__ s_lvl, uint32_t* __restrict__ h_out,
-                                                 uint32_t* __restrict__ s_out, uint8_t* __restrict__ st) {
-  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n_cand) return;
-  size_t j = idx[c];
-  g2j P = g2_clear_cofactor(ld_g2j(p_lvl, n_level, j));
-  g2j S = ld_g2j(s_lvl, n_level, j);
-  bool pi = g2_is_inf(P), si = g2_is_inf(S);
-  const g2a zero{fp2_zero(), fp2_zero()};
-  st_g2a(h_out, n_cand, c, pi ? zero : g2_to_affine(P));
-  st_g2a(s_out, n_cand, c, si ? zero : g2_to_affine(S));
-  st[c] = (pi && si) ? RLC_TRIVIAL : (pi || si) ? (uint8_t)ST_PAIRING : (uint8_t)ST_OK;
-}
 
 // Engine verdicts of the candidates -> fail flags.
 __global__ void __launch_bounds__(256) k_rlc_fail(size_t n_cand, const uint8_t* __restrict__ st,
@@ -400,18 +333,6 @@ __global__ void __launch_bounds__(256) k_rlc_fail(size_t n_cand, const uint8_t* 
   size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n_cand) return;
   fail[c] = (st[c] == ST_OK || st[c] == RLC_TRIVIAL) ? 0 : 1;
-}
-
-// Multi-GPU RLC: the per-device roots (P, S), gathered over RCCL as
-// [dev][P (G2J_WORDS), S (G2J_WORDS)] (each a stride-1 Jacobian SoA), summed
-// into one node (stride 1) that is checked once for the whole node.
-__global__ void k_rlc_sum_roots(int ndev, const uint32_t* __restrict__ roots, uint32_t* __restrict__ p_out,
-                                uint32_t* __restrict__ s_out) {
-  if (blockIdx.x != 0 || threadIdx.x >= 2) return;
-  const int w = threadIdx.x;  // 0: P, 1: S
-  g2j acc = ld_g2j(roots + w * G2J_WORDS, 1, 0);
-  for (int d = 1; d < ndev; ++d) acc = g2_add(acc, ld_g2j(roots + (size_t)d * 2 * G2J_WORDS + w * G2J_WORDS, 1, 0));
-  st_g2j(w ? s_out : p_out, 1, 0, acc);
 }
 
 // Mark the rounds of failing leaves.

@@ -10,8 +10,9 @@
 //  - per-round mode: one all-gather of the per-device verdict bitmaps (and
 //    reason bytes) -- shards are multiples of 8 rounds, so the gathered
 //    bitmaps concatenate into the batch's bitmap;
-//  - RLC mode: one all-gather of the per-device RLC roots (two Jacobian G2
-//    sums, 672 bytes, each computed by bucket MSM, rlc_msm.cuh), summed on
+//  - RLC mode: one all-gather of the per-device RLC roots (two Jacobian sums
+//    of the signature group: 672 bytes for G2 signatures, 336 for the G1
+//    schemes; each computed by bucket MSM, rlc_msm.cuh), summed on
 //    device 0 and checked there with a single pairing (one final
 //    exponentiation for the whole node); only when that fails does each
 //    device build its tree of leaves and descend it (root first) to
@@ -268,7 +269,9 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
       return rc;
     HIP_TRY(hipStreamWaitEvent(c->stream, c->done, 0));
   }
-  const bool rlc = mode == DGPU_MODE_RLC && !sig_on_g1(scheme);
+  const bool rlc = mode == DGPU_MODE_RLC;
+  const bool g1 = sig_on_g1(scheme);
+  const int jw = g1 ? G1J_WORDS : G2J_WORDS;  // root: P, S (stride-1 Jacobian of the signature group)
   std::vector<rlc_trees> trees(D);
   // phase 1: stage the shard, then per-round verification (or the RLC trees)
   rc = for_each_device(m, [&](int k) -> int {
@@ -280,8 +283,9 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
     if ((r = stage_inputs_locked(c, a, s))) return r;
     if ((r = c->status.ensure(a.n))) return r;
     c->n_ev = 0;
+    c->ev_overflow = false;
     if (rlc) {  // the shard's points and its root by bucket MSM (the leaves wait for a failing root)
-      if ((r = rlc_points_locked(c, a, s)) || (r = c->msm_root.ensure(2 * G2J_WORDS * 4))) return r;
+      if ((r = rlc_points_locked(c, a, s)) || (r = c->msm_root.ensure(2 * (size_t)jw * 4))) return r;
       return rlc_root_msm_locked(c, a, s, (uint32_t*)c->msm_root.p);
     }
     if ((r = verify_status_locked(c, keys[k], a, s))) return r;
@@ -292,19 +296,22 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
     bool all_ok = false;
     {
       // the per-device roots to every device; one check of their sum on device 0
-      g2j inf = g2_infinity();
+      // the identity (Z = 0) of the signature group, for empty shards
+      const g2j inf2 = g2_infinity();
+      const g1j inf1 = g1_infinity();
       uint32_t inf_words[G2J_WORDS];
-      const fp* co[6] = {&inf.x.c0, &inf.x.c1, &inf.y.c0, &inf.y.c1, &inf.z.c0, &inf.z.c1};
-      for (int j = 0; j < 6; ++j) memcpy(inf_words + j * FP_LIMBS, co[j]->l, FP_LIMBS * 4);
+      const fp* co2[6] = {&inf2.x.c0, &inf2.x.c1, &inf2.y.c0, &inf2.y.c1, &inf2.z.c0, &inf2.z.c1};
+      const fp* co1[3] = {&inf1.x, &inf1.y, &inf1.z};
+      for (int j = 0; j < jw / FP_LIMBS; ++j) memcpy(inf_words + j * FP_LIMBS, (g1 ? co1[j] : co2[j])->l, FP_LIMBS * 4);
       for (int k = 0; k < D; ++k) {
         dgpu_ctx* c = m->ctx[k];
         HIP_TRY(hipSetDevice(c->device));
         uint32_t* root = (uint32_t*)m->buf[k].root.p;
         if (args[k].n == 0) {
-          HIP_TRY(hipMemcpyAsync(root, inf_words, sizeof inf_words, hipMemcpyHostToDevice, c->stream));
-          HIP_TRY(hipMemcpyAsync(root + G2J_WORDS, inf_words, sizeof inf_words, hipMemcpyHostToDevice, c->stream));
+          HIP_TRY(hipMemcpyAsync(root, inf_words, (size_t)jw * 4, hipMemcpyHostToDevice, c->stream));
+          HIP_TRY(hipMemcpyAsync(root + jw, inf_words, (size_t)jw * 4, hipMemcpyHostToDevice, c->stream));
         } else {
-          HIP_TRY(hipMemcpyAsync(root, c->msm_root.p, 2 * G2J_WORDS * 4, hipMemcpyDeviceToDevice, c->stream));
+          HIP_TRY(hipMemcpyAsync(root, c->msm_root.p, 2 * (size_t)jw * 4, hipMemcpyDeviceToDevice, c->stream));
         }
       }
       std::vector<const void*> src(D);
@@ -313,16 +320,20 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
         src[k] = m->buf[k].root.p;
         dst[k] = m->buf[k].all_roots.p;
       }
-      if ((rc = multi_all_gather(m, src, dst, 2 * G2J_WORDS * 4))) return rc;
+      if ((rc = multi_all_gather(m, src, dst, 2 * (size_t)jw * 4))) return rc;
       dgpu_ctx* c0 = m->ctx[0];
       HIP_TRY(hipSetDevice(c0->device));
-      if ((rc = c0->rlc_root.ensure(2 * G2J_WORDS * 4))) return rc;
+      if ((rc = c0->rlc_root.ensure(2 * (size_t)jw * 4))) return rc;
       uint32_t* sum = (uint32_t*)c0->rlc_root.p;
-      hipLaunchKernelGGL(k_rlc_sum_roots, dim3(1), dim3(64), 0, c0->stream, D, (const uint32_t*)m->buf[0].all_roots.p,
-                         sum, sum + G2J_WORDS);
+      if (g1)
+        hipLaunchKernelGGL(k_rlc_sum_roots<G1Ops>, dim3(1), dim3(64), 0, c0->stream, D,
+                           (const uint32_t*)m->buf[0].all_roots.p, sum, sum + jw);
+      else
+        hipLaunchKernelGGL(k_rlc_sum_roots<G2Ops>, dim3(1), dim3(64), 0, c0->stream, D,
+                           (const uint32_t*)m->buf[0].all_roots.p, sum, sum + jw);
       HIP_TRY(hipGetLastError());
       std::vector<uint8_t> fail;
-      if ((rc = rlc_check_locked(c0, keys[0], std::vector<uint32_t>{0}, 1, sum, sum + G2J_WORDS, c0->stream, &fail)))
+      if ((rc = rlc_check_locked(c0, keys[0], std::vector<uint32_t>{0}, 1, sum, sum + jw, c0->stream, &fail)))
         return rc;
       all_ok = !fail[0];
     }

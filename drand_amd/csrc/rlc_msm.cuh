@@ -1,66 +1,79 @@
-// RLC root by bucket MSM (Pippenger), configs[2]: the whole batch's
-// random-linear-combination root
-//   P = sum_i r_i R_i,   S = sum_i r_i sig_i      (r_i = a_i + b_i x, kernels.cuh rlc_coeff)
-// without a per-point scalar multiplication.  With the psi split of the
-// leaves (P = sum a_i R_i + psi(sum b_i R_i), psi a group endomorphism of E')
-// the root is four MSMs with 32-bit scalars over the batch's affine points,
-// each in two 16-bit windows: every (MSM, window, digit) is a bucket, so a
-// point costs one mixed addition per MSM and window -- 8 per round instead
-// of the two window ladders of k_rlc_leaves (~32 doublings + 16 additions
-// each).  The tree of leaves is built only when this root fails
-// (capi.hip verify_status_locked).
+// RLC batch verification (configs[2], and configs[3]'s per-GPU fold for the
+// G1-signature schemes), written once over the signature group (group_ops.cuh:
+// G2Ops for pedersen-bls-*, G1Ops for bls-unchained-on-g1 / -g1-rfc9380).
+//
+// With d_i = e(pk, H_i) e(-g1, sig_i) (G2 signatures) or e(H_i, pk) e(-sig_i, g2)
+// (G1 signatures), the whole batch collapses to one pairing check by
+//   prod_i d_i^(r_i) = e(h_eff sum_i r_i R_i, .) e(sum_i r_i sig_i, .)
+// with R_i the pre-cofactor hash point (h_eff applied once per checked node,
+// by linearity) and r_i = a_i + b_i lambda (group_ops.cuh).  The root
+//   P = sum_i a_i R_i + endo(sum_i b_i R_i),  S = sum_i a_i sig_i + endo(sum_i b_i sig_i)
+// is four MSMs with 32-bit scalars over the batch's affine points, each in two
+// 16-bit windows: every (MSM, window, digit) is a bucket, so a point costs one
+// mixed addition per MSM and window -- 8 per round instead of the two window
+// ladders of k_rlc_leaves (~32 doublings + 16 additions each).  The tree of
+// leaves is built only when this root fails (capi.hip verify_status_locked).
 //
 // Pipeline (one launch each; the bucket order is a counting sort, so the
 // sums do not depend on the order the atomics hand out positions -- point
 // addition is associative and commutative, the results are exact):
-//   k_msm_aos     R_i, sig_i affine SoA -> AoS (224 B per point: gathers
-//                 read two cache lines instead of 56) + usable flags
+//   k_msm_aos     R_i, sig_i affine SoA -> AoS (G2: 224 B contiguous per point,
+//                 gathers read two cache lines instead of 56) + usable flags
 //   k_msm_count   bucket sizes (atomics)
 //   k_msm_scan    exclusive prefix sums (one block)
 //   k_msm_scatter point indices into their buckets (atomics on cursors)
 //   k_msm_bucket  one thread per bucket: sum of its points (mixed additions)
 //   k_msm_window  one thread per run of 64 buckets: sum_k k B_k of the run
-//   k_g2_sum_level  pairwise tree over the runs of each (MSM, window)
-//   k_msm_root    MSM_m = W_m0 + 2^16 W_m1; P = MSM_0 + psi(MSM_1), S = MSM_2 + psi(MSM_3)
+//   k_sum_level   pairwise tree over the runs of each (MSM, window)
+//   k_msm_root    MSM_m = W_m0 + 2^16 W_m1; P = MSM_0 + endo(MSM_1), S = MSM_2 + endo(MSM_3)
 #pragma once
 #include "kernels.cuh"
+#include "group_ops.cuh"
 
 namespace dgpu {
 
-constexpr int MSM_C = 16;                         // window bits
-constexpr int MSM_BUCKETS = 1 << MSM_C;           // per (MSM, window); digit 0 unused
-constexpr int MSM_MW = 8;                         // 4 MSMs x 2 windows
-constexpr size_t MSM_KEYS = (size_t)MSM_MW * MSM_BUCKETS;
-constexpr int MSM_RUN = 64;                       // buckets per k_msm_window thread
-constexpr int MSM_RUNS = MSM_BUCKETS / MSM_RUN;   // runs per (MSM, window)
-constexpr int MSM_AOS_WORDS = G2A_WORDS;          // 56 words per affine point
+constexpr int G1A_WORDS = 2 * FP_WORDS;  // affine G1 point
+constexpr int G1J_WORDS = 3 * FP_WORDS;  // Jacobian G1 point
 
-__device__ __forceinline__ g2a ld_aos(const uint32_t* __restrict__ base, size_t i) {
-  const uint32_t* p = base + i * MSM_AOS_WORDS;
-  g2a a;
-#pragma unroll
-  for (int l = 0; l < FP_LIMBS; ++l) {
-    a.x.c0.l[l] = p[l];
-    a.x.c1.l[l] = p[FP_LIMBS + l];
-    a.y.c0.l[l] = p[2 * FP_LIMBS + l];
-    a.y.c1.l[l] = p[3 * FP_LIMBS + l];
-  }
-  return a;
+__device__ __forceinline__ void st_g1j(uint32_t* base, size_t n, size_t i, const g1j& p) {
+  st_fp(base, n, i, p.x);
+  st_fp(base + FP_WORDS * n, n, i, p.y);
+  st_fp(base + 2 * FP_WORDS * n, n, i, p.z);
+}
+__device__ __forceinline__ g1j ld_g1j(const uint32_t* base, size_t n, size_t i) {
+  return g1j{ld_fp(base, n, i), ld_fp(base + FP_WORDS * n, n, i), ld_fp(base + 2 * FP_WORDS * n, n, i)};
+}
+__device__ __forceinline__ void st_g1a(uint32_t* base, size_t n, size_t i, const g1a& p) {
+  st_fp(base, n, i, p.x);
+  st_fp(base + FP_WORDS * n, n, i, p.y);
+}
+__device__ __forceinline__ g1a ld_g1a(const uint32_t* base, size_t n, size_t i) {
+  return g1a{ld_fp(base, n, i), ld_fp(base + FP_WORDS * n, n, i)};
 }
 
-// R (affine SoA in r_aff, (0, 0) = identity) and sig (affine SoA) -> AoS
-// [R | sig][i]; flags[i]: bit 0 R usable, bit 1 sig usable (status ST_OK and
-// not the identity; the leaves kernel skips the same points).
-__global__ void __launch_bounds__(256) k_msm_aos(size_t n, const uint32_t* __restrict__ r_aff,
-                                                 const uint32_t* __restrict__ sig_pts,
-                                                 const uint8_t* __restrict__ status, uint32_t* __restrict__ aos,
-                                                 uint8_t* __restrict__ flags) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint8_t f = 0;
-  for (int which = 0; which < 2; ++which) {
-    const g2a q = ld_g2a(which ? sig_pts : r_aff, n, i);
-    uint32_t* o = aos + ((size_t)which * n + i) * MSM_AOS_WORDS;
+// HBM layouts of one group's points: SoA [coordinate Fp][limb][index] (AFF /
+// JAC words per point), AoS rows of AFF words (the MSM's gather side).
+template <class Gr>
+struct GrMem;
+template <>
+struct GrMem<G2Ops> {
+  static constexpr int AFF = G2A_WORDS, JAC = G2J_WORDS;
+  static __device__ __forceinline__ g2a ld_aff(const uint32_t* b, size_t n, size_t i) { return ld_g2a(b, n, i); }
+  static __device__ __forceinline__ void st_aff(uint32_t* b, size_t n, size_t i, const g2a& p) { st_g2a(b, n, i, p); }
+  static __device__ __forceinline__ g2j ld_jac(const uint32_t* b, size_t n, size_t i) { return ld_g2j(b, n, i); }
+  static __device__ __forceinline__ void st_jac(uint32_t* b, size_t n, size_t i, const g2j& p) { st_g2j(b, n, i, p); }
+  static __device__ __forceinline__ g2a ld_row(const uint32_t* __restrict__ p) {
+    g2a a;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      a.x.c0.l[l] = p[l];
+      a.x.c1.l[l] = p[FP_LIMBS + l];
+      a.y.c0.l[l] = p[2 * FP_LIMBS + l];
+      a.y.c1.l[l] = p[3 * FP_LIMBS + l];
+    }
+    return a;
+  }
+  static __device__ __forceinline__ void st_row(uint32_t* __restrict__ o, const g2a& q) {
 #pragma unroll
     for (int l = 0; l < FP_LIMBS; ++l) {
       o[l] = q.x.c0.l[l];
@@ -68,7 +81,56 @@ __global__ void __launch_bounds__(256) k_msm_aos(size_t n, const uint32_t* __res
       o[2 * FP_LIMBS + l] = q.y.c0.l[l];
       o[3 * FP_LIMBS + l] = q.y.c1.l[l];
     }
-    if (status[i] == ST_OK && !(fp2_is_zero(q.x) && fp2_is_zero(q.y))) f |= (uint8_t)(1u << which);
+  }
+};
+template <>
+struct GrMem<G1Ops> {
+  static constexpr int AFF = G1A_WORDS, JAC = G1J_WORDS;
+  static __device__ __forceinline__ g1a ld_aff(const uint32_t* b, size_t n, size_t i) { return ld_g1a(b, n, i); }
+  static __device__ __forceinline__ void st_aff(uint32_t* b, size_t n, size_t i, const g1a& p) { st_g1a(b, n, i, p); }
+  static __device__ __forceinline__ g1j ld_jac(const uint32_t* b, size_t n, size_t i) { return ld_g1j(b, n, i); }
+  static __device__ __forceinline__ void st_jac(uint32_t* b, size_t n, size_t i, const g1j& p) { st_g1j(b, n, i, p); }
+  static __device__ __forceinline__ g1a ld_row(const uint32_t* __restrict__ p) {
+    g1a a;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      a.x.l[l] = p[l];
+      a.y.l[l] = p[FP_LIMBS + l];
+    }
+    return a;
+  }
+  static __device__ __forceinline__ void st_row(uint32_t* __restrict__ o, const g1a& q) {
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      o[l] = q.x.l[l];
+      o[FP_LIMBS + l] = q.y.l[l];
+    }
+  }
+};
+
+constexpr int MSM_C = 16;                         // window bits
+constexpr int MSM_BUCKETS = 1 << MSM_C;           // per (MSM, window); digit 0 unused
+constexpr int MSM_MW = 8;                         // 4 MSMs x 2 windows
+constexpr size_t MSM_KEYS = (size_t)MSM_MW * MSM_BUCKETS;
+constexpr int MSM_RUN = 64;                       // buckets per k_msm_window thread
+constexpr int MSM_RUNS = MSM_BUCKETS / MSM_RUN;   // runs per (MSM, window)
+
+// R (affine SoA in r_aff, (0, 0) = identity) and sig (affine SoA) -> AoS
+// [R | sig][i]; flags[i]: bit 0 R usable, bit 1 sig usable (status ST_OK and
+// not the identity; the leaves kernel skips the same points).
+template <class Gr>
+__global__ void __launch_bounds__(256) k_msm_aos(size_t n, const uint32_t* __restrict__ r_aff,
+                                                 const uint32_t* __restrict__ sig_pts,
+                                                 const uint8_t* __restrict__ status, uint32_t* __restrict__ aos,
+                                                 uint8_t* __restrict__ flags) {
+  using M = GrMem<Gr>;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t f = 0;
+  for (int which = 0; which < 2; ++which) {
+    const typename Gr::aff q = M::ld_aff(which ? sig_pts : r_aff, n, i);
+    M::st_row(aos + ((size_t)which * n + i) * M::AFF, q);
+    if (status[i] == ST_OK && !Gr::aff_is_zero(q)) f |= (uint8_t)(1u << which);
   }
   flags[i] = f;
 }
@@ -134,71 +196,170 @@ __global__ void __launch_bounds__(256) k_msm_scatter(size_t n, uint64_t seed, co
 }
 
 // B_b = sum of the bucket's points (Jacobian SoA, stride MSM_KEYS)
+template <class Gr>
 __global__ void __launch_bounds__(256, 2) k_msm_bucket(size_t n, const uint32_t* __restrict__ offsets,
                                                      const uint32_t* __restrict__ counts,
                                                      const uint32_t* __restrict__ list,
                                                      const uint32_t* __restrict__ aos, uint32_t* __restrict__ buckets) {
+  using M = GrMem<Gr>;
   const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= MSM_KEYS) return;
   const int m = (int)(b >> (MSM_C + 1));
-  const uint32_t* src = aos + (m >> 1 ? n * MSM_AOS_WORDS : 0);
+  const uint32_t* src = aos + (m >> 1 ? n * M::AFF : 0);
   const uint32_t o = offsets[b], cnt = counts[b];
-  g2j acc = g2_infinity();
+  typename Gr::jac acc = Gr::inf();
 #pragma unroll 1
-  for (uint32_t p = 0; p < cnt; ++p) acc = g2_add_affine_body(acc, ld_aos(src, list[o + p]));
-  st_g2j(buckets, MSM_KEYS, b, acc);
+  for (uint32_t p = 0; p < cnt; ++p) acc = Gr::add_aff_body(acc, M::ld_row(src + (size_t)list[o + p] * M::AFF));
+  M::st_jac(buckets, MSM_KEYS, b, acc);
 }
 
 // Per run of MSM_RUN buckets [lo, lo + MSM_RUN) of one (MSM, window):
 // sum_k k B_k = T + (lo - 1) R with R = sum_k B_k and T = sum_k (k - lo + 1) B_k
 // (running sums from the top).  Output [mw][run] (stride MSM_MW * MSM_RUNS).
+template <class Gr>
 __global__ void __launch_bounds__(256, 2) k_msm_window(const uint32_t* __restrict__ buckets, uint32_t* __restrict__ runs) {
+  using M = GrMem<Gr>;
+  using J = typename Gr::jac;
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (size_t)MSM_MW * MSM_RUNS) return;
   const size_t mw = g / MSM_RUNS, run = g % MSM_RUNS;
   const uint32_t lo = (uint32_t)(run * MSM_RUN);
   const size_t base = mw * MSM_BUCKETS + lo;
-  g2j R = g2_infinity(), T = g2_infinity();
+  J R = Gr::inf(), T = Gr::inf();
 #pragma unroll 1
   for (int k = MSM_RUN - 1; k >= 0; --k) {
-    R = g2_add_body(R, ld_g2j(buckets, MSM_KEYS, base + k));
-    T = g2_add_body(T, R);
+    R = Gr::add_body(R, M::ld_jac(buckets, MSM_KEYS, base + k));
+    T = Gr::add_body(T, R);
   }
   if (lo == 0) {  // digits 0..63: T counts every bucket once too often
-    T = g2_add(T, g2_neg(R));
-  } else if (lo > 1) {
+    T = Gr::add(T, Gr::neg(R));
+  } else if (lo > 1) {  // + [lo - 1] R, double-and-add over the 16-bit multiplier
     const uint32_t s = lo - 1;
-    T = g2_add(T, g2_mul_words(R, &s, 1));
+    J acc = Gr::inf();
+#pragma unroll 1
+    for (int i = 31 - __builtin_clz(s); i >= 0; --i) {
+      acc = Gr::dbl(acc);
+      if ((s >> i) & 1u) acc = Gr::add(acc, R);
+    }
+    T = Gr::add(T, acc);
   }
-  st_g2j(runs, (size_t)MSM_MW * MSM_RUNS, g, T);
+  M::st_jac(runs, (size_t)MSM_MW * MSM_RUNS, g, T);
 }
 
 // One level of pairwise sums over `groups` independent arrays of n_in
 // Jacobian points each (group-major, stride total_in / total_out).
-__global__ void __launch_bounds__(256) k_g2_sum_level(int groups, size_t n_in, const uint32_t* __restrict__ in,
-                                                      size_t n_out, uint32_t* __restrict__ out) {
+template <class Gr>
+__global__ void __launch_bounds__(256) k_sum_level(int groups, size_t n_in, const uint32_t* __restrict__ in,
+                                                   size_t n_out, uint32_t* __restrict__ out) {
+  using M = GrMem<Gr>;
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= (size_t)groups * n_out) return;
   const size_t grp = g / n_out, j = g % n_out;
   const size_t tin = (size_t)groups * n_in, tout = (size_t)groups * n_out;
-  g2j P = ld_g2j(in, tin, grp * n_in + 2 * j);
-  if (2 * j + 1 < n_in) P = g2_add_body(P, ld_g2j(in, tin, grp * n_in + 2 * j + 1));
-  st_g2j(out, tout, g, P);
+  typename Gr::jac P = M::ld_jac(in, tin, grp * n_in + 2 * j);
+  if (2 * j + 1 < n_in) P = Gr::add_body(P, M::ld_jac(in, tin, grp * n_in + 2 * j + 1));
+  M::st_jac(out, tout, g, P);
 }
 
 // The root: W[mw] (one point per (MSM, window), stride MSM_MW) ->
 // P, S (stride-1 Jacobian SoA, the node layout rlc_check_locked reads).
+template <class Gr>
 __global__ void k_msm_root(const uint32_t* __restrict__ w, uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
+  using M = GrMem<Gr>;
   if (blockIdx.x != 0 || threadIdx.x >= 2) return;
   const int tree = threadIdx.x;  // 0: P (MSMs 0, 1 over R), 1: S (MSMs 2, 3 over sig)
-  g2j msm[2];
+  typename Gr::jac msm[2];
   for (int h = 0; h < 2; ++h) {
     const int m = 2 * tree + h;
-    g2j hi = ld_g2j(w, MSM_MW, 2 * m + 1);
-    for (int k = 0; k < MSM_C; ++k) hi = g2_dbl(hi);
-    msm[h] = g2_add(ld_g2j(w, MSM_MW, 2 * m), hi);
+    typename Gr::jac hi = M::ld_jac(w, MSM_MW, 2 * m + 1);
+    for (int k = 0; k < MSM_C; ++k) hi = Gr::dbl(hi);
+    msm[h] = Gr::add(M::ld_jac(w, MSM_MW, 2 * m), hi);
   }
-  st_g2j(tree ? s_out : p_out, 1, 0, g2_add(msm[0], g2_psi(msm[1])));
+  M::st_jac(tree ? s_out : p_out, 1, 0, Gr::add(msm[0], Gr::endo(msm[1])));
+}
+
+// ---------------------------------------------------------------- leaves, tree, nodes
+// Leaves of the RLC tree: P_i = [a_i] R_i + [b_i] endo(R_i), S_i = [a_i] sig_i +
+// [b_i] endo(sig_i) with (a_i, b_i) the two halves of rlc_coeff (infinity for
+// rounds whose decode verdict is already final).  R_i is affine here (batch
+// affine ran on the pre-cofactor hash points; (0, 0) marks the identity).
+// 2n threads: j < n computes P_j, j >= n computes S_{j-n}.  The scalar
+// multiplication is the window form (every lane runs the same sequence).
+template <class Gr>
+__global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, uint64_t seed, const uint32_t* __restrict__ r_aff,
+                                                       const uint32_t* __restrict__ sig_pts,
+                                                       const uint8_t* __restrict__ status,
+                                                       uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
+  using M = GrMem<Gr>;
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const bool sig = j >= n;
+  const size_t i = sig ? j - n : j;
+  typename Gr::jac acc = Gr::inf();
+  if (status[i] == ST_OK) {
+    const typename Gr::aff q = M::ld_aff(sig ? sig_pts : r_aff, n, i);
+    if (!Gr::aff_is_zero(q)) {
+      const uint64_t z = rlc_coeff(seed, i);
+      if constexpr (std::is_same<Gr, G2Ops>::value)
+        acc = g2_mul2_win4_affine(q, (uint32_t)z, (uint32_t)(z >> 32));
+      else
+        acc = mul2_win4_affine<Gr>(q, (uint32_t)z, (uint32_t)(z >> 32));
+    }
+  }
+  M::st_jac(sig ? s_out : p_out, n, i, acc);
+}
+
+// One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied); 2 n_out
+// threads, the first n_out on the P tree, the rest on the S tree.
+template <class Gr>
+__global__ void __launch_bounds__(256) k_rlc_level(size_t n_in, const uint32_t* __restrict__ p_in,
+                                                   const uint32_t* __restrict__ s_in, size_t n_out,
+                                                   uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
+  using M = GrMem<Gr>;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * n_out) return;
+  const bool sig = t >= n_out;
+  const size_t j = sig ? t - n_out : t;
+  const uint32_t* in = sig ? s_in : p_in;
+  const size_t a = 2 * j, b = 2 * j + 1;
+  typename Gr::jac P = M::ld_jac(in, n_in, a);
+  if (b < n_in) P = Gr::add_body(P, M::ld_jac(in, n_in, b));
+  M::st_jac(sig ? s_out : p_out, n_out, j, P);
+}
+
+// Candidate nodes for the pairing engine: h[c] = affine h_eff * P, sg[c] =
+// affine S, st[c] = ST_OK when both are finite (the engine then decides),
+// RLC_TRIVIAL when both are infinity (passes), ST_PAIRING when exactly one is
+// (e(Q, .) of a non-trivial prime-order point alone is never 1).
+template <class Gr>
+__global__ void __launch_bounds__(64) k_rlc_prep(size_t n_cand, const uint32_t* __restrict__ idx, size_t n_level,
+                                                 const uint32_t* __restrict__ p_lvl,
+                                                 const uint32_t* __restrict__ s_lvl, uint32_t* __restrict__ h_out,
+                                                 uint32_t* __restrict__ s_out, uint8_t* __restrict__ st) {
+  using M = GrMem<Gr>;
+  size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cand) return;
+  size_t j = idx[c];
+  const typename Gr::jac P = Gr::clear_cofactor(M::ld_jac(p_lvl, n_level, j));
+  const typename Gr::jac S = M::ld_jac(s_lvl, n_level, j);
+  const bool pi = Gr::is_inf(P), si = Gr::is_inf(S);
+  M::st_aff(h_out, n_cand, c, pi ? Gr::aff_zero() : Gr::to_aff(P));
+  M::st_aff(s_out, n_cand, c, si ? Gr::aff_zero() : Gr::to_aff(S));
+  st[c] = (pi && si) ? RLC_TRIVIAL : (pi || si) ? (uint8_t)ST_PAIRING : (uint8_t)ST_OK;
+}
+
+// Multi-GPU RLC: the per-device roots (P, S), gathered over RCCL as
+// [dev][P (JAC words), S (JAC words)] (each a stride-1 Jacobian SoA), summed
+// into one node (stride 1) that is checked once for the whole node.
+template <class Gr>
+__global__ void k_rlc_sum_roots(int ndev, const uint32_t* __restrict__ roots, uint32_t* __restrict__ p_out,
+                                uint32_t* __restrict__ s_out) {
+  using M = GrMem<Gr>;
+  if (blockIdx.x != 0 || threadIdx.x >= 2) return;
+  const int w = threadIdx.x;  // 0: P, 1: S
+  typename Gr::jac acc = M::ld_jac(roots + w * M::JAC, 1, 0);
+  for (int d = 1; d < ndev; ++d) acc = Gr::add(acc, M::ld_jac(roots + (size_t)d * 2 * M::JAC + w * M::JAC, 1, 0));
+  M::st_jac(w ? s_out : p_out, 1, 0, acc);
 }
 
 }  // namespace dgpu

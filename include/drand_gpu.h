@@ -150,7 +150,8 @@ int dgpu_verify_recovered(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t p
  *       from rlc_seed, exact per-round verdicts by bisection; the verdicts are
  *       identical to per-round mode except with probability <= 2^-64 per
  *       failing check; pass a fresh unpredictable seed for adversarial input;
- *       G2-signature schemes only).  The scheme must sign on the same group as
+ *       every scheme: G2 signatures and the G1-signature schemes, whose
+ *       node checks run on the key's fixed-Q line table).  The scheme must sign on the same group as
  *       the installed key's scheme (else DGPU_ENOKEY).
  * verdict_bits: ceil(n/8) bytes out.  reason: optional n bytes out. */
 int dgpu_verify_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *rounds, const uint8_t *sigs,
@@ -168,16 +169,22 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
                              uint8_t *d_verdict_bits, uint8_t *d_reason, void *stream);
 
 /* Instrumentation: when enabled, every verify call records one HIP event
- * per kernel stage on the stream it runs on; dgpu_stage_times returns the
+ * per kernel stage on the stream it runs on; dgpu_stage_times writes the
  * stage durations (ms) and names of the last call, summed per name over
  * chunks (per-round mode: hash_to_g2, h_affine, decode_g2, eng_lines,
- * eng_miller, eng_inv, eng_fe, pack_verdicts; G1 signatures: hash_to_g1,
- * h_affine, decode_g1, eng_miller (eng_lines_fixed first under
- * DGPU_G1_LINES=buffer), ...; RLC mode: rlc_hash_to_g2_raw,
- * decode_g2, rlc_leaves_tree, rlc_prep and the engine stages of the node
- * checks, rlc_bisection; recovery: recover_hash, recover_decode, engine
- * stages, recover_msm, recover_verdict) and returns the number written. */
-#define DGPU_MAX_STAGES 8
+ * eng_miller, eng_inv, eng_fe, eng_fe_chain, eng_fe_kbinv, pack_verdicts; G1
+ * signatures: hash_to_g1, h_affine, decode_g1, eng_miller (eng_lines_fixed
+ * first under DGPU_G1_LINES=buffer), ...; RLC mode: rlc_hash_to_g2_raw /
+ * rlc_hash_to_g1_raw, decode_g2 / decode_g1, rlc_affine, rlc_root_msm,
+ * rlc_prep, the engine stages of the node checks, rlc_leaves_tree,
+ * rlc_bisection; recovery: recover_hash, recover_decode, engine stages,
+ * recover_msm, recover_verdict), at most max_stages of them, and returns the
+ * number of distinct stages the call recorded (like snprintf: a value above
+ * max_stages means the output was truncated).  DGPU_MAX_STAGES bounds every
+ * pipeline's count.  A call that recorded more stage events than the
+ * library's event pool holds makes dgpu_stage_times fail (DGPU_EINVAL)
+ * instead of reporting partial sums. */
+#define DGPU_MAX_STAGES 32
 int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
 

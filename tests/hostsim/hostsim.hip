@@ -8,6 +8,7 @@
 #include "../../drand_amd/csrc/pairing.cuh"
 #define DG_NO_KERNELS
 #include "../../drand_amd/csrc/g1sig.cuh"
+#include "../../drand_amd/csrc/group_ops.cuh"
 #include "../../drand_amd/csrc/lines_thread.cuh"
 #include "../../drand_amd/csrc/kb_thread.cuh"
 
@@ -122,6 +123,9 @@ static void msg_words(const uint8_t* msg32, uint32_t m[8]);
 //   k=5 k_hash_to_g1_beacons (expand under the G2 suite's DST + SSWU/iso-11 + h_eff)
 //   k=6 k_decode_g1_sigs (decode + endomorphism membership)
 //   k=7 k_g1_batch_affine per point
+//   k=8 k_hash_to_g1_raw (RLC, G1 signatures: no cofactor clearing)
+//   k=9 one G1 RLC leaf: mul2_win4_affine<G1Ops> (k_rlc_leaves<G1Ops>; two per round)
+//   k=10 one G1 tree node: g1_add_body (k_rlc_level<G1Ops>; about two per round)
 int hs_count_extra(const uint8_t* msg32, const uint8_t* sig96, const uint8_t* sig48, uint64_t coeff,
                    unsigned long long* out) {
 #ifdef DG_COUNT_OPS
@@ -188,6 +192,17 @@ int hs_count_extra(const uint8_t* msg32, const uint8_t* sig96, const uint8_t* si
     }
     out[14] = (dg_count_mul + G / 2) / G; out[15] = (dg_count_sqr + G / 2) / G;
   }
+  dg_count_mul = dg_count_sqr = 0;
+  const g1j R1 = g1_add_body(map_to_curve_sswu_iso11_body(fp_from_be64_words(uni)),
+                             map_to_curve_sswu_iso11_body(fp_from_be64_words(uni + 16)));
+  out[16] = dg_count_mul; out[17] = dg_count_sqr;
+  const g1a R1a = g1_to_affine(R1);
+  dg_count_mul = dg_count_sqr = 0;
+  const g1j leaf1 = mul2_win4_affine<G1Ops>(R1a, (uint32_t)coeff, (uint32_t)(coeff >> 32));
+  out[18] = dg_count_mul; out[19] = dg_count_sqr;
+  dg_count_mul = dg_count_sqr = 0;
+  (void)g1_add_body(leaf1, R1);
+  out[20] = dg_count_mul; out[21] = dg_count_sqr;
   return 0;
 #else
   (void)msg32; (void)sig96; (void)sig48; (void)coeff; (void)out;
@@ -426,6 +441,71 @@ extern "C" int hs_rlc_batch_check(const uint8_t* pk48, const uint8_t* msgs32, co
   }
   g2a Pa = g2_to_affine(g2_clear_cofactor(P)), Sa = g2_to_affine(S);
   fp12 f = miller_loop_2(Pa, fp_neg(pk.x), pk.y, Sa, fp_neg(C_G1_X), C_G1_NEG_Y);
+  return fp12_is_one(final_exponentiation(f)) ? 0 : 1;
+}
+
+// G1-signature RLC (rlc_msm.cuh over G1Ops): for a pre-cofactor hash point R
+// on E1 (not in G1), the group-generic window ladder [a] R + [b] phi(R) equals
+// plain double-and-add for the scalar pairs given; phi acts on H = h_eff R as
+// [-x^2]; and h_eff ([a] R + [b] phi(R)) == [a] H + [b] phi(H).
+extern "C" int hs_g1_mul2_win4_check(const uint8_t* msg32, const uint32_t* ab, int n) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  uint32_t uni[32];
+  expand_xmd<false, 4>(uni, m);
+  const g1j R = g1_add(map_to_curve_sswu_iso11(fp_from_be64_words(uni)),
+                       map_to_curve_sswu_iso11(fp_from_be64_words(uni + 16)));
+  const g1a Ra = g1_to_affine(R);
+  const g1j H = g1_clear_cofactor(R);
+  // phi(H) == -[x^2] H
+  const uint32_t absx[2] = {(uint32_t)BLS_X_ABS, (uint32_t)(BLS_X_ABS >> 32)};
+  if (!g1_eq(g1_phi(H), g1_neg(g1_mul_words(g1_mul_words(H, absx, 2), absx, 2)))) return -1;
+  // phi on R (outside G1) is not [-x^2]: the endomorphism is used as a map
+  if (g1_eq(g1_phi(R), g1_neg(g1_mul_words(g1_mul_words(R, absx, 2), absx, 2)))) return -2;
+  for (int i = 0; i < n; ++i) {
+    const uint32_t a = ab[2 * i], b = ab[2 * i + 1];
+    const g1j want = g1_add(g1_mul_words(R, &a, 1), g1_mul_words(g1_phi(R), &b, 1));
+    const g1j got = mul2_win4_affine<G1Ops>(Ra, a, b);
+    if (!g1_eq(got, want)) return i + 1;
+    const g1j lhs = g1_clear_cofactor(got);
+    const g1j rhs = g1_add(g1_mul_words(H, &a, 1), g1_mul_words(g1_phi(H), &b, 1));
+    if (!g1_eq(lhs, rhs)) return 1000 + i;
+  }
+  return 0;
+}
+
+// RLC collapse check for G1 signatures over a batch signed here with sk
+// (sig_i = [sk] H_i; sig_i of the `bad` index signs the next message instead):
+// returns 0 if e(h_eff sum r_i R_i, pk) e(-sum r_i sig_i, g2) == 1 with the
+// leaves computed as the device does (mul2_win4_affine<G1Ops>, r = a + b lambda).
+extern "C" int hs_g1_rlc_batch_check(const uint8_t* msgs32, int n, uint64_t sk, uint64_t seed, int bad, int g1dst) {
+  const uint32_t skw[2] = {(uint32_t)sk, (uint32_t)(sk >> 32)};
+  const g2j pk = g2_mul_words(g2_from_affine(g2a{C_G2_X, C_G2_Y}), skw, 2);
+  g1j P = g1_infinity(), S = g1_infinity();
+  for (int i = 0; i < n; ++i) {
+    auto raw = [&](int k) {
+      uint32_t m[8], uni[32];
+      msg_words(msgs32 + 32 * k, m);
+      if (g1dst)
+        expand_xmd<true, 4>(uni, m);
+      else
+        expand_xmd<false, 4>(uni, m);
+      return g1_add(map_to_curve_sswu_iso11(fp_from_be64_words(uni)),
+                    map_to_curve_sswu_iso11(fp_from_be64_words(uni + 16)));
+    };
+    const g1j R = raw(i);
+    const g1j sig = g1_mul_words(g1_clear_cofactor(i == bad ? raw((i + 1) % n) : R), skw, 2);
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * ((uint64_t)i + 1);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (!z) z = 1;
+    P = g1_add(P, mul2_win4_affine<G1Ops>(g1_to_affine(R), (uint32_t)z, (uint32_t)(z >> 32)));
+    S = g1_add(S, mul2_win4_affine<G1Ops>(g1_to_affine(sig), (uint32_t)z, (uint32_t)(z >> 32)));
+  }
+  const g1a Pa = g1_to_affine(g1_clear_cofactor(P)), Sa = g1_to_affine(S);
+  // e(Pa, pk) e(-Sa, g2): miller_loop_2 takes each G1 point as (-x, y)
+  fp12 f = miller_loop_2(g2_to_affine(pk), fp_neg(Pa.x), Pa.y, g2a{C_G2_X, C_G2_Y}, fp_neg(Sa.x), fp_neg(Sa.y));
   return fp12_is_one(final_exponentiation(f)) ? 0 : 1;
 }
 

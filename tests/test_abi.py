@@ -52,3 +52,13 @@ def test_ingest_library_exports_its_header():
     assert lib is not None, "libdrand_ingest.so not built (__graft_entry__.build())"
     for n in names:
         assert hasattr(lib, n), n
+
+
+def test_max_stages_macro_matches_binding():
+    """DGPU_MAX_STAGES (include/drand_gpu.h) is what the Python binding sizes
+    dgpu_stage_times' arrays by; the GPU tests assert every pipeline's stage
+    count (the call returns the count needed) stays within it."""
+    from drand_amd import _lib
+    txt = open(os.path.join(ROOT, "include", "drand_gpu.h")).read()
+    (val,) = re.findall(r"#define DGPU_MAX_STAGES (\d+)", txt)
+    assert int(val) == _lib.MAX_STAGES >= 16

@@ -159,10 +159,7 @@ def test_rlc_root_first_clean_and_single_bad(gpu_ctx):
     _lib.check(lib.dgpu_set_profiling(v.ctx.handle, 1))
     try:
         assert not v.verify_reasons(beacons, c.pk, _lib.MODE_RLC).any()
-        names = (ctypes.c_char_p * 32)()
-        ms = (ctypes.c_float * 32)()
-        ns = lib.dgpu_stage_times(v.ctx.handle, ms, 32, names)
-        stages = {names[i].decode() for i in range(ns)}
+        stages = set(_lib.stage_times(v.ctx))
     finally:
         _lib.check(lib.dgpu_set_profiling(v.ctx.handle, 0))
     # the bucket-MSM root (rlc_msm.cuh) equals the tree's: a clean batch

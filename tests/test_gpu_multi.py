@@ -67,7 +67,8 @@ def test_verify_multi_same_device_unchained_and_on_g1(monkeypatch):
     from drand_amd.synth import corrupt, make_chain
     monkeypatch.setenv("DGPU_MULTI_ALLOW_SAME_DEVICE", "1")
     for name, code in (("pedersen-bls-unchained", _lib.SCHEME_UNCHAINED),
-                       ("bls-unchained-on-g1", _lib.SCHEME_UNCHAINED_G1)):
+                       ("bls-unchained-on-g1", _lib.SCHEME_UNCHAINED_G1),
+                       ("bls-unchained-g1-rfc9380", _lib.SCHEME_G1_RFC9380)):
         c = make_chain(62, 997, code, seg_len=64)
         corrupt(c, 62, rate=5e-3)
         beacons = [c.beacon(i) for i in range(len(c))]
@@ -75,6 +76,11 @@ def test_verify_multi_same_device_unchained_and_on_g1(monkeypatch):
         mv = MultiVerifier(_sch(name), [0, 0])
         try:
             assert mv.verify_reasons(beacons, c.pk).tolist() == single.tolist(), name
+            # RLC at D = 2: per-device roots (G2 or G1 Jacobian sums) gathered and
+            # summed on device 0; descent per shard when the node fails
+            assert mv.verify_reasons(beacons, c.pk, _lib.MODE_RLC).tolist() == single.tolist(), name
+            clean = [b for b, r in zip(beacons, single) if r == 0]
+            assert not mv.verify_reasons(clean, c.pk, _lib.MODE_RLC).any(), name
         finally:
             mv.close()
 

@@ -4,6 +4,8 @@ import ctypes
 import hashlib
 import random
 
+import pytest
+
 from conftest import load_golden
 from oracle import bls12381 as B
 from oracle import drand_ref as D
@@ -164,6 +166,29 @@ def test_rlc_window_ladder_edge_scalars(hostsim):
     pairs += [(rnd.getrandbits(32), rnd.getrandbits(32)) for _ in range(8)]
     ab = (ctypes.c_uint32 * (2 * len(pairs)))(*[v for p in pairs for v in p])
     assert hostsim.hs_g2_mul2_win4_check(bytes(range(32)), ab, len(pairs)) == 0
+
+
+def test_g1_rlc_window_ladder_and_endomorphism(hostsim):
+    """G1-signature RLC leaves (rlc_msm.cuh k_rlc_leaves<G1Ops>): the
+    group-generic ladder [a] R + [b] phi(R) equals plain double-and-add on a
+    pre-cofactor hash point R outside G1; phi(x, y) = (beta x, y) acts on
+    H = h_eff R as [-x^2] (and not on R); h_eff commutes with the ladder."""
+    import random
+    rnd = random.Random(9)
+    edge = [0, 1, 7, 8, 9, 15, 16, 0x88888888, 0xFFFFFFFF, 0x80000000]
+    pairs = [(a, b) for a in edge for b in (0, 9, 0xFFFFFFFF)] + [(rnd.getrandbits(32), rnd.getrandbits(32)) for _ in range(6)]
+    ab = (ctypes.c_uint32 * (2 * len(pairs)))(*[v for p in pairs for v in p])
+    assert hostsim.hs_g1_mul2_win4_check(bytes(range(32)), ab, len(pairs)) == 0
+
+
+@pytest.mark.parametrize("g1dst", [0, 1])
+def test_g1_rlc_collapse_algebra(hostsim, g1dst):
+    """e(h_eff sum r_i R_i, pk) e(-sum r_i sig_i, g2) == 1 for a valid batch of
+    G1 signatures (both DSTs), with r_i = a_i + b_i lambda as the device draws
+    them; one signature over another round's message makes it fail."""
+    msgs = b"".join(bytes([i]) * 32 for i in range(4))
+    assert hostsim.hs_g1_rlc_batch_check(msgs, 4, ctypes.c_uint64(0x1234567), ctypes.c_uint64(5), -1, g1dst) == 0
+    assert hostsim.hs_g1_rlc_batch_check(msgs, 4, ctypes.c_uint64(0x1234567), ctypes.c_uint64(5), 2, g1dst) == 1
 
 
 def test_engine_pairing_host_emulation(hostsim):

@@ -62,6 +62,27 @@ def test_gpu_recover_matches_fixtures(name):
 
 
 @pytest.mark.gpu
+def test_gpu_recover_stage_count_within_max_stages():
+    """The recovery pipeline records the most stages of any call (hash,
+    decode, engine stages, MSM, verdicts): dgpu_stage_times' count (the
+    count needed) stays within DGPU_MAX_STAGES (_lib.stage_times asserts it)."""
+    from drand_amd import _lib
+    from drand_amd.threshold import ThresholdGroup
+    g = load_golden("recover_t17_n32.json")
+    grp = ThresholdGroup([bytes.fromhex(c) for c in g["commits"]], g["n"])
+    msgs = [bytes.fromhex(c["msg"]) for c in g["cases"]]
+    parts = [[bytes.fromhex(p) for p in c["partials"]] for c in g["cases"]]
+    lib = grp.ctx.lib
+    _lib.check(lib.dgpu_set_profiling(grp.ctx.handle, 1))
+    try:
+        grp.recover_batch(msgs, parts)
+        st = _lib.stage_times(grp.ctx)
+    finally:
+        _lib.check(lib.dgpu_set_profiling(grp.ctx.handle, 0))
+    assert 8 < len(st) <= _lib.MAX_STAGES, st
+
+
+@pytest.mark.gpu
 def test_gpu_recover_many_rounds_property():
     """Size-independent property at a larger batch: every round with >= t good
     partials recovers the group signature (sk * H(msg)); rounds with t - 1

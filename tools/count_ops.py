@@ -59,12 +59,13 @@ def main():
     import hashlib
     g1 = json.load(open(os.path.join(ROOT, "tests", "golden", "chain_on_g1_s1.json")))
     msg = hashlib.sha256(bytes.fromhex(r["prev"]) + r["round"].to_bytes(8, "big")).digest()
-    xo = (ctypes.c_ulonglong * 16)()
+    xo = (ctypes.c_ulonglong * 22)()
     rc = L.hs_count_extra(msg, bytes.fromhex(r["sig"]), bytes.fromhex(g1["rounds"][0]["sig"]),
                           ctypes.c_uint64(0x9E3779B97F4A7C15), xo)
     assert rc == 0, rc
     part = {name: (xo[2 * i], xo[2 * i + 1]) for i, name in enumerate(
-        ["rlc_hash", "decode_sub", "leaf", "node", "g2_affine", "hash_g1", "decode_g1", "g1_affine"])}
+        ["rlc_hash", "decode_sub", "leaf", "node", "g2_affine", "hash_g1", "decode_g1", "g1_affine",
+         "rlc_hash_g1", "leaf_g1", "node_g1"])}
 
     def ent(*terms):
         mul = sum(c * part[p][0] for c, p in terms)
@@ -79,6 +80,10 @@ def main():
     kernels["k_g1_batch_affine"] = ent((1, "g1_affine"))
     kernels["k_g2_batch_affine"] = ent((1, "g2_affine"))
     kernels["k_decode_g1_sigs"] = ent((1, "decode_g1"))
+    # RLC for the G1-signature schemes: raw hash (no h_eff), two G1 leaves
+    # (phi split) + the affine conversion of R + two tree nodes
+    kernels["rlc_hash_to_g1_raw"] = ent((1, "rlc_hash_g1"))
+    kernels["rlc_leaves_tree_g1"] = ent((2, "leaf_g1"), (1, "g1_affine"), (2, "node_g1"))
     # group-law ops: the recovery MSM's work figure is composed from these
     go = (ctypes.c_ulonglong * 14)()
     assert L.hs_count_group_ops(msg, go) == 0
@@ -87,6 +92,11 @@ def main():
                               "g2_to_affine"]):
         mul, sqr = go[2 * i], go[2 * i + 1]
         res_ops[name] = {"fp_mul": mul, "fp_sqr": sqr, "mads": MADS_MUL * mul + MADS_SQR * sqr}
+    # the bucket-MSM root: one mixed addition per point and (MSM, window) --
+    # 8 per round (4 MSMs x 2 windows; bucket reduction and window sums are
+    # per bucket, < 0.2 additions per round at 10M rounds)
+    kernels["rlc_root_msm"] = {k: 8 * res_ops["g2_add_affine"][k] for k in ("fp_mul", "fp_sqr", "mads")}
+    kernels["rlc_root_msm_g1"] = {k: 8 * res_ops["g1_add_affine"][k] for k in ("fp_mul", "fp_sqr", "mads")}
     res = {"per_round_verify": {"fp_mul": tot_mul, "fp_sqr": tot_sqr, "stages": stages},
            "kernels": kernels, "group_ops": res_ops,
            "unit": "per round; mads = v_mad_u64_u32 issued by the Fp multiplications (%d per mul, %d per sqr)"

@@ -86,6 +86,8 @@ def parse(argv=None):
                     help="abi driver: comma-separated device list (default 0..N-1; a repeated device needs "
                          "DGPU_MULTI_ALLOW_SAME_DEVICE=1)")
     ap.add_argument("--abi-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the chosen driver, the rank count and each rank's shard, touch no GPU")
     return ap.parse_args(argv)
 
 
@@ -479,7 +481,7 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
     import torch
     from drand_amd import _lib
     from drand_amd.chain import get_context
-    from drand_amd.dist import gather_verdict_bits, shard_range
+    from drand_amd.dist import gather_verdict_bits, shard_range, verify_rlc_sharded
     from drand_amd.synth import corrupt_global
 
     lo, hi = shard_range(n_total, world, rank)
@@ -507,6 +509,10 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
     seed = args.rlc_seed + 7 * rank
 
     def step_mode(md, sd):
+        if md == _lib.MODE_RLC and world > 1:  # the per-rank RLC protocol: roots all-gathered, one node check
+            verify_rlc_sharded(ctx, code, pk, n, d_rounds, d_sigs, d_sig_len, d_prev, d_prev_len, sd, d_bits, stream,
+                               world, rank)
+            return
         _lib.check(lib.dgpu_verify_beacons_device(
             ctx.handle, code, _lib.ptr(pk), pk.size, n, d_rounds.data_ptr(), d_sigs.data_ptr(), 96,
             d_sig_len.data_ptr(), d_prev.data_ptr(), 96, d_prev_len.data_ptr(), md, sd, d_bits.data_ptr(),
@@ -748,8 +754,26 @@ def main_verify(args, world, rank, local):
         "roofline": main.get("roofline"),
         "cpu_baseline": main.get("cpu_baseline"),
     }
+    out["driver"] = driver_info(world)
     out.update(legs)
     print(json.dumps(out), flush=True)
+
+
+def driver_info(world):
+    """How the run drove the GPUs: one process per GPU over torch.distributed
+    (every rank calls the C ABI's per-device entry points; the exchange steps
+    -- verdict bitmaps, and in RLC mode the per-rank roots of the
+    dgpu_rlc_root_device / dgpu_rlc_finish_device protocol -- over the
+    process group), with the world size the process group initialised."""
+    info = {"name": "dist", "api": "dgpu_verify_beacons_device per rank; RLC: dgpu_rlc_root_device + all-gather of "
+                                   "roots + dgpu_rlc_finish_device", "ranks": world}
+    try:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            info.update(rccl_world_size=dist.get_world_size(), backend=str(dist.get_backend()))
+    except Exception:  # reported, never fatal
+        pass
+    return info
 
 
 def main_recover(args, world, rank, local):
@@ -769,7 +793,10 @@ def dryrun(args):
     rank = int(os.environ.get("RANK", "0"))
     n_total = args.rounds or 10_000_000
     me = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "shard": shard_range(n_total, world, rank)}
-    if world > 1:
+    if args.driver == "abi":  # one process: the library shards over the devices itself
+        world = args.gpus
+        got = [{"device": k, "shard": shard_range(n_total, world, k)} for k in range(world)]
+    elif world > 1:
         dist.init_process_group("gloo")
         got = [None] * world
         dist.all_gather_object(got, me)
@@ -777,11 +804,19 @@ def dryrun(args):
     else:
         got = [me]
     if rank == 0:
-        print(json.dumps({"dryrun": True, "n_gpus": world, "rounds_total": n_total, "ranks": got}), flush=True)
+        driver = ("abi: one process, dgpu_verify_multi over %d devices" % args.gpus if args.driver == "abi" else
+                  "dist: %d rank processes over torch.distributed (nccl = RCCL on GPUs), dgpu_verify_beacons_device "
+                  "per rank, RLC roots via dgpu_rlc_root_device / dgpu_rlc_finish_device" % world)
+        print(json.dumps({"dryrun": True, "driver": args.driver, "driver_detail": driver, "n_gpus": world,
+                          "rounds_total": n_total, "ranks": got}), flush=True)
 
 
 def main():
     args = parse()
+    if args.dry_run:
+        os.environ["DRAND_BENCH_DRYRUN"] = "1"
+        if args.driver == "abi":
+            return dryrun(args)
     if args.abi_child or (args.driver == "abi" and "WORLD_SIZE" not in os.environ):
         # one process over all GPUs (never under a rank launcher)
         res = main_abi(args)

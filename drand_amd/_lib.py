@@ -62,6 +62,10 @@ SYMBOLS = [
                                        _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P]),
     ("dgpu_verify_beacons_device", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _c.c_size_t, _P,
                                               _P, _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P, _P]),
+    ("dgpu_rlc_root_bytes", _c.c_int, [_c.c_int]),
+    ("dgpu_rlc_root_device", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P,
+                                        _c.c_size_t, _P, _c.c_uint64, _P, _P]),
+    ("dgpu_rlc_finish_device", _c.c_int, [_P, _c.c_size_t, _P, _P, _P, _P]),
     ("dgpu_verify_recovered", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _c.c_size_t, _P, _c.c_size_t, _P, _P,
                                          _c.c_size_t, _P, _c.c_int, _c.c_uint64, _P, _P]),
     ("dgpu_hash_to_curve", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _c.c_size_t, _P, _P]),

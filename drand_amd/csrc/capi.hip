@@ -205,6 +205,14 @@ struct dgpu_ctx {
   std::vector<const char*> stage_name;
   int n_ev = 0;
   bool ev_overflow = false;  // the last call recorded more than STAGE_EVENTS_MAX stage events
+  // per-rank RLC protocol (dgpu_rlc_root_device -> the caller's exchange of
+  // roots -> dgpu_rlc_finish_device): the shard's points stay in rlc_tree /
+  // sig_pts / status between the two calls; any other verify or recovery
+  // call on the context cancels the pending root
+  bool rlc_pending = false;
+  verify_args rlc_args{};
+  uint8_t rlc_pk[96] = {};
+  size_t rlc_pk_len = 0;
 };
 
 namespace {
@@ -562,6 +570,18 @@ int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees&
   return sig_on_g1(a.scheme) ? rlc_tree_t<G1Ops>(c, a, s, T) : rlc_tree_t<G2Ops>(c, a, s, T);
 }
 
+// The identity (Z = 0) of the signature group as a stride-1 Jacobian point
+// (jw words): the root of an empty shard.
+int rlc_identity_words(bool g1, uint32_t* w) {
+  const g2j inf2 = g2_infinity();
+  const g1j inf1 = g1_infinity();
+  const fp* co2[6] = {&inf2.x.c0, &inf2.x.c1, &inf2.y.c0, &inf2.y.c1, &inf2.z.c0, &inf2.z.c1};
+  const fp* co1[3] = {&inf1.x, &inf1.y, &inf1.z};
+  const int nc = g1 ? 3 : 6;
+  for (int j = 0; j < nc; ++j) memcpy(w + j * FP_LIMBS, (g1 ? co1[j] : co2[j])->l, FP_LIMBS * 4);
+  return nc * FP_LIMBS;
+}
+
 // Check candidate nodes cand of a level (P_lvl, S_lvl, n_level nodes) on the
 // pairing engine: e(pk, h_eff P) e(-g1, S) == 1 (G2 signatures) or
 // e(h_eff P, pk) e(-S, g2) == 1 (G1 signatures: the key's fixed-Q line
@@ -889,6 +909,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   uint8_t* st = (uint8_t*)c->status.p;
   c->n_ev = 0;
   c->ev_overflow = false;
+  c->rlc_pending = false;
   if (a.mode == DGPU_MODE_RLC) {
     // root first, by bucket MSM; the tree of leaves only when it fails
     const int jw = rlc_geom_of(sig_on_g1(a.scheme)).jw;
@@ -1208,6 +1229,88 @@ int dgpu_verify_beacons_device(dgpu_ctx* c, int scheme, const uint8_t* pk, size_
   const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
                       d_sigs, sig_stride, d_sig_len, mode, rlc_seed};
   return verify_device_locked(c, k, a, d_bits, d_reason, s);
+}
+
+int dgpu_rlc_root_bytes(int scheme) {
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  return 2 * rlc_geom_of(sig_on_g1(scheme)).jw * 4;
+}
+
+int dgpu_rlc_root_device(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_len, size_t n,
+                         const uint64_t* d_rounds, const uint8_t* d_sigs, size_t sig_stride, const uint32_t* d_sig_len,
+                         const uint8_t* d_prev, size_t prev_stride, const uint32_t* d_prev_len, uint64_t rlc_seed,
+                         uint8_t* d_root, void* stream) {
+  if (!c || !d_root) return set_err(DGPU_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  key_entry* k = nullptr;
+  int rc = get_key_locked(c, scheme, pk, pk_len, &k);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  stream_order ord(c, s);
+  const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
+                      d_sigs, sig_stride, d_sig_len, DGPU_MODE_RLC, rlc_seed};
+  if ((rc = check_args(c, k, a))) return rc;
+  c->rlc_pending = false;
+  const rlc_geom G = rlc_geom_of(sig_on_g1(scheme));
+  if (n == 0) {
+    uint32_t inf[G2J_WORDS];
+    rlc_identity_words(G.g1, inf);
+    HIP_TRY(hipMemcpyAsync(d_root, inf, (size_t)G.jw * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_root + (size_t)G.jw * 4, inf, (size_t)G.jw * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the host source goes out of scope
+  } else {
+    if ((rc = c->status.ensure(n))) return rc;
+    c->n_ev = 0;
+    c->ev_overflow = false;
+    if ((rc = rlc_points_locked(c, a, s)) || (rc = rlc_root_msm_locked(c, a, s, (uint32_t*)d_root))) return rc;
+  }
+  c->rlc_args = a;
+  memcpy(c->rlc_pk, pk, pk_len);
+  c->rlc_pk_len = pk_len;
+  c->rlc_pending = true;
+  return DGPU_OK;
+}
+
+int dgpu_rlc_finish_device(dgpu_ctx* c, size_t n_roots, const uint8_t* d_roots, uint8_t* d_bits, uint8_t* d_reason,
+                           void* stream) {
+  if (!c || !d_roots || n_roots == 0) return set_err(DGPU_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->rlc_pending) return set_err(DGPU_EINVAL, "no pending dgpu_rlc_root_device on this context");
+  c->rlc_pending = false;
+  const verify_args a = c->rlc_args;
+  if (a.n && !d_bits) return set_err(DGPU_EINVAL, "null verdict buffer");
+  HIP_TRY(hipSetDevice(c->device));
+  key_entry* k = nullptr;
+  int rc = get_key_locked(c, a.scheme, c->rlc_pk, c->rlc_pk_len, &k);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  stream_order ord(c, s);
+  const rlc_geom G = rlc_geom_of(sig_on_g1(a.scheme));
+  if ((rc = c->rlc_root.ensure(2 * (size_t)G.jw * 4))) return rc;
+  uint32_t* sum = (uint32_t*)c->rlc_root.p;
+  mark(c, s, "rlc_root_sum");
+  if (G.g1)
+    hipLaunchKernelGGL(k_rlc_sum_roots<G1Ops>, dim3(1), dim3(64), 0, s, (int)n_roots, (const uint32_t*)d_roots, sum,
+                       sum + G.jw);
+  else
+    hipLaunchKernelGGL(k_rlc_sum_roots<G2Ops>, dim3(1), dim3(64), 0, s, (int)n_roots, (const uint32_t*)d_roots, sum,
+                       sum + G.jw);
+  HIP_TRY(hipGetLastError());
+  std::vector<uint8_t> fail;
+  if ((rc = rlc_check_locked(c, k, std::vector<uint32_t>{0}, 1, sum, sum + G.jw, s, &fail))) return rc;
+  if (a.n == 0) return DGPU_OK;
+  if (fail[0]) {  // this shard's tree, its own root first unless it is the node's (one root)
+    rlc_trees T;
+    if ((rc = rlc_tree_locked(c, a, s, T)) || (rc = rlc_descend_locked(c, k, T, s, n_roots == 1))) return rc;
+  }
+  const uint8_t* st = (const uint8_t*)c->status.p;
+  mark(c, s, "pack_verdicts");
+  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((a.n + 7) / 8, 256)), dim3(256), 0, s, a.n, st, d_bits);
+  HIP_TRY(hipGetLastError());
+  mark(c, s);
+  if (d_reason) HIP_TRY(hipMemcpyAsync(d_reason, st, a.n, hipMemcpyDeviceToDevice, s));
+  return DGPU_OK;
 }
 
 int dgpu_verify_recovered(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_len, size_t n, const uint8_t* msgs,
@@ -1621,6 +1724,7 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
   if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
   c->n_ev = 0;
   c->ev_overflow = false;
+  c->rlc_pending = false;
   if (c->recover_exact)
     return recover_exact_locked(c, n_rounds, d_msgs, m, d_parts, stride, d_plen, d_out, d_ok, d_status, s);
   const size_t items = n_rounds * m;

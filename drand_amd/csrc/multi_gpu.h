@@ -297,12 +297,8 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
     {
       // the per-device roots to every device; one check of their sum on device 0
       // the identity (Z = 0) of the signature group, for empty shards
-      const g2j inf2 = g2_infinity();
-      const g1j inf1 = g1_infinity();
       uint32_t inf_words[G2J_WORDS];
-      const fp* co2[6] = {&inf2.x.c0, &inf2.x.c1, &inf2.y.c0, &inf2.y.c1, &inf2.z.c0, &inf2.z.c1};
-      const fp* co1[3] = {&inf1.x, &inf1.y, &inf1.z};
-      for (int j = 0; j < jw / FP_LIMBS; ++j) memcpy(inf_words + j * FP_LIMBS, (g1 ? co1[j] : co2[j])->l, FP_LIMBS * 4);
+      rlc_identity_words(g1, inf_words);
       for (int k = 0; k < D; ++k) {
         dgpu_ctx* c = m->ctx[k];
         HIP_TRY(hipSetDevice(c->device));

@@ -47,3 +47,43 @@ def faulty_rounds(verdicts, first_round):
     """Ascending list of invalid rounds (None if none), like CheckPastBeacons."""
     bad = np.nonzero(~verdicts)[0]
     return [int(first_round + i) for i in bad] or None
+
+
+def verify_rlc_sharded(ctx, code, pk, n, d_rounds, d_sigs, d_sig_len, d_prev, d_prev_len, seed, d_bits, stream,
+                       world, rank, d_reason=None, sig_stride=96, prev_stride=96):
+    """RLC mode across ranks through the library's per-rank protocol
+    (include/drand_gpu.h dgpu_rlc_root_device / dgpu_rlc_finish_device, the
+    multi-process form of dgpu_verify_multi's RLC mode): this rank's shard
+    root by bucket MSM, the roots all-gathered over torch.distributed (RCCL
+    on GPUs), the node (sum of every rank's root) checked with one pairing on
+    every rank, this shard's tree descended only when the node fails.  d_* are
+    device tensors of this rank's shard; `seed` must differ per rank.  Returns
+    nothing: the verdict bits land in d_bits (and reasons in d_reason)."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from . import _lib
+    lib = ctx.lib
+    rb = lib.dgpu_rlc_root_bytes(code)
+    _lib.check(min(rb, 0))
+    dev = d_bits.device
+    root = torch.empty(rb, dtype=torch.uint8, device=dev)
+    s = ctypes.c_void_p(stream.cuda_stream)
+    pkb = pk if hasattr(pk, "ctypes") else np.frombuffer(bytes(pk), dtype=np.uint8).copy()
+    _lib.check(lib.dgpu_rlc_root_device(ctx.handle, code, _lib.ptr(pkb), pkb.size, n, d_rounds.data_ptr(),
+                                        d_sigs.data_ptr(), sig_stride, d_sig_len.data_ptr(), d_prev.data_ptr(),
+                                        prev_stride, d_prev_len.data_ptr(), seed, root.data_ptr(), s))
+    if world > 1:
+        roots = torch.empty(world * rb, dtype=torch.uint8, device=dev)
+        stream.synchronize()  # the library's stream and the collective's
+        if dist.get_backend() == "gloo":  # CPU collectives (tests)
+            out = [torch.empty(rb, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(out, root.cpu())
+            roots.copy_(torch.cat(out))
+        else:
+            dist.all_gather_into_tensor(roots, root)
+        torch.cuda.current_stream(dev).synchronize()
+    else:
+        roots = root
+    _lib.check(lib.dgpu_rlc_finish_device(ctx.handle, world, roots.data_ptr(), d_bits.data_ptr(),
+                                          None if d_reason is None else d_reason.data_ptr(), s))

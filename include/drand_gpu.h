@@ -127,6 +127,33 @@ int dgpu_verify_beacons_device(dgpu_ctx *ctx, int scheme, const uint8_t *pk, siz
                                const uint32_t *d_prev_len, int mode, uint64_t rlc_seed, uint8_t *d_verdict_bits,
                                uint8_t *d_reason, void *stream);
 
+/* Per-rank RLC protocol for callers that run one process (or one context)
+ * per GPU and exchange data themselves -- the multi-process form of
+ * dgpu_verify_multi's RLC mode (chain/beacon/sync_manager.go:188-222 sharded
+ * by round range):
+ *   1. dgpu_rlc_root_device: hash, decode (+ subgroup) and the bucket-MSM
+ *      root of this rank's shard (device records as
+ *      dgpu_verify_beacons_device) into d_root (dgpu_rlc_root_bytes(scheme)
+ *      bytes of device memory: two Jacobian points of the signature group);
+ *      the shard's points stay in the context.  rlc_seed must differ per rank
+ *      (and be unpredictable to the beacons' producer).
+ *   2. the caller all-gathers the ranks' roots (RCCL / any transport) into
+ *      n_roots contiguous roots in device memory;
+ *   3. dgpu_rlc_finish_device: sums the roots and checks the node (one
+ *      pairing check); when it fails, descends this shard's tree; writes the
+ *      shard's verdict bits (and reasons) exactly as dgpu_verify_beacons_device.
+ * Every rank sees the same node verdict (the same roots, summed in order).
+ * Any other verify / recovery call on the context between 1 and 3 cancels
+ * the pending root (step 3 then fails with DGPU_EINVAL).  Synchronizes the
+ * stream in step 3 (node verdict) like RLC mode does. */
+int dgpu_rlc_root_bytes(int scheme);
+int dgpu_rlc_root_device(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t pk_len, size_t n,
+                         const uint64_t *d_rounds, const uint8_t *d_sigs, size_t sig_stride, const uint32_t *d_sig_len,
+                         const uint8_t *d_prev, size_t prev_stride, const uint32_t *d_prev_len, uint64_t rlc_seed,
+                         uint8_t *d_root, void *stream);
+int dgpu_rlc_finish_device(dgpu_ctx *ctx, size_t n_roots, const uint8_t *d_roots, uint8_t *d_verdict_bits,
+                           uint8_t *d_reason, void *stream);
+
 /* Batch key.Scheme.VerifyRecovered(pk, msg, sig) (= bls.Verify (R); call
  * sites chain/verify.go:44, chain/beacon/chain.go:165; AuthScheme
  * key/curve.go:39) over raw messages of any length: message i is msg_len[i]

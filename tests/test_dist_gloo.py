@@ -7,6 +7,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -85,3 +86,24 @@ def test_bench_launches_ranks():
     assert line["n_gpus"] == 2
     assert sorted(r["rank"] for r in line["ranks"]) == [0, 1]
     assert [tuple(r["shard"]) for r in sorted(line["ranks"], key=lambda r: r["rank"])] == [(0, 504), (504, 1000)]
+
+
+@pytest.mark.parametrize("driver", ["dist", "abi"])
+def test_bench_dry_run_reports_driver_and_ranks(driver):
+    """bench.py --gpus 2 --dry-run prints the chosen driver and the rank (or
+    device) count with each shard; both drivers shard the chain the same way
+    (dgpu_shard_range's rule), so their gathered verdict bitmaps cover the
+    same round ranges."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--rounds", "1000",
+                          "--dry-run", "--driver", driver], env=env, capture_output=True, text=True, timeout=300,
+                         check=True).stdout
+    line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+    assert line["driver"] == driver and line["n_gpus"] == 2
+    shards = [tuple(r["shard"]) for r in sorted(line["ranks"], key=lambda r: r.get("rank", r.get("device")))]
+    assert shards == [(0, 504), (504, 1000)]

@@ -158,7 +158,12 @@ class _Bucket:
 class BoltStore:
     """chain.Store's read side over a drand bolt file (read-only)."""
 
-    def __init__(self, path, bucket=b"beacons"):
+    def __init__(self, path, bucket=b"beacons", lenient_page_size=False):
+        """lenient_page_size (opt-in DEVIATION from bbolt v1.3.4): when meta 0
+        is torn, also try 4/8/16/64 KiB for meta 1 instead of only the OS
+        page size -- opens files the reference refuses (a file written with
+        another page size whose meta 0 is damaged)."""
+        self._lenient = lenient_page_size
         self._f = open(path, "rb")
         try:
             self._mm = mmap.mmap(self._f.fileno(), 0, access=mmap.ACCESS_READ)
@@ -196,9 +201,10 @@ class BoltStore:
         """bbolt v1.3.4 DB.Open + DB.meta: the page size comes from meta 0 only
         if meta 0 validates; otherwise bbolt assumes the OS page size (the
         size the file was created with) and finds meta 1 one page later.
-        Then the valid meta with the larger txid is current.  Besides the OS
-        page size, other common page sizes are tried for meta 1 when meta 0
-        is torn (a file written on another machine)."""
+        Then the valid meta with the larger txid is current.  Like bbolt,
+        only the OS page size is tried for meta 1 when meta 0 is torn (a
+        file with another page size then fails to open, as in the
+        reference) unless the store was opened with lenient_page_size."""
         mm = self._mm
         if len(mm) < 2 * 1024:
             raise BoltFormatError("file shorter than two meta pages")
@@ -206,7 +212,9 @@ class BoltStore:
         if m0 is not None:
             sizes = [m0["page_size"]]
         else:
-            sizes = [mmap.PAGESIZE] + [s for s in (4096, 8192, 16384, 65536) if s != mmap.PAGESIZE]
+            sizes = [mmap.PAGESIZE]
+            if self._lenient:
+                sizes += [s for s in (4096, 8192, 16384, 65536) if s != mmap.PAGESIZE]
         best = m0
         for ps in sizes:
             m1 = self._read_meta(ps)

@@ -180,6 +180,7 @@ struct dgpu_ctx {
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
+  bool kb_fused = true;          // DGPU_KB_DEC=separate: norms / inversion / decompression as three kernels (A/B)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
@@ -701,20 +702,28 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
   for (int seg = 0; seg < nseg; ++seg) {
     if (seg > 0) {
       mark(c, s, "eng_fe_chain");
-      if (c->kb_thread)
-        hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
-      else
-        hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
-      HIP_TRY(hipGetLastError());
-      mark(c, s, "eng_fe_kbinv");
-      hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
-                         pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
-                         (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
-      HIP_TRY(hipGetLastError());
+      if (c->kb_thread && c->kb_fused) {
+        // chain + norms + batch inversion + decompression in one kernel (the
+        // norms' prefix products in ebuf's first five planes)
+        hipLaunchKernelGGL(k_kb_chain_dec_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, xbuf, ebuf, flags,
+                           (const uint8_t*)st, c->kb_test_flag);
+        HIP_TRY(hipGetLastError());
+      } else {
+        if (c->kb_thread)
+          hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
+        else
+          hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
+        HIP_TRY(hipGetLastError());
+        mark(c, s, "eng_fe_kbinv");
+        hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
+                           pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
+                           (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
+        HIP_TRY(hipGetLastError());
+      }
     }
     mark(c, s, "eng_fe");
     hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
@@ -1091,6 +1100,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* kcv = getenv("DGPU_KB_CHAIN");
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
+  const char* kdv = getenv("DGPU_KB_DEC");
+  if (kdv && !strcmp(kdv, "separate")) c->kb_fused = false;
   const char* lnv = getenv("DGPU_LINES");
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* gl = getenv("DGPU_G1_LINES");

@@ -112,15 +112,20 @@ DG_NOINL g1j hash_to_g1(const uint32_t msg[8], bool g1dst) { return hash_to_g1_t
 
 // G1 membership of an affine point on E1: (beta x, y) == -[x^2] P (Scott's
 // endomorphism test; same verdict as [r] P == O, tests/test_oracle_g1.py).
-DG_NOINL bool g1_in_subgroup_endo(const g1a& p) {
+DG_FN bool g1_in_subgroup_endo_body(const g1a& p) {
   const g1j t = g1_mul_absx(g1_mul_absx(g1j{p.x, p.y, fp_one()}));
   if (g1_is_inf(t)) return false;
   const fp z2 = fp_sqr(t.z);
   return fp_eq(fp_mul(fp_mul(C_G1_BETA, p.x), z2), t.x) && fp_is_zero(fp_add(fp_mul(p.y, fp_mul(z2, t.z)), t.y));
 }
+DG_NOINL bool g1_in_subgroup_endo(const g1a& p) { return g1_in_subgroup_endo_body(p); }
 
 // 48-byte compressed G1 signature (kilic G1.FromCompressed semantics (R)).
-DG_NOINL int g1_decompress_sig(g1a* out, const uint8_t* in) {
+// The _body form is force-inlined into k_decode_g1_sigs: an out-of-line
+// callee's registers escape the kernel's launch bounds (249 VGPRs + 32 AGPRs,
+// 1 wave/SIMD), inlined the kernel runs at 2 waves/SIMD -- 313.5 -> 229.0 ms
+// per 10M (tools/engbench/dec_g1.hip, profiles/r04/r04c_dec_g1_variants.txt).
+DG_FN int g1_decompress_sig_body(g1a* out, const uint8_t* in) {
   const uint8_t b0 = in[0];
   if (!(b0 & 0x80)) return DEC_ERR_FLAG;
   if (b0 & 0x40) {
@@ -141,8 +146,9 @@ DG_NOINL int g1_decompress_sig(g1a* out, const uint8_t* in) {
   if (fp_std_gt_half(fp_from_mont(y)) != sign) y = fp_neg(y);
   out->x = x;
   out->y = y;
-  return g1_in_subgroup_endo(*out) ? DEC_OK : DEC_ERR_SUBGROUP;
+  return g1_in_subgroup_endo_body(*out) ? DEC_OK : DEC_ERR_SUBGROUP;
 }
+DG_NOINL int g1_decompress_sig(g1a* out, const uint8_t* in) { return g1_decompress_sig_body(out, in); }
 
 #ifndef DG_NO_KERNELS  // (the host-emulation test build takes the device functions only)
 // ---------------------------------------------------------------- kernels
@@ -242,7 +248,7 @@ __global__ void __launch_bounds__(256, 2) k_decode_g1_sigs(size_t n, const uint8
     uint8_t buf[48];
     const uint8_t* src = sigs + i * sig_stride;
     for (int k = 0; k < 48; ++k) buf[k] = src[k];
-    const int rc = g1_decompress_sig(&p, buf);
+    const int rc = g1_decompress_sig_body(&p, buf);
     st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
   }
   st_fp(sig_out, n, i, p.x);

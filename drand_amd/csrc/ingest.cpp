@@ -48,12 +48,18 @@ struct scan_state {
   size_t cap, n;
   int depth;
   bool done;
+  size_t visits;  // page visits left: a well-formed tree visits each page at most once
 };
 
 // -1: malformed file; -2: output full; 0: ok
 int scan_page(scan_state& S, uint64_t pgid) {
   if (S.done) return 0;
   if (++S.depth > 64) return -1;
+  // a crafted branch page pointing back into the tree (itself, an ancestor)
+  // would make the walk exponential: more visits than the file has pages is
+  // a malformed file
+  if (S.visits == 0) return -1;
+  --S.visits;
   if (pgid > (S.file_len - PAGE_HEADER) / S.page_size) return -1;
   const size_t po = (size_t)pgid * S.page_size;
   const uint8_t* p = S.file + po;
@@ -154,8 +160,10 @@ inline bool hex_field(const uint8_t*& p, const uint8_t* end, uint8_t* out, size_
 
 // leaf elements under page pgid (bucket.Stats().KeyN counts every leaf
 // element of the bucket's tree); -1: malformed
-long count_page(const uint8_t* file, size_t file_len, size_t ps, uint64_t pgid, int depth) {
+long count_page(const uint8_t* file, size_t file_len, size_t ps, uint64_t pgid, int depth, size_t& visits) {
   if (depth > 64 || pgid > (file_len - PAGE_HEADER) / ps) return -1;
+  if (visits == 0) return -1;  // more page visits than pages: a cycle (see scan_page)
+  --visits;
   const uint8_t* p = file + (size_t)pgid * ps;
   const uint16_t flags = rd16(p + 8), count = rd16(p + 10);
   if ((size_t)pgid * ps + PAGE_HEADER + (size_t)count * ELEMENT > file_len) return -1;
@@ -163,7 +171,7 @@ long count_page(const uint8_t* file, size_t file_len, size_t ps, uint64_t pgid, 
   if (!(flags & BRANCH_PAGE)) return -1;
   long total = 0;
   for (int i = 0; i < count; ++i) {
-    const long c = count_page(file, file_len, ps, rd64(p + PAGE_HEADER + (size_t)i * ELEMENT + 8), depth + 1);
+    const long c = count_page(file, file_len, ps, rd64(p + PAGE_HEADER + (size_t)i * ELEMENT + 8), depth + 1, visits);
     if (c < 0) return -1;
     total += c;
   }
@@ -178,7 +186,8 @@ extern "C" {
 // Len, :51-62); -1 for a malformed file.
 long dgpu_ingest_count(const uint8_t* file, size_t file_len, size_t page_size, uint64_t root_pgid) {
   if (!file || page_size < 64 || file_len < 2 * page_size) return -1;
-  return count_page(file, file_len, page_size, root_pgid, 0);
+  size_t visits = file_len / page_size;
+  return count_page(file, file_len, page_size, root_pgid, 0, visits);
 }
 
 // In-order walk of a bucket's B+tree (bbolt pages of page_size bytes in the
@@ -194,6 +203,7 @@ long dgpu_ingest_scan(const uint8_t* file, size_t file_len, size_t page_size, ui
   S.file = file;
   S.file_len = file_len;
   S.page_size = page_size;
+  S.visits = file_len / page_size;
   for (int b = 0; b < 8; ++b) {
     S.lo[b] = (uint8_t)(lo >> (56 - 8 * b));
     S.hi[b] = (uint8_t)(hi >> (56 - 8 * b));

@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(64) k_recover_cand(size_t n_rounds, size_t m, 
 // key (-x, y); rec_st combines A with B's identity flag from
 // k_recover_finish (both identity: trivially equal; one: fails).  A
 // candidate index without a table entry (i >= n) sends the round REC_EXACT.
-__global__ void __launch_bounds__(64) k_recover_rlc_g1(size_t n_rounds, int t, int n_group,
+__global__ void __launch_bounds__(64, 2) k_recover_rlc_g1(size_t n_rounds, int t, int n_group,
                                                        const uint32_t* __restrict__ sel,
                                                        const uint32_t* __restrict__ idx,
                                                        const uint64_t* __restrict__ digits,

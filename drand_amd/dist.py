@@ -75,15 +75,18 @@ def verify_rlc_sharded(ctx, code, pk, n, d_rounds, d_sigs, d_sig_len, d_prev, d_
                                         prev_stride, d_prev_len.data_ptr(), seed, root.data_ptr(), s))
     if world > 1:
         roots = torch.empty(world * rb, dtype=torch.uint8, device=dev)
-        stream.synchronize()  # the library's stream and the collective's
+        # device-wide: a NULL stream handle (torch's default stream) makes the
+        # library enqueue on its context's own stream
+        torch.cuda.synchronize(dev)
         if dist.get_backend() == "gloo":  # CPU collectives (tests)
             out = [torch.empty(rb, dtype=torch.uint8) for _ in range(world)]
             dist.all_gather(out, root.cpu())
             roots.copy_(torch.cat(out))
         else:
             dist.all_gather_into_tensor(roots, root)
-        torch.cuda.current_stream(dev).synchronize()
+        torch.cuda.synchronize(dev)
     else:
         roots = root
     _lib.check(lib.dgpu_rlc_finish_device(ctx.handle, world, roots.data_ptr(), d_bits.data_ptr(),
                                           None if d_reason is None else d_reason.data_ptr(), s))
+    torch.cuda.synchronize(dev)  # the verdicts are final (whatever stream the library ran on)

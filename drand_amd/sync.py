@@ -195,7 +195,9 @@ def _check_past_records(store, verifier, pubkey, up_to, n, cb, window, cancelled
     import numpy as np
     from concurrent.futures import ThreadPoolExecutor
     from .ingest import window_records
-    end = min(n, up_to + 1)  # visited rounds: [1, end)
+    # visited rounds: [1, end) -- round 1 always (the loop tests i >= upTo only
+    # after checking round i, sync_manager.go:188-221), so up_to = 0 checks it too
+    end = min(n, max(up_to, 1) + 1)
     if end <= 1:
         return None
     bounds = [(lo, min(end, lo + window)) for lo in range(1, end, window)]

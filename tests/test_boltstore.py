@@ -97,7 +97,7 @@ def test_check_past_beacons_from_bolt(tmp_path, window):
     p = tmp_path / "drand.db"
     write_bolt(p, _kv(st))
     bs = BoltStore(p)
-    for up_to in (1, 350, 10 ** 9):
+    for up_to in (0, 1, 350, 10 ** 9):  # 0: round 1 is still checked (the loop breaks after it)
         c1, c2 = [], []
         got = check_past_beacons(bs, MarkerVerifier(), b"pk", up_to, cb=lambda i, u: c1.append((i, u)), window=window)
         mem = check_past_beacons(st, MarkerVerifier(), b"pk", up_to, cb=lambda i, u: c2.append((i, u)), window=window)
@@ -161,13 +161,19 @@ def test_torn_meta0_opens_from_meta1(tmp_path):
     bs = BoltStore(p)
     assert bs.txid == 1 and bs.last() == st.last() and bs.len() == st.len()
     bs.close()
-    # a 16 KiB-page file whose meta 0 is torn still opens (meta 1 at 16384)
+    # a 16 KiB-page file whose meta 0 is torn: bbolt v1.3.4 looks for meta 1
+    # one OS page in only and refuses it; the opt-in lenient mode
+    # (a documented deviation) also probes 16 KiB and opens it
     q = tmp_path / "big.db"
     write_bolt(q, _kv(st), page_size=16384)
     raw = bytearray(q.read_bytes())
     raw[16 + 40] ^= 1
     q.write_bytes(bytes(raw))
-    bq = BoltStore(q)
+    import mmap
+    if mmap.PAGESIZE != 16384:
+        with pytest.raises(BoltFormatError):
+            BoltStore(q)
+    bq = BoltStore(q, lenient_page_size=True)
     assert bq.txid == 1 and bq.page_size == 16384 and bq.last() == st.last()
     bq.close()
 
@@ -258,3 +264,28 @@ def test_native_scan_equals_python_scan(tmp_path):
         assert rr.tolist() == [r for r, _ in want]
         assert [bytes(buf[o:o + n]) for o, n in zip(off, ln)] == [v for _, v in want]
     bs.close()
+
+
+@pytest.mark.timeout(60)
+def test_native_walk_rejects_self_referencing_branch_page():
+    """A crafted branch page whose 254 children all point back to itself (a
+    cycle, never produced by bbolt) must be rejected as malformed by the
+    native walk and count instead of taking 254^64 steps: the
+    walk stops after as many page visits as the file has pages."""
+    import numpy as np
+    from drand_amd import ingest
+    ps, pg = 4096, 2
+    f = bytearray(3 * ps)
+    count = 254
+    base = pg * ps
+    struct.pack_into("<QHHI", f, base, pg, 0x01, count, 0)  # branch page, no overflow
+    key_off = base + 16 + count * 16  # one 8-byte key shared by every element
+    struct.pack_into(">Q", f, key_off, 1)
+    for i in range(count):
+        e = base + 16 + 16 * i
+        struct.pack_into("<IIQ", f, e, key_off - e, 8, pg)  # pos, ksize, child = this page
+    buf = np.frombuffer(bytes(f), dtype=np.uint8)
+    with pytest.raises(BoltFormatError):
+        ingest.scan(buf, ps, pg, 0, 1 << 16)
+    with pytest.raises(BoltFormatError):
+        ingest.count(buf, ps, pg)

@@ -46,7 +46,7 @@ def _rank(rank, world, port, code, seed, rate, q):
         stream = torch.cuda.current_stream(dev)
         verify_rlc_sharded(ctx, code, np.frombuffer(c.pk, dtype=np.uint8).copy(), n, d_rounds, d_sigs, d_sig_len,
                            d_prev, d_prev_len, 1000 + 17 * rank, d_bits, stream, world, rank, d_reason=d_reason)
-        stream.synchronize()
+        torch.cuda.synchronize()
         bits = gather_verdict_bits(d_bits.cpu(), n, N, world, rank)
         reasons = [None] * world
         dist.all_gather_object(reasons, d_reason.cpu().numpy()[:n].tolist())

@@ -76,6 +76,15 @@ struct DevBuf {
 
 inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
+// SplitMix64 step on the host: independent RLC seeds derived from a call's
+// seed (per device of dgpu_verify_multi, the confirmation check)
+uint64_t splitmix_host(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
 // signatures on G1 / public key on G2 (bls-unchained-on-g1, bls-unchained-g1-rfc9380)
 inline bool sig_on_g1(int scheme) { return scheme == DGPU_SCHEME_UNCHAINED_G1 || scheme == DGPU_SCHEME_G1_RFC9380; }
 inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && scheme <= DGPU_SCHEME_G1_RFC9380; }
@@ -181,6 +190,7 @@ struct dgpu_ctx {
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
   bool kb_fused = true;          // DGPU_KB_DEC=separate: norms / inversion / decompression as three kernels (A/B)
+  bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
@@ -478,7 +488,7 @@ int rlc_points_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s) {
 // RLC root by bucket MSM (rlc_msm.cuh) into root (P then S, stride-1
 // Jacobian of the signature group).  Asynchronous on s.
 template <class Gr>
-int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root) {
+int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root, const char* stage) {
   using M = GrMem<Gr>;
   const unsigned B = 256;
   const size_t n = a.n;
@@ -495,7 +505,7 @@ int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* r
   uint32_t* offsets = counts + MSM_KEYS;
   uint32_t* cursor = offsets + MSM_KEYS;
   uint32_t* list = (uint32_t*)c->msm_list.p;
-  mark(c, s, "rlc_root_msm");
+  mark(c, s, stage);
   hipLaunchKernelGGL(k_msm_aos<Gr>, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)rlc_rpts(c, n, M::JAC),
                      (const uint32_t*)c->sig_pts.p, (const uint8_t*)c->status.p, aos, flags);
   HIP_TRY(hipGetLastError());
@@ -530,15 +540,17 @@ int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* r
   return DGPU_OK;
 }
 
-int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root) {
-  return sig_on_g1(a.scheme) ? rlc_root_msm_t<G1Ops>(c, a, s, root) : rlc_root_msm_t<G2Ops>(c, a, s, root);
+int rlc_root_msm_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* root,
+                        const char* stage = "rlc_root_msm") {
+  return sig_on_g1(a.scheme) ? rlc_root_msm_t<G1Ops>(c, a, s, root, stage)
+                             : rlc_root_msm_t<G2Ops>(c, a, s, root, stage);
 }
 
 // The segment trees of one RLC batch (leaves P_i = r_i R_i, S_i = r_i sig_i,
 // r_i from the seed and the batch position i; then sums up to the root),
 // built from rlc_points_locked's points.  Asynchronous on s.
 template <class Gr>
-int rlc_tree_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
+int rlc_tree_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T, bool plain) {
   using M = GrMem<Gr>;
   const unsigned B = 256;
   const size_t n = a.n;
@@ -554,10 +566,15 @@ int rlc_tree_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
     T.S[l] = tree + off;
     off += T.sz[l] * M::JAC;
   }
-  mark(c, s, "rlc_leaves_tree");
-  hipLaunchKernelGGL(k_rlc_leaves<Gr>, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed,
-                     (const uint32_t*)rlc_rpts(c, n, M::JAC), (const uint32_t*)c->sig_pts.p,
-                     (const uint8_t*)c->status.p, T.P[0], T.S[0]);
+  mark(c, s, plain ? "rlc_plain_tree" : "rlc_leaves_tree");
+  if (plain)
+    hipLaunchKernelGGL(k_rlc_leaves_plain<Gr>, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n,
+                       (const uint32_t*)rlc_rpts(c, n, M::JAC), (const uint32_t*)c->sig_pts.p,
+                       (const uint8_t*)c->status.p, T.P[0], T.S[0]);
+  else
+    hipLaunchKernelGGL(k_rlc_leaves<Gr>, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, a.seed,
+                       (const uint32_t*)rlc_rpts(c, n, M::JAC), (const uint32_t*)c->sig_pts.p,
+                       (const uint8_t*)c->status.p, T.P[0], T.S[0]);
   HIP_TRY(hipGetLastError());
   for (size_t l = 0; l + 1 < T.sz.size(); ++l) {
     hipLaunchKernelGGL(k_rlc_level<Gr>, dim3(grid_for(2 * T.sz[l + 1], B)), dim3(B), 0, s, T.sz[l], T.P[l], T.S[l],
@@ -567,8 +584,8 @@ int rlc_tree_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
   return DGPU_OK;
 }
 
-int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T) {
-  return sig_on_g1(a.scheme) ? rlc_tree_t<G1Ops>(c, a, s, T) : rlc_tree_t<G2Ops>(c, a, s, T);
+int rlc_tree_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s, rlc_trees& T, bool plain = false) {
+  return sig_on_g1(a.scheme) ? rlc_tree_t<G1Ops>(c, a, s, T, plain) : rlc_tree_t<G2Ops>(c, a, s, T, plain);
 }
 
 // The identity (Z = 0) of the signature group as a stride-1 Jacobian point
@@ -677,6 +694,41 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
     l = nl;
   }
   return DGPU_OK;
+}
+
+// RLC phase 2 when a root containing this shard failed: exact per-round
+// verdicts (DESIGN.md 2c "localize, then confirm").
+//  1. Localize on the tree of plain sums (coefficients 1, k_rlc_leaves_plain):
+//     its leaves cost nothing (the points themselves) and a leaf check is the
+//     round's own pairing check, so every round it marks ST_PAIRING is
+//     exactly invalid.  Bad rounds can hide only in an internal node whose
+//     errors cancel in the plain sum (crafted input).
+//  2. Confirm the rest: a fresh random combination (bucket MSM over the
+//     rounds still ST_OK, seed derived from the call's seed) and one check.
+//     It passes for a correct localization; then every remaining round is
+//     valid except with probability 2^-64 -- the soundness of the root.
+//  3. Only if the confirmation fails: the random-coefficient tree (leaves
+//     [a] R + [b] endo(R)) over what is left, descended as before.
+// The shard's own root is checked first unless it is known failing
+// (root_failed: the node's root was this shard's).
+int rlc_resolve_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s, bool root_failed) {
+  int rc;
+  rlc_trees T;
+  if (c->rlc_localize) {
+    if ((rc = rlc_tree_locked(c, a, s, T, true)) || (rc = rlc_descend_locked(c, key, T, s, root_failed))) return rc;
+    const int jw = rlc_geom_of(sig_on_g1(a.scheme)).jw;
+    verify_args a2 = a;
+    a2.seed = splitmix_host(a.seed ^ 0xC0F1A7ull);
+    if ((rc = c->rlc_root.ensure(2 * (size_t)jw * 4))) return rc;
+    uint32_t* root = (uint32_t*)c->rlc_root.p;
+    if ((rc = rlc_root_msm_locked(c, a2, s, root, "rlc_confirm"))) return rc;
+    std::vector<uint8_t> fail;
+    if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, root, root + jw, s, &fail))) return rc;
+    if (!fail[0]) return DGPU_OK;
+    root_failed = false;  // the random tree's root is another combination
+  }
+  if ((rc = rlc_tree_locked(c, a, s, T))) return rc;
+  return rlc_descend_locked(c, key, T, s, root_failed);
 }
 
 // Karabina final exponentiation of one chunk (pairing_engine.cuh, DESIGN.md
@@ -936,9 +988,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
       }
       return DGPU_OK;
     }
-    rlc_trees T;
-    if ((rc = rlc_tree_locked(c, a, s, T))) return rc;
-    return rlc_descend_locked(c, key, T, s, true);
+    return rlc_resolve_locked(c, key, a, s, true);
   }
   if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
   const uint32_t* consts = (const uint32_t*)key->consts.p;
@@ -1100,6 +1150,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* kcv = getenv("DGPU_KB_CHAIN");
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
+  const char* rlv = getenv("DGPU_RLC_LOCALIZE");
+  if (rlv && !strcmp(rlv, "0")) c->rlc_localize = false;
   const char* kdv = getenv("DGPU_KB_DEC");
   if (kdv && !strcmp(kdv, "separate")) c->kb_fused = false;
   const char* lnv = getenv("DGPU_LINES");
@@ -1311,10 +1363,8 @@ int dgpu_rlc_finish_device(dgpu_ctx* c, size_t n_roots, const uint8_t* d_roots, 
   std::vector<uint8_t> fail;
   if ((rc = rlc_check_locked(c, k, std::vector<uint32_t>{0}, 1, sum, sum + G.jw, s, &fail))) return rc;
   if (a.n == 0) return DGPU_OK;
-  if (fail[0]) {  // this shard's tree, its own root first unless it is the node's (one root)
-    rlc_trees T;
-    if ((rc = rlc_tree_locked(c, a, s, T)) || (rc = rlc_descend_locked(c, k, T, s, n_roots == 1))) return rc;
-  }
+  // this shard's verdicts, its own root first unless it is the node's (one root)
+  if (fail[0] && (rc = rlc_resolve_locked(c, k, a, s, n_roots == 1))) return rc;
   const uint8_t* st = (const uint8_t*)c->status.p;
   mark(c, s, "pack_verdicts");
   hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((a.n + 7) / 8, 256)), dim3(256), 0, s, a.n, st, d_bits);

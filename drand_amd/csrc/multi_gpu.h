@@ -69,13 +69,6 @@ struct multi_bufs {
   DevBuf bits, reasons, all_bits, all_reasons, root, all_roots;
 };
 
-uint64_t splitmix_host(uint64_t x) {
-  uint64_t z = x + 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
 }  // namespace
 
 struct dgpu_multi {
@@ -272,7 +265,6 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
   const bool rlc = mode == DGPU_MODE_RLC;
   const bool g1 = sig_on_g1(scheme);
   const int jw = g1 ? G1J_WORDS : G2J_WORDS;  // root: P, S (stride-1 Jacobian of the signature group)
-  std::vector<rlc_trees> trees(D);
   // phase 1: stage the shard, then per-round verification (or the RLC trees)
   rc = for_each_device(m, [&](int k) -> int {
     dgpu_ctx* c = m->ctx[k];
@@ -338,10 +330,8 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
       const size_t cnt = args[k].n;
       if (cnt == 0) return DGPU_OK;
       int r;
-      if (!all_ok) {  // this shard's tree, its own root first (D = 1: that root is the node's, known failing)
-        if ((r = rlc_tree_locked(c, args[k], c->stream, trees[k]))) return r;
-        if ((r = rlc_descend_locked(c, keys[k], trees[k], c->stream, D == 1))) return r;
-      }
+      // this shard's verdicts, its own root first (D = 1: that root is the node's, known failing)
+      if (!all_ok && (r = rlc_resolve_locked(c, keys[k], args[k], c->stream, D == 1))) return r;
       return pack_shard_locked(c, cnt, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, c->stream);
     });
     if (rc) return rc;

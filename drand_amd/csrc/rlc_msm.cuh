@@ -309,6 +309,30 @@ __global__ void __launch_bounds__(256, 2) k_rlc_leaves(size_t n, uint64_t seed, 
   M::st_jac(sig ? s_out : p_out, n, i, acc);
 }
 
+// Leaves of the localization tree (coefficients 1): P_i = R_i, S_i = sig_i
+// as Jacobian points (infinity for rounds whose verdict is already final).
+// A leaf check of this tree is the round's own pairing check (exact); an
+// internal node can only hide bad rounds whose errors cancel in a plain sum,
+// which the confirmation check with fresh random coefficients catches
+// (capi.hip rlc_resolve_locked).
+template <class Gr>
+__global__ void __launch_bounds__(256) k_rlc_leaves_plain(size_t n, const uint32_t* __restrict__ r_aff,
+                                                          const uint32_t* __restrict__ sig_pts,
+                                                          const uint8_t* __restrict__ status,
+                                                          uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
+  using M = GrMem<Gr>;
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const bool sig = j >= n;
+  const size_t i = sig ? j - n : j;
+  typename Gr::jac acc = Gr::inf();
+  if (status[i] == ST_OK) {
+    const typename Gr::aff q = M::ld_aff(sig ? sig_pts : r_aff, n, i);
+    if (!Gr::aff_is_zero(q)) acc = Gr::from_aff(q);
+  }
+  M::st_jac(sig ? s_out : p_out, n, i, acc);
+}
+
 // One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied); 2 n_out
 // threads, the first n_out on the P tree, the rest on the S tree.
 template <class Gr>

@@ -145,6 +145,51 @@ def test_rlc_duplicate_rounds_cannot_cancel(gpu_ctx):
         assert v.verify_reasons(beacons, c.pk, _lib.MODE_RLC, seed).tolist() == expect
 
 
+def test_rlc_localize_then_confirm_and_fallback(gpu_ctx):
+    """A failing RLC root is resolved on the tree of plain sums (leaf checks
+    are the rounds' own pairings), then the rest is confirmed with a fresh
+    random combination (capi.hip rlc_resolve_locked).  Ordinary corruption:
+    the confirmation passes and the random-coefficient leaves are never
+    built.  Errors crafted to cancel in a plain sum (sig + D, sig - D under
+    one node) slip past the localization: the confirmation fails and the
+    random-coefficient tree finds them -- verdicts equal per-round mode either
+    way."""
+    from drand_amd import _lib
+    from drand_amd.chain import Beacon, Verifier
+    from drand_amd.synth import corrupt, make_chain
+    v = Verifier(_sch("pedersen-bls-chained"))
+    lib = v.ctx.lib
+
+    def rlc_stages(beacons, pk):
+        _lib.check(lib.dgpu_set_profiling(v.ctx.handle, 1))
+        try:
+            got = v.verify_reasons(beacons, pk, _lib.MODE_RLC)
+            return got, set(_lib.stage_times(v.ctx))
+        finally:
+            _lib.check(lib.dgpu_set_profiling(v.ctx.handle, 0))
+
+    c = make_chain(45, 4000, _lib.SCHEME_CHAINED, seg_len=64)
+    corrupt(c, 45, rate=3e-3)
+    beacons = [c.beacon(i) for i in range(len(c))]
+    per = v.verify_reasons(beacons, c.pk)
+    got, st = rlc_stages(beacons, c.pk)
+    assert got.tolist() == per.tolist()
+    assert {"rlc_plain_tree", "rlc_confirm"} <= st and "rlc_leaves_tree" not in st, st
+    # +D / -D in rounds 137 and 138: one level-5 node of the plain tree, the
+    # first level the descent checks for a batch above 64Ki rounds
+    c2 = make_chain(46, 70000, _lib.SCHEME_CHAINED, seg_len=64)
+    b2 = [c2.beacon(i) for i in range(len(c2))]
+    s = B.g2_decompress(b2[137].signature)
+    s2 = B.g2_decompress(b2[138].signature)
+    b2[137] = Beacon(b2[137].previous_sig, b2[137].round, B.g2_compress(B.g2_add(s, B.G2_GEN)))
+    b2[138] = Beacon(b2[138].previous_sig, b2[138].round, B.g2_compress(B.g2_add(s2, B.g2_neg(B.G2_GEN))))
+    per2 = v.verify_reasons(b2, c2.pk)
+    assert per2[137] == per2[138] == _lib.REASON_PAIRING
+    got2, st2 = rlc_stages(b2, c2.pk)
+    assert got2.tolist() == per2.tolist()
+    assert {"rlc_plain_tree", "rlc_confirm", "rlc_leaves_tree"} <= st2, st2
+
+
 def test_rlc_root_first_clean_and_single_bad(gpu_ctx):
     """A clean batch passes with the root check alone; one bad round among
     70k is found (descent from the root) -- verdicts equal per-round mode."""

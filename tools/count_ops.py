@@ -84,6 +84,10 @@ def main():
     # (phi split) + the affine conversion of R + two tree nodes
     kernels["rlc_hash_to_g1_raw"] = ent((1, "rlc_hash_g1"))
     kernels["rlc_leaves_tree_g1"] = ent((2, "leaf_g1"), (1, "g1_affine"), (2, "node_g1"))
+    # the localization tree of plain sums (rlc_resolve_locked): leaves are the
+    # points themselves, about two node additions per round
+    kernels["rlc_plain_tree"] = ent((2, "node"))
+    kernels["rlc_plain_tree_g1"] = ent((2, "node_g1"))
     # group-law ops: the recovery MSM's work figure is composed from these
     go = (ctypes.c_ulonglong * 14)()
     assert L.hs_count_group_ops(msg, go) == 0

@@ -226,12 +226,6 @@ def roofline_for(stage_ms, items, pipeline="g2", stage_items=None, extra_work=No
     if "eng_fe_chain" in stage_ms and "eng_fe" in wmap:
         wmap.update(KB_STAGE_WORK)
     work = dict(hash_work(), **engine_work())
-    # the fused chain kernel (default: no separate eng_fe_kbinv stage) does the
-    # chains and the decompression side in one launch
-    if "eng_fe_chain" in stage_ms and "eng_fe_kbinv" not in stage_ms and wmap.get("eng_fe_chain") == "k_kb_chain_thr":
-        if "k_kb_chain_thr" in work and "k_kb_dec_fused" in work:
-            wmap["eng_fe_chain"] = "k_kb_chain_dec_thr"
-            work["k_kb_chain_dec_thr"] = {"mads": work["k_kb_chain_thr"]["mads"] + work["k_kb_dec_fused"]["mads"]}
     work.update(extra_work or {})
     have = {s: t for s, t in stage_ms.items() if s in wmap and wmap[s] in work and t > 0}
     if not have:

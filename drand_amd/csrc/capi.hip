@@ -189,8 +189,8 @@ struct dgpu_ctx {
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
-  bool kb_fused = true;          // DGPU_KB_DEC=separate: norms / inversion / decompression as three kernels (A/B)
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
+  int rlc_descent_step = 5;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
@@ -474,8 +474,8 @@ int rlc_points_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s) {
     HIP_TRY(hipGetLastError());
   }
   mark(c, s, "decode_g2");
-  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
-                     1, sg, st);
+  hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len,
+                     a.m, sg, st);
   HIP_TRY(hipGetLastError());
   mark(c, s, "rlc_affine");
   // R_i to affine in place (X, Y slots; Z follows them in the Jacobian SoA)
@@ -644,13 +644,14 @@ int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32
 
 // RLC phase 2, root first: the whole batch is one node check (one final
 // exponentiation) when every round is valid.  Otherwise the wide descent:
-// check every node of the level with <= 64Ki nodes (a multiple of D = 5 levels
+// check every node of the level with <= 64Ki nodes (a multiple of D levels,
+// DGPU_RLC_DESCENT_STEP, default 5,
 // up from the leaves), then all descendants D levels down of each failing
 // node, to the leaves; a failing leaf is an invalid round (ST_PAIRING).
 int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hipStream_t s,
                        bool root_failed = false) {
   const unsigned B = 256;
-  const int D = 5;
+  const int D = c->rlc_descent_step;
   const int top = T.top();
   uint8_t* st = (uint8_t*)c->status.p;
   std::vector<uint8_t> fail;
@@ -754,28 +755,20 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
   for (int seg = 0; seg < nseg; ++seg) {
     if (seg > 0) {
       mark(c, s, "eng_fe_chain");
-      if (c->kb_thread && c->kb_fused) {
-        // chain + norms + batch inversion + decompression in one kernel (the
-        // norms' prefix products in ebuf's first five planes)
-        hipLaunchKernelGGL(k_kb_chain_dec_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, xbuf, ebuf, flags,
-                           (const uint8_t*)st, c->kb_test_flag);
-        HIP_TRY(hipGetLastError());
-      } else {
-        if (c->kb_thread)
-          hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
-        else
-          hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
-        HIP_TRY(hipGetLastError());
-        mark(c, s, "eng_fe_kbinv");
-        hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
-                           pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
-                           (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
-        HIP_TRY(hipGetLastError());
-      }
+      if (c->kb_thread)
+        hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
+      else
+        hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
+      HIP_TRY(hipGetLastError());
+      mark(c, s, "eng_fe_kbinv");
+      hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
+                         pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
+                         (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
+      HIP_TRY(hipGetLastError());
     }
     mark(c, s, "eng_fe");
     hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
@@ -919,8 +912,12 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   HIP_TRY(hipGetLastError());
   mark(c, s, "decode_g2");
   // membership of the signature: checked by the lines kernel (eng_pairing_locked sig_subgroup)
-  hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m,
-                     c->decode_subgroup ? 1 : 0, sg, st);
+  if (c->decode_subgroup)
+    hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m, sg,
+                       st);
+  else
+    hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m, 0, sg,
+                       st);
   HIP_TRY(hipGetLastError());
   return DGPU_OK;
 }
@@ -1150,10 +1147,10 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* kcv = getenv("DGPU_KB_CHAIN");
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
+  const char* rds = getenv("DGPU_RLC_DESCENT_STEP");
+  if (rds && atoi(rds) >= 1 && atoi(rds) <= 8) c->rlc_descent_step = atoi(rds);
   const char* rlv = getenv("DGPU_RLC_LOCALIZE");
   if (rlv && !strcmp(rlv, "0")) c->rlc_localize = false;
-  const char* kdv = getenv("DGPU_KB_DEC");
-  if (kdv && !strcmp(kdv, "separate")) c->kb_fused = false;
   const char* lnv = getenv("DGPU_LINES");
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* gl = getenv("DGPU_G1_LINES");

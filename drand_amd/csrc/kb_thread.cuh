@@ -117,117 +117,5 @@ __global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt,
                });
 }
 
-// Fused exponentiation side, one thread per round: the compressed chain of
-// k_kb_chain_thr, then -- inside the same kernel -- the norms N_j =
-// Norm(4 f1_j) of the six stored values (formed in registers at each snap,
-// their prefix products to `pre` ([j][limb][cnt], j < 5)), the batch
-// inversion of the products P_i = N_0 ... N_5 (Montgomery's trick per wave:
-// lane 0 runs the wave's 64 products through LDS with one Fp inversion), and
-// the decompression of each stored value (f0, f3; engine.cuh
-// eng_kb_decompress) with 1/N_j = P^-1 prefix_(j-1) prod_(k>j) N_k taken
-// backwards.  Replaces k_eng_kb_norm -> k_eng_inv -> k_eng_kb_dec, which
-// re-read the stored values and the norms' products from HBM (DGPU_KB_DEC=
-// separate keeps them, A/B).  A zero norm (f1 = 0) flags the item for the
-// Granger-Scott fallback unless it has already failed (k_eng_kb_norm's rule);
-// flagged items are not decompressed.  flag_every: DGPU_KB_TEST_FLAG.
-#ifndef DG_KB_FUSED_OCC
-#define DG_KB_FUSED_OCC 2
-#endif
-__global__ void __launch_bounds__(256, DG_KB_FUSED_OCC) k_kb_chain_dec_thr(size_t cnt, size_t r0,
-                                                                          uint32_t* __restrict__ xbuf,
-                                                                          uint32_t* __restrict__ pre,
-                                                                          uint8_t* __restrict__ flags,
-                                                                          const uint8_t* __restrict__ status,
-                                                                          size_t flag_every) {
-  __shared__ uint32_t sP[FP_LIMBS * 256];  // [limb][thread]: P_i, then 1 / P_i
-  __shared__ uint32_t sT[FP_LIMBS * 256];  // [limb][thread]: prefix products within the wave
-  const int tid = threadIdx.x, wbase = tid & ~63;
-  const size_t i = (size_t)blockIdx.x * blockDim.x + tid;
-  const bool valid = i < cnt;
-  auto ld = [&](int plane, int comp) {
-    const uint32_t* b = xbuf + kb_off(i, plane, comp);
-    fp2 v;
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) {
-      const uint2 w = *reinterpret_cast<const uint2*>(b + l * ENG_WAVE_WORDS);
-      v.c0.l[l] = w.x, v.c1.l[l] = w.y;
-    }
-    return v;
-  };
-  auto st = [&](int plane, int comp, const fp2& v) {
-    uint32_t* b = xbuf + kb_off(i, plane, comp);
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) *reinterpret_cast<uint2*>(b + l * ENG_WAVE_WORDS) = make_uint2(v.c0.l[l], v.c1.l[l]);
-  };
-  auto lds_ld = [](const uint32_t* a, int t) {
-    fp v;
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) v.l[l] = a[l * 256 + t];
-    return v;
-  };
-  auto lds_st = [](uint32_t* a, int t, const fp& v) {
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) a[l * 256 + t] = v.l[l];
-  };
-  fp acc = fp_one();
-  bool zero = false;
-  if (valid) {
-    zero = flag_every && i % flag_every == 0;
-    kb_chain_thr(ld(ENG_KB_PL_M, 2), ld(ENG_KB_PL_M, 4), ld(ENG_KB_PL_M, 8), ld(ENG_KB_PL_M, 10),
-                 [&](int j, const fp2& f1, const fp2& f2, const fp2& f4, const fp2& f5) {
-                   const int pl = ENG_KB_PL_X0 + j;
-                   st(pl, 2, f1);
-                   st(pl, 4, f2);
-                   st(pl, 8, f4);
-                   st(pl, 10, f5);
-                   fp nj = eng_kb_norm(f1);
-                   if (fp_is_zero(nj)) {
-                     nj = fp_one();
-                     zero = true;
-                   }
-                   acc = j ? fp_mul(acc, nj) : nj;
-                   if (j < ENG_KB_NSNAP - 1) st_soa(pre + (size_t)j * FP_LIMBS * cnt, cnt, i, acc);
-                 });
-  }
-  lds_st(sP, tid, acc);  // inactive lanes contribute 1
-  __syncthreads();
-  if ((tid & 63) == 0) {  // the wave's 64 products: prefix, one inversion, backward
-    fp t = lds_ld(sP, wbase);
-    lds_st(sT, wbase, t);
-#pragma unroll 1
-    for (int k = 1; k < 64; ++k) {
-      t = fp_mul(t, lds_ld(sP, wbase + k));
-      lds_st(sT, wbase + k, t);
-    }
-    fp inv = fp_inv(t);
-#pragma unroll 1
-    for (int k = 63; k > 0; --k) {
-      const fp pk = lds_ld(sP, wbase + k);
-      lds_st(sP, wbase + k, fp_mul(inv, lds_ld(sT, wbase + k - 1)));
-      inv = fp_mul(inv, pk);
-    }
-    lds_st(sP, wbase, inv);
-  }
-  __syncthreads();
-  if (!valid) return;
-  if (zero) {
-    if (status[r0 + i] == ST_OK) flags[i] = 1;
-    return;
-  }
-  if (flags[i]) return;  // flagged at an earlier exponentiation: the fallback recomputes it
-  fp pinv = lds_ld(sP, tid);  // 1 / (N_0 ... N_5); after value j: 1 / (N_0 ... N_(j-1))
-#pragma unroll 1
-  for (int j = ENG_KB_NSNAP - 1; j >= 0; --j) {
-    const int pl = ENG_KB_PL_X0 + j;
-    const fp2 f1 = ld(pl, 2);
-    const fp ninv = j ? fp_mul(pinv, ld_soa(pre + (size_t)(j - 1) * FP_LIMBS * cnt, cnt, i)) : pinv;
-    if (j) pinv = fp_mul(pinv, eng_kb_norm(f1));
-    fp2 f0, f3;
-    eng_kb_decompress(f1, ld(pl, 4), ld(pl, 8), ld(pl, 10), ninv, f0, f3);
-    st(pl, 0, f0);
-    st(pl, 6, f3);
-  }
-}
-
 }  // namespace dgpu
 #endif

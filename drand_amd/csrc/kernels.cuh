@@ -260,6 +260,33 @@ __global__ void __launch_bounds__(256, 4) k_decode_g2_sigs(size_t n, const uint8
   status[i] = st;
 }
 
+// The same decode with the G2 membership check (RLC mode and recovery need
+// it up front; DGPU_SUBGROUP=decode): the 63-doubling ladder inlined into
+// the kernel at 2 waves/SIMD -- out of line in g2_decompress its registers
+// escaped the kernel's budget (4.6 KB of scratch at 4 waves/SIMD): 389.6 ->
+// 360.2 ms per 10M (tools/engbench/dec_g2.hip, profiles/r04/r04f_dec_g2_variants.txt).
+__global__ void __launch_bounds__(256, 2) k_decode_g2_sigs_sub(size_t n, const uint8_t* __restrict__ sigs,
+                                                             size_t sig_stride, const uint32_t* __restrict__ sig_len,
+                                                             msg_src m, uint32_t* __restrict__ sig_out,
+                                                             uint8_t* __restrict__ status) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t st;
+  g2a p{fp2_zero(), fp2_zero()};
+  if (sig_len[i] != 96 || msg_bad_record(m, i)) {
+    st = ST_DECODE;
+  } else {
+    uint8_t buf[96];
+    const uint8_t* src = sigs + i * sig_stride;
+    for (int k = 0; k < 96; ++k) buf[k] = src[k];
+    int rc = g2_decompress(&p, buf, false);
+    if (rc == DEC_OK && !g2_in_subgroup(g2_from_affine(p))) rc = DEC_ERR_SUBGROUP;
+    st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
+  }
+  st_g2a(sig_out, n, i, p);
+  status[i] = st;
+}
+
 // Synthetic-chain generator (test-data tool, not the verify path): one step
 // of S independent chained segments, following the reference's fixture
 // generator client/test/result/mock/result.go:86-130 (msg = DigestMessage,

@@ -51,21 +51,6 @@ def test_rlc_node_check_stages_not_priced_per_round(monkeypatch):
     assert not any(s.startswith("eng_") for s in r["stage_frac"])
 
 
-def test_fused_chain_stage_priced_with_decompression(monkeypatch):
-    """The fused Karabina kernel (k_kb_chain_dec_thr, default: no separate
-    eng_fe_kbinv stage) is priced as the chains plus the decompression side;
-    with DGPU_KB_DEC=separate the two stages keep their own figures."""
-    b = _bench(monkeypatch)
-    st = dict(_stages())
-    del st["eng_fe_kbinv"]
-    r = b.roofline_for(st, 10_000_000)
-    work = dict(b.hash_work(), **b.engine_work())
-    want = 10_000_000 * (work["k_kb_chain_thr"]["mads"] + work["k_kb_dec_fused"]["mads"]) / (st["eng_fe_chain"] * 1e-3)
-    assert abs(r["stage_frac"]["eng_fe_chain"] - want / b.PEAK_MAD_U64_PER_S) < 1e-9
-    r2 = b.roofline_for(_stages(), 10_000_000)
-    assert r2["stage_frac"]["eng_fe_chain"] < r["stage_frac"]["eng_fe_chain"]
-
-
 def test_g1_rlc_pipeline_priced(monkeypatch):
     """RLC for G1 signatures prices its own stages (raw G1 hash, G1 decode,
     G1 MSM root, G1 leaves + tree)."""

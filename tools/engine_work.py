@@ -79,14 +79,6 @@ def main():
     kern["k_eng_kb_inv"] = {"mads": n_exp * (norm + inv + dec), "per_exponentiation": {
         "k_eng_kb_norm": norm, "k_eng_inv": inv, "k_eng_kb_dec": dec}}
     kern["k_eng_fe_karabina"] = {"mads": seg_work["mads"] + chain["mads"] + kern["k_eng_kb_inv"]["mads"]}
-    # the fused per-thread form (kb_thread.cuh k_kb_chain_dec_thr): the same
-    # norms (formed at the snaps) and decompression, the products inverted per
-    # wave of 64 (3 mul + an inversion / 64); bench adds the chain's own
-    # squarings (op_counts k_kb_chain_thr)
-    inv_w = 3 * MUL + (82 * MUL + 380 * SQR) // 64
-    dec_back = (ns - 1) * (2 * MUL + 2 * SQR) + ns * 17 * MUL
-    kern["k_kb_dec_fused"] = {"mads": n_exp * (norm + inv_w + dec_back), "per_exponentiation": {
-        "norms": norm, "inversion_per_wave": inv_w, "decompression": dec_back}}
     # on-G1 schemes: the Miller program with every line formed at its LDLINE
     # from the key's fixed table, 8 of the 12 exports scaled by one Fp
     # multiplication (a P coordinate): 68 line steps x 8 x 392 mads more

@@ -147,12 +147,11 @@ STAGE_WORK = {
     # RLC: the per-round stages only (node checks are data-dependent: 1 at 0% corruption)
     "rlc": {"rlc_hash_to_g2_raw": "rlc_hash_to_g2_raw", "decode_g2": "k_decode_g2_sigs+subgroup",
             "rlc_affine": "k_g2_batch_affine", "rlc_root_msm": "rlc_root_msm", "rlc_leaves_tree": "rlc_leaves_tree",
-            "rlc_plain_tree": "rlc_plain_tree", "rlc_confirm": "rlc_root_msm"},
+            "rlc_plain_tree": "rlc_plain_tree"},
     # RLC for the G1-signature schemes (configs[3]'s per-GPU fold)
     "rlc_g1": {"rlc_hash_to_g1_raw": "rlc_hash_to_g1_raw", "decode_g1": "k_decode_g1_sigs",
                "rlc_affine": "k_g1_batch_affine", "rlc_root_msm": "rlc_root_msm_g1",
-               "rlc_leaves_tree": "rlc_leaves_tree_g1", "rlc_plain_tree": "rlc_plain_tree_g1",
-               "rlc_confirm": "rlc_root_msm_g1"},
+               "rlc_leaves_tree": "rlc_leaves_tree_g1", "rlc_plain_tree": "rlc_plain_tree_g1"},
     # recovery (batched check): per round, one pairing check and the MSMs
     "recover": {"eng_lines": "k_eng_lines", "eng_miller": "k_eng_miller", "eng_inv": "k_eng_inv",
                 "eng_fe": "k_eng_fe", "recover_msm": "recover_msm", "recover_rlc_g1": "recover_rlc_g1"},

@@ -176,6 +176,8 @@ struct dgpu_ctx {
   DevBuf h_pts, sig_pts, status, h_z, h_pre, h_tmp;
   // RLC mode: pre-cofactor hash points, segment-tree levels, bisection scratch
   DevBuf rlc_tree, rlc_idx, rlc_fail, rlc_h, rlc_s, rlc_st, rlc_root;
+  // localize-then-confirm: the confirmation root + compacted list, the marked rounds' leaf sums
+  DevBuf rlc_conf, rlc_fsum;
   // RLC root by bucket MSM (rlc_msm.cuh): AoS points, flags, counts / offsets /
   // cursors, bucket lists, bucket sums, per-run window sums
   DevBuf msm_aos, msm_flags, msm_counts, msm_list, msm_buckets, msm_runs, msm_root;
@@ -649,7 +651,7 @@ int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32
 // up from the leaves), then all descendants D levels down of each failing
 // node, to the leaves; a failing leaf is an invalid round (ST_PAIRING).
 int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hipStream_t s,
-                       bool root_failed = false) {
+                       bool root_failed = false, std::vector<uint32_t>* leaf_cand = nullptr) {
   const unsigned B = 256;
   const int D = c->rlc_descent_step;
   const int top = T.top();
@@ -681,6 +683,7 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
       hipLaunchKernelGGL(k_rlc_mark, dim3(grid_for(cand.size(), B)), dim3(B), 0, s, cand.size(),
                          (const uint32_t*)c->rlc_idx.p, (const uint8_t*)c->rlc_fail.p, st);
       HIP_TRY(hipGetLastError());
+      if (leaf_cand) leaf_cand->swap(cand);  // rlc_idx / rlc_fail still hold them on the device
       break;
     }
     const int nl = l >= D ? l - D : 0;
@@ -698,38 +701,96 @@ int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hi
 }
 
 // RLC phase 2 when a root containing this shard failed: exact per-round
-// verdicts (DESIGN.md 2c "localize, then confirm").
+// verdicts (DESIGN.md 2c "localize, then confirm").  shard_root: this
+// shard's random-combination root (stride-1 P, S; seed a.seed).
+//  0. Unless it is known failing (root_failed: it was the node's root), the
+//     shard's own root is checked first: passing, the shard is valid.
 //  1. Localize on the tree of plain sums (coefficients 1, k_rlc_leaves_plain):
 //     its leaves cost nothing (the points themselves) and a leaf check is the
 //     round's own pairing check, so every round it marks ST_PAIRING is
 //     exactly invalid.  Bad rounds can hide only in an internal node whose
 //     errors cancel in the plain sum (crafted input).
-//  2. Confirm the rest: a fresh random combination (bucket MSM over the
-//     rounds still ST_OK, seed derived from the call's seed) and one check.
-//     It passes for a correct localization; then every remaining round is
-//     valid except with probability 2^-64 -- the soundness of the root.
+//  2. Confirm the rest: the shard's root minus the marked rounds' terms (their
+//     random-coefficient leaves, a few per thousand rounds), one check.  It
+//     passes for a correct localization; then every remaining round is valid
+//     except with probability 2^-64 -- the coefficients are uniform and
+//     independent of the localization, which uses plain sums only.
 //  3. Only if the confirmation fails: the random-coefficient tree (leaves
 //     [a] R + [b] endo(R)) over what is left, descended as before.
-// The shard's own root is checked first unless it is known failing
-// (root_failed: the node's root was this shard's).
-int rlc_resolve_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s, bool root_failed) {
+template <class Gr>
+int rlc_confirm_t(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s, const uint32_t* shard_root,
+                  const std::vector<uint32_t>& leaf_cand, bool* ok) {
+  using M = GrMem<Gr>;
+  const unsigned B = 256;
   int rc;
+  mark(c, s, "rlc_confirm");
+  const size_t mc = leaf_cand.size();
+  if ((rc = c->rlc_conf.ensure((mc + 1) * 4 + 2 * (size_t)M::JAC * 4))) return rc;
+  uint32_t* conf = (uint32_t*)c->rlc_conf.p;       // confirmation root (P, S)
+  uint32_t* count = conf + 2 * M::JAC;             // compaction counter, then the list
+  uint32_t* list = count + 1;
+  uint32_t nf = 0;
+  if (mc) {
+    HIP_TRY(hipMemsetAsync(count, 0, 4, s));
+    hipLaunchKernelGGL(k_rlc_compact_fail, dim3(grid_for(mc, B)), dim3(B), 0, s, mc, (const uint32_t*)c->rlc_idx.p,
+                       (const uint8_t*)c->rlc_fail.p, list, count);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&nf, count, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  const uint32_t* fsum = nullptr;
+  if (nf) {  // the marked rounds' leaves, summed pairwise to one (P, S)
+    std::vector<size_t> sz{nf};
+    while (sz.back() > 1) sz.push_back((sz.back() + 1) / 2);
+    size_t words = 0;
+    for (size_t v : sz) words += 2 * v * M::JAC;
+    if ((rc = c->rlc_fsum.ensure(words * 4))) return rc;
+    uint32_t* lv = (uint32_t*)c->rlc_fsum.p;
+    hipLaunchKernelGGL(k_rlc_leaves_list<Gr>, dim3(grid_for(2 * (size_t)nf, B)), dim3(B), 0, s, (size_t)nf,
+                       (const uint32_t*)list, a.n, a.seed, (const uint32_t*)rlc_rpts(c, a.n, M::JAC),
+                       (const uint32_t*)c->sig_pts.p, lv, lv + (size_t)nf * M::JAC);
+    HIP_TRY(hipGetLastError());
+    for (size_t l = 0; l + 1 < sz.size(); ++l) {
+      uint32_t* nx = lv + 2 * sz[l] * M::JAC;
+      hipLaunchKernelGGL(k_rlc_level<Gr>, dim3(grid_for(2 * sz[l + 1], B)), dim3(B), 0, s, sz[l], lv,
+                         lv + sz[l] * M::JAC, sz[l + 1], nx, nx + sz[l + 1] * M::JAC);
+      HIP_TRY(hipGetLastError());
+      lv = nx;
+    }
+    fsum = lv;  // P at lv, S at lv + JAC (one node: stride 1)
+    hipLaunchKernelGGL(k_rlc_sub_root<Gr>, dim3(1), dim3(64), 0, s, shard_root, fsum, fsum + M::JAC, conf);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemcpyAsync(conf, shard_root, 2 * (size_t)M::JAC * 4, hipMemcpyDeviceToDevice, s));
+  }
+  std::vector<uint8_t> fail;
+  if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, conf, conf + M::JAC, s, &fail))) return rc;
+  *ok = !fail[0];
+  return DGPU_OK;
+}
+
+int rlc_resolve_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s,
+                       const uint32_t* shard_root, bool root_failed) {
+  int rc;
+  const bool g1 = sig_on_g1(a.scheme);
+  const int jw = rlc_geom_of(g1).jw;
+  if (!root_failed) {
+    std::vector<uint8_t> fail;
+    if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, shard_root, shard_root + jw, s, &fail))) return rc;
+    if (!fail[0]) return DGPU_OK;
+  }
   rlc_trees T;
   if (c->rlc_localize) {
-    if ((rc = rlc_tree_locked(c, a, s, T, true)) || (rc = rlc_descend_locked(c, key, T, s, root_failed))) return rc;
-    const int jw = rlc_geom_of(sig_on_g1(a.scheme)).jw;
-    verify_args a2 = a;
-    a2.seed = splitmix_host(a.seed ^ 0xC0F1A7ull);
-    if ((rc = c->rlc_root.ensure(2 * (size_t)jw * 4))) return rc;
-    uint32_t* root = (uint32_t*)c->rlc_root.p;
-    if ((rc = rlc_root_msm_locked(c, a2, s, root, "rlc_confirm"))) return rc;
-    std::vector<uint8_t> fail;
-    if ((rc = rlc_check_locked(c, key, std::vector<uint32_t>{0}, 1, root, root + jw, s, &fail))) return rc;
-    if (!fail[0]) return DGPU_OK;
-    root_failed = false;  // the random tree's root is another combination
+    std::vector<uint32_t> leaf_cand;
+    if ((rc = rlc_tree_locked(c, a, s, T, true)) || (rc = rlc_descend_locked(c, key, T, s, true, &leaf_cand)))
+      return rc;
+    bool ok = false;
+    rc = g1 ? rlc_confirm_t<G1Ops>(c, key, a, s, shard_root, leaf_cand, &ok)
+            : rlc_confirm_t<G2Ops>(c, key, a, s, shard_root, leaf_cand, &ok);
+    if (rc || ok) return rc;
   }
   if ((rc = rlc_tree_locked(c, a, s, T))) return rc;
-  return rlc_descend_locked(c, key, T, s, root_failed);
+  return rlc_descend_locked(c, key, T, s, true);
 }
 
 // Karabina final exponentiation of one chunk (pairing_engine.cuh, DESIGN.md
@@ -985,7 +1046,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
       }
       return DGPU_OK;
     }
-    return rlc_resolve_locked(c, key, a, s, true);
+    return rlc_resolve_locked(c, key, a, s, root, true);
   }
   if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
   const uint32_t* consts = (const uint32_t*)key->consts.p;
@@ -1323,7 +1384,10 @@ int dgpu_rlc_root_device(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_l
     if ((rc = c->status.ensure(n))) return rc;
     c->n_ev = 0;
     c->ev_overflow = false;
-    if ((rc = rlc_points_locked(c, a, s)) || (rc = rlc_root_msm_locked(c, a, s, (uint32_t*)d_root))) return rc;
+    if ((rc = rlc_points_locked(c, a, s)) || (rc = c->msm_root.ensure(2 * (size_t)G.jw * 4)) ||
+        (rc = rlc_root_msm_locked(c, a, s, (uint32_t*)c->msm_root.p)))
+      return rc;
+    HIP_TRY(hipMemcpyAsync(d_root, c->msm_root.p, 2 * (size_t)G.jw * 4, hipMemcpyDeviceToDevice, s));
   }
   c->rlc_args = a;
   memcpy(c->rlc_pk, pk, pk_len);
@@ -1361,7 +1425,7 @@ int dgpu_rlc_finish_device(dgpu_ctx* c, size_t n_roots, const uint8_t* d_roots, 
   if ((rc = rlc_check_locked(c, k, std::vector<uint32_t>{0}, 1, sum, sum + G.jw, s, &fail))) return rc;
   if (a.n == 0) return DGPU_OK;
   // this shard's verdicts, its own root first unless it is the node's (one root)
-  if (fail[0] && (rc = rlc_resolve_locked(c, k, a, s, n_roots == 1))) return rc;
+  if (fail[0] && (rc = rlc_resolve_locked(c, k, a, s, (const uint32_t*)c->msm_root.p, n_roots == 1))) return rc;
   const uint8_t* st = (const uint8_t*)c->status.p;
   mark(c, s, "pack_verdicts");
   hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((a.n + 7) / 8, 256)), dim3(256), 0, s, a.n, st, d_bits);

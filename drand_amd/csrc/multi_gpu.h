@@ -331,7 +331,8 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
       if (cnt == 0) return DGPU_OK;
       int r;
       // this shard's verdicts, its own root first (D = 1: that root is the node's, known failing)
-      if (!all_ok && (r = rlc_resolve_locked(c, keys[k], args[k], c->stream, D == 1))) return r;
+      if (!all_ok && (r = rlc_resolve_locked(c, keys[k], args[k], c->stream, (const uint32_t*)c->msm_root.p, D == 1)))
+        return r;
       return pack_shard_locked(c, cnt, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, c->stream);
     });
     if (rc) return rc;

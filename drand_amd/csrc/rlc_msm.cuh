@@ -333,6 +333,52 @@ __global__ void __launch_bounds__(256) k_rlc_leaves_plain(size_t n, const uint32
   M::st_jac(sig ? s_out : p_out, n, i, acc);
 }
 
+// Leaves of listed rounds (the localization's failing leaves), whatever
+// their status now: P_k = [a] R_i + [b] endo(R_i), S_k likewise, i = list[k]
+// -- the terms those rounds contributed to the shard's root.
+template <class Gr>
+__global__ void __launch_bounds__(256, 2) k_rlc_leaves_list(size_t m, const uint32_t* __restrict__ list, size_t n,
+                                                            uint64_t seed, const uint32_t* __restrict__ r_aff,
+                                                            const uint32_t* __restrict__ sig_pts,
+                                                            uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
+  using M = GrMem<Gr>;
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * m) return;
+  const bool sig = j >= m;
+  const size_t k = sig ? j - m : j, i = list[k];
+  typename Gr::jac acc = Gr::inf();
+  const typename Gr::aff q = M::ld_aff(sig ? sig_pts : r_aff, n, i);
+  if (!Gr::aff_is_zero(q)) {
+    const uint64_t z = rlc_coeff(seed, i);
+    if constexpr (std::is_same<Gr, G2Ops>::value)
+      acc = g2_mul2_win4_affine(q, (uint32_t)z, (uint32_t)(z >> 32));
+    else
+      acc = mul2_win4_affine<Gr>(q, (uint32_t)z, (uint32_t)(z >> 32));
+  }
+  M::st_jac(sig ? s_out : p_out, m, k, acc);
+}
+
+// Compaction of the failing candidates: out[atomic] = idx[k] where fail[k]
+// (order irrelevant: the listed leaves are summed).
+__global__ void __launch_bounds__(256) k_rlc_compact_fail(size_t m, const uint32_t* __restrict__ idx,
+                                                          const uint8_t* __restrict__ fail, uint32_t* __restrict__ out,
+                                                          uint32_t* __restrict__ count) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < m && fail[k]) out[atomicAdd(count, 1u)] = idx[k];
+}
+
+// root - F (each a stride-1 (P, S) pair of Jacobian points) -> out
+template <class Gr>
+__global__ void k_rlc_sub_root(const uint32_t* __restrict__ root, const uint32_t* __restrict__ fp_,
+                               const uint32_t* __restrict__ fs, uint32_t* __restrict__ out) {
+  using M = GrMem<Gr>;
+  if (blockIdx.x != 0 || threadIdx.x >= 2) return;
+  const int w = threadIdx.x;  // 0: P, 1: S
+  const typename Gr::jac r = M::ld_jac(root + w * M::JAC, 1, 0);
+  const typename Gr::jac f = M::ld_jac(w ? fs : fp_, 1, 0);
+  M::st_jac(out + w * M::JAC, 1, 0, Gr::add(r, Gr::neg(f)));
+}
+
 // One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied); 2 n_out
 // threads, the first n_out on the P tree, the rest on the S tree.
 template <class Gr>

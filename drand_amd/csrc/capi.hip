@@ -192,7 +192,7 @@ struct dgpu_ctx {
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
-  int rlc_descent_step = 5;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step)
+  int rlc_descent_step = 3;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step; r04g: 3 > 2 > 5)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
@@ -647,7 +647,7 @@ int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32
 // RLC phase 2, root first: the whole batch is one node check (one final
 // exponentiation) when every round is valid.  Otherwise the wide descent:
 // check every node of the level with <= 64Ki nodes (a multiple of D levels,
-// DGPU_RLC_DESCENT_STEP, default 5,
+// DGPU_RLC_DESCENT_STEP, default 3,
 // up from the leaves), then all descendants D levels down of each failing
 // node, to the leaves; a failing leaf is an invalid round (ST_PAIRING).
 int rlc_descend_locked(dgpu_ctx* c, const key_entry* key, const rlc_trees& T, hipStream_t s,

@@ -86,7 +86,9 @@ __global__ void k_pubpoly_table(int n, int t, const uint32_t* __restrict__ commi
 // signature decoded (96 bytes after the index; any other length, including
 // one above the stride, is a decode error; at most 98 bytes are read), the share key PubPoly.Eval(index) (table for index < n, else
 // evaluated here), status ST_* (ST_OK -> still to be pairing-checked).
-__global__ void __launch_bounds__(256) k_decode_partials(size_t n_items, const uint8_t* __restrict__ partials,
+// (the membership ladder inlined at 2 waves/SIMD, as k_decode_g2_sigs_sub:
+// out of line in g2_decompress its registers escape the kernel's budget)
+__global__ void __launch_bounds__(256, 2) k_decode_partials(size_t n_items, const uint8_t* __restrict__ partials,
                                                           size_t stride, const uint32_t* __restrict__ plen, int n_group,
                                                           int t, const uint32_t* __restrict__ table,
                                                           const uint32_t* __restrict__ commits,
@@ -104,7 +106,8 @@ __global__ void __launch_bounds__(256) k_decode_partials(size_t n_items, const u
     if (len == 98) {
       uint8_t buf[96];
       for (int k = 0; k < 96; ++k) buf[k] = src[2 + k];
-      const int rc = g2_decompress(&p, buf, true);
+      int rc = g2_decompress(&p, buf, false);
+      if (rc == DEC_OK && !g2_in_subgroup(g2_from_affine(p))) rc = DEC_ERR_SUBGROUP;
       st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
     }
   }

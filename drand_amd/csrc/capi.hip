@@ -191,9 +191,11 @@ struct dgpu_ctx {
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
+  bool kb_split = false;         // DGPU_KB_DEC=split: norms + decompression parts at the chain's snaps, per-thread inversion (A/B)
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
   int rlc_descent_step = 3;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step; r04g: 3 > 2 > 5)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
+  size_t thr_min = 0;            // DGPU_THR_MIN=<items>: smaller pairing chunks take the lane kernels (they fill the chip)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
@@ -794,9 +796,12 @@ int rlc_resolve_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, 
 }
 
 // Karabina final exponentiation of one chunk (pairing_engine.cuh, DESIGN.md
-// 2b): segment 0 (easy part), then per exponentiation by |x| the 8-lane
-// compressed chain, the batched inversion of its six stored values' norms,
-// their decompression and the next 12-lane segment; last, the Granger-Scott
+// 2b): segment 0 (easy part), then per exponentiation by |x| the compressed
+// chain, its six stored values' norms, the batched inversion of their
+// products (divsteps, fp.cuh fp_inv), the decompression, and the next 12-lane
+// segment (DGPU_KB_DEC=split: norms and decompression parts formed at the
+// chain's snaps, k_kb_chain_pre_thr, then one thread per round inverting and
+// decompressing, k_kb_dec_thr -- measured slower); last, the Granger-Scott
 // kernel for the listed blocks with a flagged item.  capb: the chunk capacity
 // rounded up to whole blocks of 5 rounds (>= cnt); kb: ENG_KB_BYTES_PER_ROUND
 // x capb bytes.
@@ -816,20 +821,32 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
   for (int seg = 0; seg < nseg; ++seg) {
     if (seg > 0) {
       mark(c, s, "eng_fe_chain");
-      if (c->kb_thread)
-        hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
-      else
-        hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
-      HIP_TRY(hipGetLastError());
-      mark(c, s, "eng_fe_kbinv");
-      hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
-                         pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
-      HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
-                         (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
-      HIP_TRY(hipGetLastError());
+      const bool kb_thread = c->kb_thread && cnt >= c->thr_min;
+      if (kb_thread && c->kb_split) {
+        // chain with the norms (to ebuf's planes) and decompression parts
+        // formed at the snaps; then per thread one inversion + decompression
+        hipLaunchKernelGGL(k_kb_chain_pre_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
+        HIP_TRY(hipGetLastError());
+        mark(c, s, "eng_fe_kbinv");
+        hipLaunchKernelGGL(k_kb_dec_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, xbuf,
+                           (const uint32_t*)ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+        HIP_TRY(hipGetLastError());
+      } else {
+        if (kb_thread)
+          hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
+        else
+          hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
+        HIP_TRY(hipGetLastError());
+        mark(c, s, "eng_fe_kbinv");
+        hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
+                           pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
+                           (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
+        HIP_TRY(hipGetLastError());
+      }
     }
     mark(c, s, "eng_fe");
     hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
@@ -890,7 +907,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                            fixed_table, lines);
       } else {
         mark(c, s, "eng_lines");
-        if (c->lines_thread)
+        if (c->lines_thread && cnt >= c->thr_min)
           hipLaunchKernelGGL(k_lines_thr, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, n, r0, cnt, h, h_stride, h_idx,
                              sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
         else
@@ -1208,12 +1225,16 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* kcv = getenv("DGPU_KB_CHAIN");
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
+  const char* kdv = getenv("DGPU_KB_DEC");
+  if (kdv && !strcmp(kdv, "split")) c->kb_split = true;
   const char* rds = getenv("DGPU_RLC_DESCENT_STEP");
   if (rds && atoi(rds) >= 1 && atoi(rds) <= 8) c->rlc_descent_step = atoi(rds);
   const char* rlv = getenv("DGPU_RLC_LOCALIZE");
   if (rlv && !strcmp(rlv, "0")) c->rlc_localize = false;
   const char* lnv = getenv("DGPU_LINES");
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
+  const char* tmv = getenv("DGPU_THR_MIN");
+  if (tmv) c->thr_min = (size_t)atol(tmv);
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");

@@ -399,7 +399,128 @@ DG_NOINL fp fp_pow_sched(fp a, const uint32_t* sched, int nsteps, int tail) {
 }
 #define DG_POW(a, NAME) fp_pow_sched((a), NAME##_SCHED, (int)(sizeof(NAME##_SCHED) / sizeof(uint32_t)), NAME##_SCHED_TAIL)
 
-DG_FN fp fp_inv(const fp& a) { return DG_POW(a, EXP_P_MINUS_2); }
+// a^-1 by Fermat (a^(p-2)): 381 squarings and ~82 multiplications.
+DG_FN fp fp_inv_pow(const fp& a) { return DG_POW(a, EXP_P_MINUS_2); }
+
+// ---------------------------------------------------------------- inversion by divsteps
+// Bernstein-Yang "safegcd" with half-delta divsteps (the variant whose
+// iteration bound for d-bit inputs is floor((45907 d + 26313) / 19929): 879
+// for d = 381), run in 32 batches of 28 on the low limb -- 896 divsteps --
+// with each batch's 2x2 transition matrix applied to the full-width (f, g)
+// and to the cofactors (d, e) at once.  Invariant: f = d x, g = e x (mod p),
+// starting from (f, g, d, e) = (p, x, 0, 1); at the end g = 0, f = +-1 and
+// x^-1 = +-d.  About 25k VALU operations against ~230k for the Fermat chain,
+// and no data-dependent control flow (the batch count is the bound).
+//
+// Signed numbers in radix 2^28: limbs 0..12 in [0, 2^28), limb 13 signed.
+struct fp_s {
+  int32_t l[FP_LIMBS];
+};
+
+// 28 divsteps on the low words f, g (only their low 28 bits are read):
+// returns (uf, vf; ug, vg) with 2^28 (f', g') = (uf f + vf g, ug f + vg g).
+// eta = 2 delta.  The swap case (delta > 0, g odd: f' = g, g' = (g - f) / 2)
+// is a swap with negation (f, g) <- (g, -f) followed by the g-odd case.
+DG_FN void fp_divsteps28(int32_t& eta, int32_t f, int32_t g, int32_t& uf, int32_t& vf, int32_t& ug, int32_t& vg) {
+  uf = 1, vf = 0, ug = 0, vg = 1;
+#pragma unroll 4
+  for (int k = 0; k < FP_BITS; ++k) {
+    const bool odd = g & 1;
+    const bool sw = odd && eta > 0;
+    const int32_t f0 = f, uf0 = uf, vf0 = vf;
+    f = sw ? g : f, uf = sw ? ug : uf, vf = sw ? vg : vf;
+    g = sw ? -f0 : g, ug = sw ? -uf0 : ug, vg = sw ? -vf0 : vg;
+    eta = sw ? -eta : eta;
+    g += odd ? f : 0, ug += odd ? uf : 0, vg += odd ? vf : 0;
+    g >>= 1, uf *= 2, vf *= 2, eta += 2;
+  }
+}
+
+// (a, b) <- ((ua a + va b) / 2^28, (ub a + vb b) / 2^28), exact (the low
+// 28 bits of both combinations vanish).  |u| + |v| <= 2^28, so every column
+// sum stays below 2^58.
+DG_FN void fp_s_apply(fp_s& a, fp_s& b, int32_t ua, int32_t va, int32_t ub, int32_t vb) {
+  int64_t ca = ((int64_t)ua * a.l[0] + (int64_t)va * b.l[0]) >> FP_BITS;
+  int64_t cb = ((int64_t)ub * a.l[0] + (int64_t)vb * b.l[0]) >> FP_BITS;
+#pragma unroll
+  for (int i = 1; i < FP_LIMBS; ++i) {
+    ca += (int64_t)ua * a.l[i] + (int64_t)va * b.l[i];
+    cb += (int64_t)ub * a.l[i] + (int64_t)vb * b.l[i];
+    a.l[i - 1] = (int32_t)(ca & FP_MASK), b.l[i - 1] = (int32_t)(cb & FP_MASK);
+    ca >>= FP_BITS, cb >>= FP_BITS;
+  }
+  a.l[FP_LIMBS - 1] = (int32_t)ca, b.l[FP_LIMBS - 1] = (int32_t)cb;
+}
+
+// The cofactors: (d, e) <- ((ud d + vd e + md p) / 2^28, (ue d + ve e + me p)
+// / 2^28) with md, me in [0, 2^28) chosen so that the divisions are exact,
+// i.e. the matrix applied mod p with the factor 2^-28.  |d|, |e| grow by < p
+// per batch: < 33p after 32 (top limb < 2^24).
+DG_FN void fp_s_apply_mod(fp_s& d, fp_s& e, int32_t ud, int32_t vd, int32_t ue, int32_t ve) {
+  const uint32_t md = (((uint32_t)ud * (uint32_t)d.l[0] + (uint32_t)vd * (uint32_t)e.l[0]) * FP_PINV) & FP_MASK;
+  const uint32_t me = (((uint32_t)ue * (uint32_t)d.l[0] + (uint32_t)ve * (uint32_t)e.l[0]) * FP_PINV) & FP_MASK;
+  int64_t cd = ((int64_t)ud * d.l[0] + (int64_t)vd * e.l[0] + (int64_t)md * FP_P[0]) >> FP_BITS;
+  int64_t ce = ((int64_t)ue * d.l[0] + (int64_t)ve * e.l[0] + (int64_t)me * FP_P[0]) >> FP_BITS;
+#pragma unroll
+  for (int i = 1; i < FP_LIMBS; ++i) {
+    cd += (int64_t)ud * d.l[i] + (int64_t)vd * e.l[i] + (int64_t)md * FP_P[i];
+    ce += (int64_t)ue * d.l[i] + (int64_t)ve * e.l[i] + (int64_t)me * FP_P[i];
+    d.l[i - 1] = (int32_t)(cd & FP_MASK), e.l[i - 1] = (int32_t)(ce & FP_MASK);
+    cd >>= FP_BITS, ce >>= FP_BITS;
+  }
+  d.l[FP_LIMBS - 1] = (int32_t)cd, e.l[FP_LIMBS - 1] = (int32_t)ce;
+}
+
+// r = a^-1 (Montgomery in, Montgomery out; 0 -> 0).  The Montgomery value
+// x = a R is inverted as an integer (x^-1 = a^-1 R^-1) and multiplied by R^3
+// through the Montgomery product: a^-1 R.  false if g has not reached 0
+// (excluded by the divstep bound); fp_inv then takes the Fermat chain.
+DG_FN bool fp_inv_ds(const fp& a, fp& r) {
+  const fp x = fp_csub_p(fp_csub_p(a));  // CI (< 2.01p) -> [0, p)
+  fp_s f, g, d, e;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) {
+    f.l[i] = (int32_t)FP_P[i], g.l[i] = (int32_t)x.l[i];
+    d.l[i] = 0, e.l[i] = 0;
+  }
+  e.l[0] = 1;
+  int32_t eta = 1;
+#pragma unroll 1
+  for (int b = 0; b < 32; ++b) {
+    int32_t uf, vf, ug, vg;
+    fp_divsteps28(eta, f.l[0], g.l[0], uf, vf, ug, vg);
+    fp_s_apply(f, g, uf, vf, ug, vg);
+    fp_s_apply_mod(d, e, uf, vf, ug, vg);
+  }
+  int32_t gz = 0, pos = f.l[0] ^ 1, neg = f.l[0] ^ (int32_t)FP_MASK;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) gz |= g.l[i];
+#pragma unroll
+  for (int i = 1; i < FP_LIMBS - 1; ++i) pos |= f.l[i], neg |= f.l[i] ^ (int32_t)FP_MASK;
+  pos |= f.l[FP_LIMBS - 1], neg |= f.l[FP_LIMBS - 1] + 1;
+  if (gz != 0) return false;
+  if (pos != 0 && neg != 0) {  // gcd(p, x) = p: x = 0
+    r = fp_zero();
+    return true;
+  }
+  // +-d + 34p in (p, 67p), carried into normalized limbs; times R^3
+  const int64_t sgn = pos == 0 ? 1 : -1;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) {
+    c += sgn * d.l[i] + 34 * (int64_t)FP_P[i];
+    r.l[i] = (uint32_t)(c & FP_MASK);
+    c >>= FP_BITS;
+  }
+  r.l[FP_LIMBS - 1] += (uint32_t)c << FP_BITS;
+  r = fp_mul(r, FP_R3);
+  return true;
+}
+DG_NOINL fp fp_inv(const fp& a) {
+  fp r;
+  if (!fp_inv_ds(a, r)) r = fp_inv_pow(a);
+  return r;
+}
 
 // candidate square root a^((p+1)/4); caller checks (r^2 == a)
 DG_FN fp fp_sqrt_cand(const fp& a) { return DG_POW(a, EXP_P_PLUS_1_DIV_4); }

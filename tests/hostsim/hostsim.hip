@@ -252,6 +252,48 @@ int hs_fp_ops(const uint8_t* a48, const uint8_t* b48, uint8_t* mul, uint8_t* add
   return 0;
 }
 
+// fp_inv (divsteps) against fp_inv_pow (Fermat) on n pseudo-random CI inputs
+// (values up to 2.01p, not reduced) and the edge values 0, p, 2p, 1, p - 1,
+// 2^k (Montgomery words); returns the number of disagreements.
+int hs_fp_inv_check(int n, uint64_t seed) {
+  uint64_t s = seed | 1;
+  auto next = [&]() {
+    s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+    return s;
+  };
+  int bad = 0;
+  auto check = [&](const fp& x) {
+    fp a;
+    if (!fp_inv_ds(x, a)) ++bad;  // the divstep path itself, no fallback
+    const fp b = fp_inv_pow(x);
+    if (!fp_is_zero(fp_sub(a, b))) ++bad;
+    if (!fp_is_zero(x) && !fp_is_zero(fp_sub(fp_mul(a, x), fp_one()))) ++bad;
+  };
+  fp e = fp_zero();
+  check(e);
+  for (int i = 0; i < FP_LIMBS; ++i) e.l[i] = FP_P[i];
+  check(e);
+  for (int i = 0; i < FP_LIMBS; ++i) e.l[i] = FP_2P[i];
+  check(e);
+  e = fp_zero(), e.l[0] = 1;
+  check(e);
+  e = fp_zero(), e.l[0] = FP_P[0] - 1;
+  for (int i = 1; i < FP_LIMBS; ++i) e.l[i] = FP_P[i];
+  check(e);
+  for (int k = 0; k < 381; k += 7) {
+    e = fp_zero(), e.l[k / FP_BITS] = 1u << (k % FP_BITS);
+    check(e);
+  }
+  for (int t = 0; t < n; ++t) {
+    fp x;
+    for (int i = 0; i < FP_LIMBS; ++i) x.l[i] = (uint32_t)next() & FP_MASK;
+    x.l[FP_LIMBS - 1] &= (t & 1) ? 0x1FFFFu : 0x3FFFFu;  // < 2^381 or < 2^382 ...
+    x = fp_reduce(x);                                     // ... into CI (< 2.01p)
+    check(x);
+  }
+  return bad;
+}
+
 int hs_fp2_ops(const uint8_t* a96, const uint8_t* b96, uint8_t* mul, uint8_t* sqr, uint8_t* inv, uint8_t* sqrt_out,
                int* sqrt_ok) {
   fp2 a{fp_from_be(a96), fp_from_be(a96 + 48)}, b{fp_from_be(b96), fp_from_be(b96 + 48)};
@@ -881,4 +923,31 @@ extern "C" int hs_eng_pairing(const uint8_t* pk48, const uint8_t* msg32, const u
     one = one && acc == 0;
   }
   return one ? 1 : 0;
+}
+
+// engine.cuh eng_kb_dec_parts + eng_kb_dec_finish (the split used by
+// k_kb_chain_pre_thr / k_kb_dec_thr) == eng_kb_decompress on n random
+// inputs; returns the number of disagreements.
+extern "C" int hs_kb_dec_split_check(int n, uint64_t seed) {
+  uint64_t s = seed | 1;
+  auto rnd = [&]() {
+    fp x;
+    for (int i = 0; i < FP_LIMBS; ++i) {
+      s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+      x.l[i] = (uint32_t)s & FP_MASK;
+    }
+    x.l[FP_LIMBS - 1] &= 0x1FFFFu;
+    return fp_reduce(x);
+  };
+  int bad = 0;
+  for (int t = 0; t < n; ++t) {
+    const fp2 f1{rnd(), rnd()}, f2{rnd(), rnd()}, f4{rnd(), rnd()}, f5{rnd(), rnd()};
+    const fp ninv = rnd();
+    fp2 a0, a3, b0, b3, nn, vv;
+    eng_kb_decompress(f1, f2, f4, f5, ninv, a0, a3);
+    eng_kb_dec_parts(f1, f2, f4, f5, nn, vv);
+    eng_kb_dec_finish(f1, nn, vv, ninv, b0, b3);
+    if (!fp2_eq(a0, b0) || !fp2_eq(a3, b3)) ++bad;
+  }
+  return bad;
 }

@@ -221,8 +221,9 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     and against the Karabina path with every 7th item of each chunk forced
     onto the fallback list (DGPU_KB_TEST_FLAG=7: flagged as if f1 = 0, its FE
     re-run on prog_fe by k_eng_fe_fb) -- the fallback otherwise practically
-    never runs -- and with the 8-lane compressed chain (DGPU_KB_CHAIN=lanes)
-    in place of the per-thread one.  20,011 rounds (a ragged last block), 1%
+    never runs -- with the 8-lane compressed chain (DGPU_KB_CHAIN=lanes)
+    in place of the per-thread one, and with the decompression split at the
+    inversion (DGPU_KB_DEC=split; fallback forced and not).  20,011 rounds (a ragged last block), 1%
     corrupted: identical reasons, equal to the construction."""
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
@@ -233,7 +234,9 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     gs = _verify_with_env(c, {"DGPU_FE": "gs"})
     fb = _verify_with_env(c, {"DGPU_KB_TEST_FLAG": "7"})
     lanes = _verify_with_env(c, {"DGPU_KB_CHAIN": "lanes"})
-    assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist()
+    split = _verify_with_env(c, {"DGPU_KB_DEC": "split"})
+    split_fb = _verify_with_env(c, {"DGPU_KB_DEC": "split", "DGPU_KB_TEST_FLAG": "7"})
+    assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist() == split.tolist() == split_fb.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(kb == 0, expect)

@@ -6,7 +6,7 @@
 # pipeline -- one rocprofv3 run per pass, kernel trace only.
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)"; }
-O=gpurun_out/r04h
+O=gpurun_out/${HTAG:-r04h}
 mkdir -p $O
 if [ -z "$NOAB" ]; then
 TAG=r04h1 PYTEST_K="recover" REPS=1 VARIANTS="head=X conf=LIB=libdrand_gpu_conf.so" BENCH_ARGS="--mode recover --steps 3 --no-cpu-baseline" bash tools/gpu/r04_ab.sh || exit $?

@@ -89,7 +89,7 @@ const char *dgpu_last_error(void);
  * DGPU_LINES=engine and DGPU_KB_CHAIN=lanes run the Miller loops' T-steps and
  * the final exponentiation's compressed chains on the 12- / 8-lane engine
  * instead of one thread per item (default; verdicts are identical);
- * DGPU_THR_MIN=<items> (default 65536): pairing batches smaller than this
+ * DGPU_THR_MIN=<items> (default 65536): RLC node checks on fewer items
  * take those engine kernels, which fill the chip at small sizes;
  * DGPU_KB_DEC=split forms the Karabina decompression parts inside the chain
  * (A/B, measured slower); DGPU_FE=gs runs the Granger-Scott final

@@ -23,7 +23,7 @@
 //   k_msm_scan    exclusive prefix sums (one block)
 //   k_msm_scatter point indices into their buckets (atomics on cursors)
 //   k_msm_bucket  one thread per bucket: sum of its points (mixed additions)
-//   k_msm_window  one thread per run of 64 buckets: sum_k k B_k of the run
+//   k_msm_window  one thread per run of MSM_RUN buckets: sum_k k B_k of the run
 //   k_sum_level   pairwise tree over the runs of each (MSM, window)
 //   k_msm_root    MSM_m = W_m0 + 2^16 W_m1; P = MSM_0 + endo(MSM_1), S = MSM_2 + endo(MSM_3)
 #pragma once
@@ -112,7 +112,14 @@ constexpr int MSM_C = 16;                         // window bits
 constexpr int MSM_BUCKETS = 1 << MSM_C;           // per (MSM, window); digit 0 unused
 constexpr int MSM_MW = 8;                         // 4 MSMs x 2 windows
 constexpr size_t MSM_KEYS = (size_t)MSM_MW * MSM_BUCKETS;
-constexpr int MSM_RUN = 64;                       // buckets per k_msm_window thread
+// Buckets per k_msm_window thread: 8 (64Ki threads for the 8 (MSM, window)
+// pairs, short serial runs) measured faster than 64 (8Ki threads, 512 waves
+// for 1,024 SIMDs): root MSM 96.2 -> 87.2 ms per 10M G2 points, 37.8 -> 35.6
+// for G1 (profiles/r04/r04p_msm_run_ab.txt).
+#ifndef DG_MSM_RUN
+#define DG_MSM_RUN 8
+#endif
+constexpr int MSM_RUN = DG_MSM_RUN;
 constexpr int MSM_RUNS = MSM_BUCKETS / MSM_RUN;   // runs per (MSM, window)
 
 // R (affine SoA in r_aff, (0, 0) = identity) and sig (affine SoA) -> AoS
@@ -231,7 +238,7 @@ __global__ void __launch_bounds__(256, 2) k_msm_window(const uint32_t* __restric
     R = Gr::add_body(R, M::ld_jac(buckets, MSM_KEYS, base + k));
     T = Gr::add_body(T, R);
   }
-  if (lo == 0) {  // digits 0..63: T counts every bucket once too often
+  if (lo == 0) {  // digits 0..MSM_RUN-1: T counts every bucket once too often
     T = Gr::add(T, Gr::neg(R));
   } else if (lo > 1) {  // + [lo - 1] R, double-and-add over the 16-bit multiplier
     const uint32_t s = lo - 1;

@@ -184,6 +184,26 @@ def test_rlc_mode_large_chain(chained):
     assert np.array_equal(per == 0, expect)
 
 
+def test_rlc_node_checks_on_either_kernel_family():
+    """RLC mode's node checks below DGPU_THR_MIN (default 65,536) run on the
+    12-lane lines and 8-lane chain kernels; DGPU_THR_MIN=0 puts every check on
+    the per-thread kernels (what the 10M bench's 64Ki-node top level uses).
+    20,011 rounds, 1% corrupted: identical reasons either way, equal to
+    per-round mode and to the construction."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 20011
+    c = make_chain(23, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 23, rate=1e-2)
+    per = _verify_with_env(c, {})
+    lanes = _verify_with_env(c, {}, mode=_lib.MODE_RLC)
+    thread = _verify_with_env(c, {"DGPU_THR_MIN": "0"}, mode=_lib.MODE_RLC)
+    assert lanes.tolist() == thread.tolist() == per.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(per == 0, expect)
+
+
 def _verify_with_env(c, env, mode=None):
     """Verify chain c on a fresh context opened under the environment `env`
     (the library reads its A/B and test knobs at dgpu_open); returns reasons."""

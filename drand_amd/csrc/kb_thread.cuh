@@ -167,18 +167,14 @@ __global__ void __launch_bounds__(256, DG_KB_DECT_OCC) k_kb_dec_thr(size_t cnt, 
                                                    const uint8_t* __restrict__ status, size_t flag_every) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cnt) return;
-  auto norm = [&](int j) {
-    const fp nj = ld_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i);
-    return fp_is_zero(nj) ? fp_one() : nj;
-  };
+  auto norm = [&](int j) { return ld_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i); };
   bool zero = flag_every && i % flag_every == 0;
   fp pre[ENG_KB_NSNAP - 1];  // prefix products N_0 .. N_j
   fp acc;
 #pragma unroll
   for (int j = 0; j < ENG_KB_NSNAP; ++j) {
-    const fp raw = ld_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i);
-    zero = zero || fp_is_zero(raw);
     const fp nj = norm(j);
+    zero = zero || fp_is_zero(nj);
     acc = j ? fp_mul(acc, nj) : nj;
     if (j < ENG_KB_NSNAP - 1) pre[j] = acc;
   }
@@ -187,7 +183,7 @@ __global__ void __launch_bounds__(256, DG_KB_DECT_OCC) k_kb_dec_thr(size_t cnt, 
     return;
   }
   if (flags[i]) return;  // flagged at an earlier exponentiation: the fallback recomputes it
-  fp pinv = fp_inv(acc);  // after value j: 1 / (N_0 ... N_(j-1))
+  fp pinv = fp_inv(acc);  // every N_j nonzero here; after value j: 1 / (N_0 ... N_(j-1))
 #pragma unroll
   for (int j = ENG_KB_NSNAP - 1; j >= 0; --j) {
     const int pl = ENG_KB_PL_X0 + j;

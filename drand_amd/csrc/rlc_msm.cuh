@@ -389,10 +389,9 @@ __global__ void k_rlc_sub_root(const uint32_t* __restrict__ root, const uint32_t
 // One tree level: out[j] = in[2j] + in[2j+1] (odd tail copied); 2 n_out
 // threads, the first n_out on the P tree, the rest on the S tree.
 template <class Gr>
-#ifndef DG_RLC_LEVEL_OCC
-#define DG_RLC_LEVEL_OCC 1
-#endif
-__global__ void __launch_bounds__(256, DG_RLC_LEVEL_OCC) k_rlc_level(size_t n_in, const uint32_t* __restrict__ p_in,
+// (bounded at 2 waves/SIMD it spills 233 VGPRs for G2 and gains nothing:
+// profiles/r04/r04s_rlc_level_occ_ab.txt)
+__global__ void __launch_bounds__(256) k_rlc_level(size_t n_in, const uint32_t* __restrict__ p_in,
                                                    const uint32_t* __restrict__ s_in, size_t n_out,
                                                    uint32_t* __restrict__ p_out, uint32_t* __restrict__ s_out) {
   using M = GrMem<Gr>;

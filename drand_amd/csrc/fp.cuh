@@ -41,8 +41,10 @@
 #if defined(DG_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
 extern unsigned long long dg_count_mul, dg_count_sqr;
 #define DG_COUNT(x) (++(x))
+#define DG_COUNT_N(x, n) ((x) += (n))
 #else
 #define DG_COUNT(x)
+#define DG_COUNT_N(x, n)
 #endif
 
 namespace dgpu {
@@ -476,6 +478,9 @@ DG_FN void fp_s_apply_mod(fp_s& d, fp_s& e, int32_t ud, int32_t vd, int32_t ue, 
 // through the Montgomery product: a^-1 R.  false if g has not reached 0
 // (excluded by the divstep bound); fp_inv then takes the Fermat chain.
 DG_FN bool fp_inv_ds(const fp& a, fp& r) {
+  // work counters (tools/count_ops.py): the batches' 32 x 140 signed 32x32->64
+  // mads, 4,480, as 11 multiplications' worth (392 each); fp_mul by R^3 counts itself
+  DG_COUNT_N(dg_count_mul, 11);
   const fp x = fp_csub_p(fp_csub_p(a));  // CI (< 2.01p) -> [0, p)
   fp_s f, g, d, e;
 #pragma unroll

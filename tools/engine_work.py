@@ -41,6 +41,9 @@ def program_work(ops, prog):
             "simt_lane_mads": 12 * simt_terms * MADS_PER_PRODUCT}
 
 
+INV_MADS = 32 * 140 + 392  # one field inversion by divsteps (round 4; a^(p-2) was 82 mul + 380 sqr)
+
+
 def main():
     ops = G.build_ops()
     kern = {
@@ -48,14 +51,15 @@ def main():
         "k_eng_miller": program_work(ops, G.prog_miller()),
         "k_eng_fe": program_work(ops, G.prog_fe()),
         # Montgomery's trick: 3 Fp multiplications per item (392 mads each), one
-        # exponentiation per 64 items (~475 multiplications) amortized
-        "k_eng_inv": {"mads": 3 * 392 + 475 * 392 // 64},
+        # inversion per 64 items amortized (fp.cuh fp_inv: 32 divstep batches of
+        # 140 signed 32x32->64 mads, 4,480, plus one multiplication by R^3)
+        "k_eng_inv": {"mads": 3 * 392 + INV_MADS // 64},
     }
     # Karabina FE: the 12-lane program segments, the 8-lane
     # compressed chains (63 squarings of the E_CYC records for f1, f2, f4, f5,
     # five exponentiations), and the per-thread decompression side: norms of
     # the six stored values (k_eng_kb_norm: 2 sqr each, 5 mul), their product's
-    # inversion (k_eng_inv: 3 mul + an inversion, 82 mul + 380 sqr, per
+    # inversion (k_eng_inv: 3 mul + an inversion, INV_MADS, per
     # KB_INV_CHAIN items), the per-value inverses and eng_kb_decompress
     # (k_eng_kb_dec: 12 sqr + 5 mul forward, 2 mul + 2 sqr per value after the
     # first backward, 17 mul per decompression)
@@ -72,7 +76,7 @@ def main():
     KB_INV_CHAIN = 16
     ns = len(G.KB_SNAP)
     norm = 2 * ns * SQR + (ns - 1) * MUL
-    inv = 3 * MUL + (82 * MUL + 380 * SQR) // KB_INV_CHAIN
+    inv = 3 * MUL + INV_MADS // KB_INV_CHAIN
     dec = 2 * ns * SQR + (ns - 1) * MUL + (ns - 1) * (2 * MUL + 2 * SQR) + ns * 17 * MUL
     kern["k_eng_fe_seg"] = seg_work
     kern["k_eng_kb_chain"] = chain

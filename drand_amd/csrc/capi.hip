@@ -198,6 +198,8 @@ struct dgpu_ctx {
   size_t thr_min = 65536;        // DGPU_THR_MIN=<items>: RLC node checks smaller than this take the lane kernels,
                                  // which fill the chip (r04k: 11.15M -> 11.49M rounds/s at 0.1% corrupted)
   size_t lane_below = 0;         // pairing batches below this take the lane kernels (thr_min inside rlc_check_locked)
+  size_t rlc_min = 131072;       // DGPU_RLC_MIN=<rounds>: smaller RLC-mode batches run the per-round path (identical
+                                 // verdicts; the root MSM's and the descent's fixed costs lose below ~150k rounds, r04x)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
   bool decode_subgroup = false;  // DGPU_SUBGROUP=decode: G2 membership in the decoder, not the lines kernel (A/B)
   // threshold group (dgpu_set_group): commitments, PubPoly.Eval table; recovery scratch
@@ -1050,7 +1052,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   c->n_ev = 0;
   c->ev_overflow = false;
   c->rlc_pending = false;
-  if (a.mode == DGPU_MODE_RLC) {
+  if (a.mode == DGPU_MODE_RLC && n >= c->rlc_min) {
     // root first, by bucket MSM; the tree of leaves only when it fails
     const int jw = rlc_geom_of(sig_on_g1(a.scheme)).jw;
     if ((rc = rlc_points_locked(c, a, s))) return rc;
@@ -1239,6 +1241,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* tmv = getenv("DGPU_THR_MIN");
   if (tmv) c->thr_min = (size_t)atol(tmv);
+  const char* rmv = getenv("DGPU_RLC_MIN");
+  if (rmv) c->rlc_min = (size_t)atol(rmv);
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");

@@ -91,6 +91,9 @@ const char *dgpu_last_error(void);
  * instead of one thread per item (default; verdicts are identical);
  * DGPU_THR_MIN=<items> (default 65536): RLC node checks on fewer items
  * take those engine kernels, which fill the chip at small sizes;
+ * DGPU_RLC_MIN=<rounds> (default 131072): DGPU_MODE_RLC batches of fewer
+ * rounds run the per-round path instead (identical verdicts and reasons;
+ * below that size the combination's fixed costs make it the slower one);
  * DGPU_KB_DEC=split forms the Karabina decompression parts inside the chain
  * (A/B, measured slower); DGPU_FE=gs runs the Granger-Scott final
  * exponentiation (A/B). */

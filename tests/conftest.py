@@ -7,6 +7,12 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# The library runs DGPU_MODE_RLC batches under 131,072 rounds on the per-round
+# path (DGPU_RLC_MIN); the tests' RLC batches are smaller, so they lower the
+# threshold to exercise the RLC path itself (read at every dgpu_open).
+# tests/test_gpu_parity.py::test_rlc_small_batches_take_per_round_path
+# checks the default.
+os.environ.setdefault("DGPU_RLC_MIN", "0")
 HOSTSIM = os.path.join(ROOT, "tests", "hostsim", "libdrand_hostsim.so")
 
 

@@ -204,6 +204,21 @@ def test_rlc_node_checks_on_either_kernel_family():
     assert np.array_equal(per == 0, expect)
 
 
+def test_rlc_small_batches_take_per_round_path():
+    """Below DGPU_RLC_MIN rounds (default 131,072) an RLC-mode call runs the
+    per-round path: same reasons as RLC mode on the RLC path
+    (DGPU_RLC_MIN=0, the test suite's setting) and as per-round mode."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 5003
+    c = make_chain(29, n, _lib.SCHEME_CHAINED, seg_len=64)
+    corrupt(c, 29, rate=1e-2)
+    per = _verify_with_env(c, {})
+    small = _verify_with_env(c, {"DGPU_RLC_MIN": "131072"}, mode=_lib.MODE_RLC)
+    rlc = _verify_with_env(c, {"DGPU_RLC_MIN": "0"}, mode=_lib.MODE_RLC)
+    assert small.tolist() == rlc.tolist() == per.tolist()
+
+
 def _verify_with_env(c, env, mode=None):
     """Verify chain c on a fresh context opened under the environment `env`
     (the library reads its A/B and test knobs at dgpu_open); returns reasons."""

@@ -195,9 +195,9 @@ struct dgpu_ctx {
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
   int rlc_descent_step = 3;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step; r04g: 3 > 2 > 5)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
-  size_t thr_min = 65536;        // DGPU_THR_MIN=<items>: RLC node checks smaller than this take the lane kernels,
-                                 // which fill the chip (r04k: 11.15M -> 11.49M rounds/s at 0.1% corrupted)
-  size_t lane_below = 0;         // pairing batches below this take the lane kernels (thr_min inside rlc_check_locked)
+  size_t thr_min = 65536;        // DGPU_THR_MIN=<items>: pairing chunks smaller than this take the lane kernels,
+                                 // which fill the chip and cut the per-item latency (RLC node checks, r04k: 11.15M
+                                 // -> 11.49M rounds/s at 0.1% corrupted; small per-round batches, r04z)
   size_t rlc_min = 131072;       // DGPU_RLC_MIN=<rounds>: smaller RLC-mode batches run the per-round path (identical
                                  // verdicts; the root MSM's and the descent's fixed costs lose below ~150k rounds, r04x)
   bool fused_fixed = true;       // DGPU_G1_LINES=buffer: on-G1 lines through k_eng_lines_fixed (A/B)
@@ -636,11 +636,9 @@ int rlc_check_locked(dgpu_ctx* c, const key_entry* key, const std::vector<uint32
     hipLaunchKernelGGL(k_rlc_prep<G2Ops>, dim3(grid_for(m, 64)), dim3(64), 0, s, m, d_idx, n_level, P_lvl, S_lvl, ch,
                        cs, cst);
   HIP_TRY(hipGetLastError());
-  c->lane_below = c->thr_min;  // the descent's node checks are small batches
-  rc = eng_pairing_locked(c, (const uint32_t*)key->consts.p, m, ch, cs, cst, s, 0, nullptr, nullptr,
-                          G.g1 ? (const uint32_t*)key->table.p : nullptr);
-  c->lane_below = 0;
-  if (rc) return rc;
+  if ((rc = eng_pairing_locked(c, (const uint32_t*)key->consts.p, m, ch, cs, cst, s, 0, nullptr, nullptr,
+                               G.g1 ? (const uint32_t*)key->table.p : nullptr)))
+    return rc;
   mark(c, s, "rlc_bisection");
   hipLaunchKernelGGL(k_rlc_fail, dim3(grid_for(m, B)), dim3(B), 0, s, m, cst, d_fail);
   HIP_TRY(hipGetLastError());
@@ -827,7 +825,7 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
   for (int seg = 0; seg < nseg; ++seg) {
     if (seg > 0) {
       mark(c, s, "eng_fe_chain");
-      const bool kb_thread = c->kb_thread && cnt >= c->lane_below;
+      const bool kb_thread = c->kb_thread && cnt >= c->thr_min;
       if (kb_thread && c->kb_split) {
         // chain with the norms (to ebuf's planes) and decompression parts
         // formed at the snaps; then per thread one inversion + decompression
@@ -913,7 +911,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                            fixed_table, lines);
       } else {
         mark(c, s, "eng_lines");
-        if (c->lines_thread && cnt >= c->lane_below)
+        if (c->lines_thread && cnt >= c->thr_min)
           hipLaunchKernelGGL(k_lines_thr, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, n, r0, cnt, h, h_stride, h_idx,
                              sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
         else

@@ -89,8 +89,9 @@ const char *dgpu_last_error(void);
  * DGPU_LINES=engine and DGPU_KB_CHAIN=lanes run the Miller loops' T-steps and
  * the final exponentiation's compressed chains on the 12- / 8-lane engine
  * instead of one thread per item (default; verdicts are identical);
- * DGPU_THR_MIN=<items> (default 65536): RLC node checks on fewer items
- * take those engine kernels, which fill the chip at small sizes;
+ * DGPU_THR_MIN=<items> (default 65536): pairing batches (per-round chunks
+ * and RLC node checks) on fewer items take those engine kernels, which fill
+ * the chip and cut the per-item latency at small sizes;
  * DGPU_RLC_MIN=<rounds> (default 131072): DGPU_MODE_RLC batches of fewer
  * rounds run the per-round path instead (identical verdicts and reasons;
  * below that size the combination's fixed costs make it the slower one);

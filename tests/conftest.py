@@ -13,6 +13,11 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 # tests/test_gpu_parity.py::test_rlc_small_batches_take_per_round_path
 # checks the default.
 os.environ.setdefault("DGPU_RLC_MIN", "0")
+# Likewise pairing batches under DGPU_THR_MIN (65,536) items run the 12-lane
+# lines and 8-lane chain; the suite lowers it so its batches run the
+# per-thread kernels the bulk path uses.  Tests that compare the two kernel
+# families set it (or DGPU_LINES / DGPU_KB_CHAIN) on their own contexts.
+os.environ.setdefault("DGPU_THR_MIN", "0")
 HOSTSIM = os.path.join(ROOT, "tests", "hostsim", "libdrand_hostsim.so")
 
 

@@ -1238,9 +1238,9 @@ int dgpu_open(int device, dgpu_ctx** out) {
   const char* lnv = getenv("DGPU_LINES");
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* tmv = getenv("DGPU_THR_MIN");
-  if (tmv) c->thr_min = (size_t)atol(tmv);
+  if (tmv && atol(tmv) >= 0) c->thr_min = (size_t)atol(tmv);
   const char* rmv = getenv("DGPU_RLC_MIN");
-  if (rmv) c->rlc_min = (size_t)atol(rmv);
+  if (rmv && atol(rmv) >= 0) c->rlc_min = (size_t)atol(rmv);
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");

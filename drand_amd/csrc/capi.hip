@@ -93,7 +93,10 @@ inline bool scheme_known(int scheme) { return scheme >= DGPU_SCHEME_CHAINED && s
 // quarter of the free HBM): the line buffer takes 45.7 KB per round (24 GB at
 // 512Ki, per lane).  r01u A/B at 1M rounds: 64Ki 1.333M, 128Ki 1.362M,
 // 256Ki 1.383M, 512Ki 1.394M rounds/s.
-constexpr size_t ENG_CHUNK = 524288;
+// Rounds per engine chunk and lane: 1Mi measured +0.4% over 512Ki on the
+// 10M headline (per-thread lines and chains 4-5% faster per round, r04c1);
+// at most half the free HBM (two lanes x ~53 KB per round = 112 GB at 1Mi).
+constexpr size_t ENG_CHUNK = 1048576;
 constexpr size_t ENG_CHUNK_MIN = 16384;
 // Karabina FE state per round and lane: the planes (t, t2, m, six stored
 // values), the product of the six norms + its prefix products (k_eng_inv),
@@ -1177,7 +1180,7 @@ int verify_host_locked(dgpu_ctx* c, const key_entry* key, verify_args a, uint8_t
 size_t size_engine_chunk(int lanes) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return ENG_CHUNK;
-  const size_t fit = free_b / 4 / ((size_t)std::max(lanes, 1) * ENG_BYTES_PER_ROUND);
+  const size_t fit = free_b / 2 / ((size_t)std::max(lanes, 1) * ENG_BYTES_PER_ROUND);
   return std::max(ENG_CHUNK_MIN, std::min(ENG_CHUNK, fit));
 }
 

@@ -192,6 +192,7 @@ struct dgpu_ctx {
   size_t kb_inv_chain = 16;      // DGPU_KB_INV_CHAIN: norms per k_eng_inv thread in the Karabina FE (A/B)
   size_t kb_test_flag = 0;       // DGPU_KB_TEST_FLAG=k (tests): flag every k-th item so the fallback runs
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
+  size_t lane_slices = 2;        // DGPU_LANE_SLICES: slices of a two-lane batch, alternating between the lanes
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
   bool kb_split = false;         // DGPU_KB_DEC=split: norms + decompression parts at the chain's snaps, per-thread inversion (A/B)
@@ -1083,25 +1084,36 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   // are done, so its register-bound hash runs beside lane 0's LDS-bound
   // engine.  Profiled passes stay on one stream (clean per-kernel times).
   const bool two = c->lanes > 1 && !c->profile && n >= LANE_MIN;
-  const size_t n0 = two ? ((n / 2 + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
+  const size_t slices = two ? std::max<size_t>(2, c->lane_slices) : 1;
+  const size_t n0 = two ? ((n / slices + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
   if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s))) return rc;
   const bool sub = !c->decode_subgroup;
   if (!two)
     return eng_pairing_locked(c, consts, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
                               nullptr, nullptr, nullptr, &L0, sub);
-  const size_t n1 = n - n0;
   hipStream_t s2 = c->stream2;
   HIP_TRY(hipEventRecord(c->lane_ev[0], s));
   HIP_TRY(hipStreamWaitEvent(s2, c->lane_ev[0], 0));
   if ((rc = eng_pairing_locked(c, consts, n0, (const uint32_t*)L0.h_pts->p, (const uint32_t*)L0.sig_pts->p, st, s, 0,
                                nullptr, nullptr, nullptr, &L0, sub)))
     return rc;
-  if ((rc = g2_lane_hash_locked(c, L1, n1, src_slice(a.m, n0), a.sigs + n0 * a.sig_stride, a.sig_stride,
-                                a.sig_len + n0, st + n0, s2)))
-    return rc;
-  if ((rc = eng_pairing_locked(c, consts, n1, (const uint32_t*)L1.h_pts->p, (const uint32_t*)L1.sig_pts->p, st + n0,
-                               s2, 0, nullptr, nullptr, nullptr, &L1, sub)))
-    return rc;
+  // the remaining slices alternate between the lanes (stream order keeps each
+  // lane's buffers in use by one slice at a time), so a slice's hash runs
+  // beside the other lane's engine chunks (DGPU_LANE_SLICES, default 2)
+  const lane_bufs* LL[2] = {&L0, &L1};
+  hipStream_t ss[2] = {s, s2};
+  size_t k = 1;
+  for (size_t off = n0; off < n; off += n0, ++k) {
+    const size_t nk = std::min(n0, n - off);
+    const int ln = (int)(k & 1);
+    if ((rc = g2_lane_hash_locked(c, *LL[ln], nk, src_slice(a.m, off), a.sigs + off * a.sig_stride, a.sig_stride,
+                                  a.sig_len + off, st + off, ss[ln])))
+      return rc;
+    if ((rc = eng_pairing_locked(c, consts, nk, (const uint32_t*)LL[ln]->h_pts->p,
+                                 (const uint32_t*)LL[ln]->sig_pts->p, st + off, ss[ln], 0, nullptr, nullptr, nullptr,
+                                 LL[ln], sub)))
+      return rc;
+  }
   HIP_TRY(hipEventRecord(c->lane_ev[1], s2));
   HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
   return DGPU_OK;
@@ -1228,6 +1240,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   c->device = device;
   const char* lv = getenv("DGPU_LANES");
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
+  const char* lsv = getenv("DGPU_LANE_SLICES");
+  if (lsv && atol(lsv) >= 2 && atol(lsv) <= 64) c->lane_slices = (size_t)atol(lsv);
   const char* ec = getenv("DGPU_ENG_CHUNK");
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* kcv = getenv("DGPU_KB_CHAIN");

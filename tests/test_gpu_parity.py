@@ -329,7 +329,8 @@ def test_two_lane_per_round_large_chain():
 
     two = _verify_with_env(c, {"DGPU_LANES": "2"})
     one = _verify_with_env(c, {"DGPU_LANES": "1", "DGPU_ENG_CHUNK": "65536"})
-    assert two.tolist() == one.tolist()
+    five = _verify_with_env(c, {"DGPU_LANES": "2", "DGPU_LANE_SLICES": "5"})  # slices alternating between lanes
+    assert two.tolist() == one.tolist() == five.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(two == 0, expect)

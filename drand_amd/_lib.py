@@ -47,6 +47,7 @@ SYMBOLS = [
     ("dgpu_verify_batch_device", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P, _c.c_size_t,
                                             _P, _c.c_int, _c.c_uint64, _P, _P, _P]),
     ("dgpu_set_profiling", _c.c_int, [_P, _c.c_int]),
+    ("dgpu_synchronize", _c.c_int, [_P]),
     ("dgpu_stage_times", _c.c_int, [_P, _c.POINTER(_c.c_float), _c.c_int, _c.POINTER(_c.c_char_p)]),
     ("dgpu_digest_batch", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P]),
     ("dgpu_hash_to_g2", _c.c_int, [_P, _c.c_size_t, _P, _P]),
@@ -80,7 +81,7 @@ SYMBOLS = [
     ("dgpu_recover_multi", _c.c_int, [_P, _c.c_size_t, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P, _P]),
 ]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class DrandGPUError(RuntimeError):

@@ -77,7 +77,9 @@ struct DevBuf {
 inline unsigned grid_for(size_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 // SplitMix64 step on the host: independent RLC seeds derived from a call's
-// seed (per device of dgpu_verify_multi, the confirmation check)
+// seed per device of dgpu_verify_multi (drand_amd/dist.py rank_seed is the
+// same derivation per rank).  The confirmation check reuses the shard's seed:
+// it subtracts terms from that seed's root.
 uint64_t splitmix_host(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -250,6 +252,16 @@ struct stream_order {
   stream_order(dgpu_ctx* c_, hipStream_t s_) : c(c_), s(s_) { hipStreamWaitEvent(s, c->done, 0); }
   ~stream_order() { hipEventRecord(c->done, s); }
 };
+
+// The stream a *_device entry point enqueues on: the caller's, and NULL is
+// the device's legacy default (null) stream -- the handle torch's default
+// stream has -- never the context's own non-blocking stream.  Until ABI 2
+// NULL meant the context's stream, which is unordered with the null stream:
+// a caller that zero-filled outputs or read the RLC root on its default
+// stream raced the library (gpurun_out/r04c: a rank read its root before the
+// MSM wrote it, the all-zero root is the identity, the node check passed and
+// a corrupted round was accepted).
+hipStream_t caller_stream(void* stream) { return (hipStream_t)stream; }
 
 // Stage markers: mark(c, s, name) records an event that *starts* stage `name`
 // (and ends the previous one); mark(c, s, nullptr) closes the last stage.
@@ -875,22 +887,32 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                        uint8_t* st, hipStream_t s, size_t h_stride, const uint32_t* h_idx, const uint32_t* pk_items,
                        const uint32_t* fixed_table, const lane_bufs* L, bool sig_subgroup) {
   if (!h_stride) h_stride = n;
-  // equal chunks of at most eng_chunk items (whole 5-item blocks): no short tail launch
-  const size_t nchunks = (n + c->eng_chunk - 1) / c->eng_chunk;
-  size_t cap = (n + nchunks - 1) / nchunks;
-  cap = std::min(n, (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK * ENG_ROUNDS_PER_BLOCK);
-  const size_t cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
   DevBuf* b_lines = L ? L->lines : &c->eng_lines;
   DevBuf* b_f = L ? L->f : &c->eng_f;
   DevBuf* b_n1 = L ? L->n1 : &c->eng_n1;
   DevBuf* b_kb = L ? L->kb : &c->eng_kb;
   const bool need_lines = !(fixed_table && c->fused_fixed);
   int rc;
-  // the Karabina planes are wave-blocked: whole blocks of 5 rounds (cap may be n, not a multiple of 5)
-  if (!c->fe_gs && (rc = b_kb->ensure(cap_blk * ENG_ROUNDS_PER_BLOCK * ENG_KB_BYTES_PER_ROUND))) return rc;
-  if (need_lines && (rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
-  if ((rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4))) return rc;
-  if ((rc = b_n1->ensure(cap * FP_LIMBS * 4))) return rc;
+  size_t cap = 0, cap_blk = 0;
+  for (;;) {
+    // equal chunks of at most eng_chunk items (whole 5-item blocks): no short tail launch
+    const size_t nchunks = (n + c->eng_chunk - 1) / c->eng_chunk;
+    cap = (n + nchunks - 1) / nchunks;
+    cap = std::min(n, (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK * ENG_ROUNDS_PER_BLOCK);
+    cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
+    // the Karabina planes are wave-blocked: whole blocks of 5 rounds (cap may be n, not a multiple of 5)
+    rc = c->fe_gs ? DGPU_OK : b_kb->ensure(cap_blk * ENG_ROUNDS_PER_BLOCK * ENG_KB_BYTES_PER_ROUND);
+    if (!rc && need_lines) rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4);
+    if (!rc) rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4);
+    if (!rc) rc = b_n1->ensure(cap * FP_LIMBS * 4);
+    if (rc != DGPU_ENOMEM || c->eng_chunk <= ENG_CHUNK_MIN || cap <= ENG_CHUNK_MIN) break;
+    // HBM is shared (other contexts, torch): the chunk was sized from the free
+    // memory at dgpu_open; halve it for this context and retry
+    hipDeviceSynchronize();
+    for (DevBuf* b : {b_kb, b_lines, b_f, b_n1}) b->release();
+    c->eng_chunk = std::max(ENG_CHUNK_MIN, c->eng_chunk / 2);
+  }
+  if (rc) return rc;
   // k_eng_inv's prefix products reuse the line buffer (or f, on the fused path)
   uint32_t* lines = need_lines ? (uint32_t*)b_lines->p : nullptr;
   uint32_t* f = (uint32_t*)b_f->p;
@@ -1345,7 +1367,7 @@ int dgpu_verify_batch_device(dgpu_ctx* c, int scheme, size_t n, const uint64_t* 
   if (!c) return set_err(DGPU_EINVAL, "null ctx");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = caller_stream(stream);
   stream_order ord(c, s);
   const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
                       d_sigs, sig_stride, d_sig_len, mode, rlc_seed};
@@ -1389,7 +1411,7 @@ int dgpu_verify_beacons_device(dgpu_ctx* c, int scheme, const uint8_t* pk, size_
   key_entry* k = nullptr;
   int rc = get_key_locked(c, scheme, pk, pk_len, &k);
   if (rc) return rc;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = caller_stream(stream);
   stream_order ord(c, s);
   const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
                       d_sigs, sig_stride, d_sig_len, mode, rlc_seed};
@@ -1411,7 +1433,7 @@ int dgpu_rlc_root_device(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_l
   key_entry* k = nullptr;
   int rc = get_key_locked(c, scheme, pk, pk_len, &k);
   if (rc) return rc;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = caller_stream(stream);
   stream_order ord(c, s);
   const verify_args a{scheme, n, beacon_src(d_rounds, d_prev, prev_stride, d_prev_len, scheme == DGPU_SCHEME_CHAINED),
                       d_sigs, sig_stride, d_sig_len, DGPU_MODE_RLC, rlc_seed};
@@ -1452,7 +1474,7 @@ int dgpu_rlc_finish_device(dgpu_ctx* c, size_t n_roots, const uint8_t* d_roots, 
   key_entry* k = nullptr;
   int rc = get_key_locked(c, a.scheme, c->rlc_pk, c->rlc_pk_len, &k);
   if (rc) return rc;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = caller_stream(stream);
   stream_order ord(c, s);
   const rlc_geom G = rlc_geom_of(sig_on_g1(a.scheme));
   if ((rc = c->rlc_root.ensure(2 * (size_t)G.jw * 4))) return rc;
@@ -1494,6 +1516,14 @@ int dgpu_verify_recovered(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t pk_
   const verify_args a{scheme, n, raw_src(msgs ? msgs : &empty, msg_stride, msg_len), sigs, sig_stride, sig_len, mode,
                       rlc_seed};
   return verify_host_locked(c, k, a, verdict_bits, reason);
+}
+
+int dgpu_synchronize(dgpu_ctx* c) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventSynchronize(c->done));
+  return DGPU_OK;
 }
 
 int dgpu_set_profiling(dgpu_ctx* c, int enable) {
@@ -2013,7 +2043,7 @@ int dgpu_recover_batch_device(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msg
   if (m == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = caller_stream(stream);
   stream_order ord(c, s);
   return recover_device_locked(c, n_rounds, d_msgs32, m, d_partials, partial_stride, d_partial_len, d_out_sigs96,
                                d_ok, d_status, s);

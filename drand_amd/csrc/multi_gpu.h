@@ -277,6 +277,7 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
     c->n_ev = 0;
     c->ev_overflow = false;
     if (rlc) {  // the shard's points and its root by bucket MSM (the leaves wait for a failing root)
+      c->rlc_pending = false;  // overwrites the points a pending per-rank root (dgpu_rlc_root_device) kept
       if ((r = rlc_points_locked(c, a, s)) || (r = c->msm_root.ensure(2 * (size_t)jw * 4))) return r;
       return rlc_root_msm_locked(c, a, s, (uint32_t*)c->msm_root.p);
     }

@@ -26,6 +26,13 @@
  *    device: each call's work starts after the previous call's, whatever
  *    streams the *_device entry points are given.  There is no CPU fallback:
  *    without a usable GPU, dgpu_open fails with DGPU_EDEVICE.
+ *  - Streams (*_device entry points): `stream` is a hipStream_t of the
+ *    context's device and the call's work is enqueued on it, ordered after
+ *    everything the caller enqueued on it before the call (zero-fills, input
+ *    copies) and before anything enqueued after it (readouts, collectives).
+ *    NULL is the device's legacy default (null) stream -- torch's default
+ *    stream -- exactly as in HIP itself.  A caller that does not bind HIP
+ *    (cgo) waits for results with dgpu_synchronize.
  *  - Public keys are passed per call (dgpu_verify_beacons*, like
  *    VerifyBeacon(b, pubkey), chain/verify.go:38) and cached decoded per
  *    context (8 keys, LRU), so one context serves any number of chains and
@@ -43,7 +50,12 @@
 extern "C" {
 #endif
 
-#define DGPU_ABI_VERSION 2
+/* 3 (round 5): a NULL stream in the *_device entry points is the device's
+ * legacy default (null) stream, no longer the context's own stream;
+ * dgpu_synchronize added; dgpu_stage_times returns the count of stages the
+ * call recorded (may exceed max_stages); RLC mode accepted for the G1-signature
+ * schemes; DGPU_MAX_STAGES 32. */
+#define DGPU_ABI_VERSION 3
 
 /* scheme IDs (common/scheme/scheme.go:9,12; bls-unchained-on-g1 added by this build) */
 enum {
@@ -196,8 +208,8 @@ int dgpu_verify_batch(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *round
 
 /* Same contract with every array already resident in device memory of the
  * context's GPU (d_* are device pointers) and work enqueued on `stream`
- * (a hipStream_t, NULL = the context's stream).  Asynchronous: results are
- * valid after the stream synchronizes. */
+ * (a hipStream_t, NULL = the legacy default stream).  Asynchronous: results
+ * are valid after the stream synchronizes (or dgpu_synchronize returns). */
 int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t *d_rounds, const uint8_t *d_sigs,
                              size_t sig_stride, const uint32_t *d_sig_len, const uint8_t *d_prev,
                              size_t prev_stride, const uint32_t *d_prev_len, int mode, uint64_t rlc_seed,
@@ -220,6 +232,9 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
  * library's event pool holds makes dgpu_stage_times fail (DGPU_EINVAL)
  * instead of reporting partial sums. */
 #define DGPU_MAX_STAGES 32
+/* Block until every call made so far on the context has finished on the
+ * device (its results are then valid on the host and on any stream). */
+int dgpu_synchronize(dgpu_ctx *ctx);
 int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
 
@@ -288,7 +303,7 @@ int dgpu_recover_batch(dgpu_ctx *ctx, size_t n_rounds, const uint8_t *msgs32, si
                        uint8_t *partial_valid);
 
 /* dgpu_recover_batch over device buffers already resident in HBM, enqueued on
- * `stream` (hipStream_t; NULL = the context's stream) without host
+ * `stream` (hipStream_t; NULL = the legacy default stream) without host
  * synchronisation.  d_ok: n_rounds bytes (1 = recovered); d_status
  * (optional): n_rounds*m bytes, DGPU_REASON_* of every partial (0 = verified).
  * A partial_len above partial_stride reads as an invalid partial. */

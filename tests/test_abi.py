@@ -24,7 +24,7 @@ def test_library_exports_all_symbols():
     lib = _lib.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.dgpu_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.dgpu_abi_version() == _lib.ABI_VERSION == 3
     assert lib.dgpu_scheme_from_name(b"") == _lib.SCHEME_CHAINED
     assert lib.dgpu_scheme_from_name(b"pedersen-bls-unchained") == _lib.SCHEME_UNCHAINED
     assert lib.dgpu_scheme_from_name(b"bls-unchained-on-g1") == _lib.SCHEME_UNCHAINED_G1

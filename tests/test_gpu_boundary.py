@@ -1,4 +1,4 @@
-"""GPU tests of the C-ABI boundary (include/drand_gpu.h, ABI 2) beyond the
+"""GPU tests of the C-ABI boundary (include/drand_gpu.h, ABI 3) beyond the
 per-round verdicts of test_gpu_parity.py:
 
   * raw-message surface (key.Scheme.VerifyRecovered / AuthScheme with any msg,
@@ -175,8 +175,9 @@ def test_rlc_localize_then_confirm_and_fallback(gpu_ctx):
     got, st = rlc_stages(beacons, c.pk)
     assert got.tolist() == per.tolist()
     assert {"rlc_plain_tree", "rlc_confirm"} <= st and "rlc_leaves_tree" not in st, st
-    # +D / -D in rounds 137 and 138: one level-5 node of the plain tree, the
-    # first level the descent checks for a batch above 64Ki rounds
+    # +D / -D in rounds 137 and 138: one level-3 node (rounds 136..143) of
+    # the plain tree, the first level the descent checks for a batch above
+    # 64Ki rounds (descent step 3: 70,000 -> 8,750 nodes)
     c2 = make_chain(46, 70000, _lib.SCHEME_CHAINED, seg_len=64)
     b2 = [c2.beacon(i) for i in range(len(c2))]
     s = B.g2_decompress(b2[137].signature)
@@ -312,7 +313,8 @@ def test_async_calls_on_two_streams_are_ordered(gpu_ctx):
         t = [torch.from_numpy(a).to(dev) for a in (c.rounds.view(np.int64), c.sigs, c.sig_len.view(np.int32), c.prev,
                                                   c.prev_len.view(np.int32))]
         torch.cuda.synchronize()
-        bits = torch.zeros((len(c) + 7) // 8, dtype=torch.uint8, device=dev)
+        with torch.cuda.stream(st):  # zero-filled in the order of the stream the library runs on
+            bits = torch.zeros((len(c) + 7) // 8, dtype=torch.uint8, device=dev)
         pk = np.frombuffer(c.pk, dtype=np.uint8).copy()
         keep.append((t, pk))
         _lib.check(gpu_ctx.lib.dgpu_verify_beacons_device(
@@ -326,3 +328,40 @@ def test_async_calls_on_two_streams_are_ordered(gpu_ctx):
         expect = np.ones(len(c), dtype=bool)
         expect[list(bad.keys())] = False
         assert np.array_equal(got, expect)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_null_stream_is_the_default_stream(mode, gpu_ctx):
+    """ABI 3 stream contract: a NULL stream is the legacy
+    default stream, so outputs torch fills on its default stream before the
+    call and reads after it are ordered with the library's work -- no
+    synchronize anywhere.  Outputs are pre-filled with a pattern the verdict
+    packing never leaves (0xA5), inputs are copied with non_blocking H2D on
+    the default stream; per-round and RLC mode (a 70k batch, above the RLC
+    threshold), verdicts and reasons equal construction."""
+    import ctypes
+    import torch
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    dev = torch.device("cuda", 0)
+    assert torch.cuda.current_stream(dev).cuda_stream == 0
+    c = make_chain(81, 70001, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 81, rate=1e-3)
+    n = len(c)
+    t = [torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)
+         for a in (c.rounds.view(np.int64), c.sigs, c.sig_len.view(np.int32), c.prev, c.prev_len.view(np.int32))]
+    bits = torch.full(((n + 7) // 8,), 0xA5, dtype=torch.uint8, device=dev)
+    reason = torch.full((n,), 0xA5, dtype=torch.uint8, device=dev)
+    pk = np.frombuffer(c.pk, dtype=np.uint8).copy()
+    _lib.check(gpu_ctx.lib.dgpu_verify_beacons_device(
+        gpu_ctx.handle, _lib.SCHEME_CHAINED, _lib.ptr(pk), pk.size, n, t[0].data_ptr(), t[1].data_ptr(), 96,
+        t[2].data_ptr(), t[3].data_ptr(), 96, t[4].data_ptr(), mode, 12345, bits.data_ptr(), reason.data_ptr(),
+        ctypes.c_void_p(None)))
+    got = np.unpackbits(bits.cpu().numpy(), bitorder="little")[:n].astype(bool)
+    r = reason.cpu().numpy()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(got, expect)
+    assert np.array_equal(r == 0, expect) and set(np.unique(r)) <= {0, 1, 2, 3, 4}
+    # dgpu_synchronize: the host-side wait a caller without HIP (cgo) uses
+    _lib.check(gpu_ctx.lib.dgpu_synchronize(gpu_ctx.handle))

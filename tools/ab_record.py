@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Collect an A/B session's bench lines (tools/gpu/r02_ab2.sh) and engine op
+"""Collect an A/B session's bench lines (tools/gpu/session.sh ab) and engine op
 microbench lines into one record: ab_record.py DIR WHAT OUT.json"""
 import glob
 import json

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarize A/B bench lines written by tools/gpu/r03_kb.sh (ab_<name>_<rep>.json):
+"""Summarize A/B bench lines written by tools/gpu/session.sh ab (ab_<name>.json):
 rounds/s and the engine/hash stage times per variant and repetition.
 
     python tools/ab_summary.py gpurun_out/<tag>

@@ -86,6 +86,9 @@ def parse(argv=None):
                     help="abi driver: comma-separated device list (default 0..N-1; a repeated device needs "
                          "DGPU_MULTI_ALLOW_SAME_DEVICE=1)")
     ap.add_argument("--abi-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-small-batch", action="store_true", help="skip the small-batch latency leg")
+    ap.add_argument("--small-batch-only", action="store_true",
+                    help="only the small-batch latency leg (host records, n = 1 .. 4096) on a 4096-round chain")
     ap.add_argument("--dry-run", action="store_true",
                     help="print the chosen driver, the rank count and each rank's shard, touch no GPU")
     return ap.parse_args(argv)
@@ -400,6 +403,77 @@ def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
     return res
 
 
+# ---------------------------------------------------------------- latency callers
+SMALL_BATCH_SIZES = (1, 8, 64, 500, 4096)
+
+
+def small_batch_leg(chain, scheme, sizes=SMALL_BATCH_SIZES, budget_s=20.0):
+    """The latency-bound callers: tryNode verifies a peer stream buffered
+    MaxSyncBuffer = 500 beacons deep (net/client_grpc.go:220, verify at
+    chain/beacon/sync_manager.go:397), the client walk verifies a fetched
+    range (client/verify.go:149-169), the gossip validator one beacon per
+    message (lp2p/client/validator.go:64-66).  Each size n: wall time of one
+    dgpu_verify_beacons call on n host records (H2D, verify, D2H; the
+    library's default kernel thresholds), median and p90 over repeated calls,
+    beside the C port's single-core time for the same n beacons (the
+    reference's loops are one goroutine).  The crossover is the smallest n
+    where the GPU call beats the single core."""
+    from drand_amd import _lib
+    from drand_amd.chain import get_context
+    ctx = get_context(0)
+    lib = ctx.lib
+    code = lib.dgpu_scheme_from_name(scheme.encode())
+    pk = np.frombuffer(chain.pk, dtype=np.uint8).copy()
+    cpu_ms_per_round = None
+    try:
+        from oracle import c_ref
+        c_ref.load()
+        k = 8
+        sub = [np.ascontiguousarray(a[:k]) for a in (chain.rounds, chain.sigs, chain.sig_len, chain.prev,
+                                                     chain.prev_len)]
+        c_ref.verify_batch(code == _lib.SCHEME_CHAINED, chain.pk, *sub, 1)  # warm
+        t0 = time.perf_counter()
+        c_ref.verify_batch(code == _lib.SCHEME_CHAINED, chain.pk, *sub, 1)
+        cpu_ms_per_round = (time.perf_counter() - t0) * 1e3 / k
+    except Exception as e:  # reported, never fatal
+        log(f"small-batch: no C port timing ({e!r})")
+    rows = []
+    per_size = budget_s / len(sizes)
+    for n in sizes:
+        n = min(n, len(chain))
+        cols = [np.ascontiguousarray(a[:n]) for a in (chain.rounds, chain.sigs, chain.sig_len, chain.prev,
+                                                        chain.prev_len)]
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+
+        def call():
+            _lib.check(lib.dgpu_verify_beacons(ctx.handle, code, _lib.ptr(pk), pk.size, n, _lib.ptr(cols[0]),
+                                               _lib.ptr(cols[1]), 96, _lib.ptr(cols[2]), _lib.ptr(cols[3]), 96,
+                                               _lib.ptr(cols[4]), _lib.MODE_PER_ROUND, 0, _lib.ptr(bits), None))
+        for _ in range(3):  # buffers sized, kernels loaded
+            call()
+        ts = []
+        t_end = time.perf_counter() + per_size
+        while len(ts) < 5 or (time.perf_counter() < t_end and len(ts) < 200):
+            t0 = time.perf_counter()
+            call()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        ts.sort()
+        row = {"n": n, "gpu_ms_median": ts[len(ts) // 2], "gpu_ms_p90": ts[int(len(ts) * 0.9)], "calls": len(ts),
+               "gpu_rounds_per_s": n / (ts[len(ts) // 2] * 1e-3)}
+        if cpu_ms_per_round:
+            row["cpu_1core_ms"] = n * cpu_ms_per_round
+            row["gpu_faster"] = row["gpu_ms_median"] < row["cpu_1core_ms"]
+        rows.append(row)
+        log(f"small-batch n={n}: {row['gpu_ms_median']:.2f} ms")
+    cross = next((r["n"] for r in rows if r.get("gpu_faster")), None)
+    return {"api": "dgpu_verify_beacons (host records, per-round mode, default thresholds)", "scheme": scheme,
+            "rows": rows, "cpu_1core_ms_per_round": cpu_ms_per_round,
+            "cpu_kind": "port (oracle/c/bls381_ref.c, one thread; kilic's x86 asm is not available here)",
+            "crossover_n": cross,
+            "callers": "tryNode windows of <= 500 (net/client_grpc.go:220), gossip validator 1 per message "
+                       "(lp2p/client/validator.go:64-66)"}
+
+
 # ---------------------------------------------------------------- check-chain ingest (SURVEY 8(f) row 2)
 def _hex_rows(a, lens):
     """numpy (n, stride) bytes -> lowercase hex of each row's first lens[i] bytes"""
@@ -582,6 +656,11 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
                                    "bisection (dgpu_verify_beacons_device mode DGPU_MODE_RLC)")}
         log(f"rlc: {res['rlc']['value']:.0f} rounds/s")
 
+    if main and rank == 0 and world == 1 and not args.no_small_batch:
+        try:
+            res["small_batch"] = small_batch_leg(chain, scheme)
+        except Exception as e:  # reported, never fatal
+            res["small_batch"] = {"error": repr(e)}
     if main and rank == 0 and world == 1 and not args.no_ingest:
         _EXPECT[id(chain)] = {gi - lo: False for gi in bad if lo <= gi < hi}
         try:
@@ -752,6 +831,7 @@ def main_verify(args, world, rank, local):
         "end_to_end": main.get("end_to_end"),
         "rlc": main.get("rlc"),
         "ingest": main.get("ingest"),
+        "small_batch": main.get("small_batch"),
         "roofline": main.get("roofline"),
         "cpu_baseline": main.get("cpu_baseline"),
     }
@@ -828,6 +908,14 @@ def main():
         return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
+    if args.small_batch_only:
+        from drand_amd import _lib
+        from drand_amd.synth import corrupt, make_chain
+        code = _lib.load().dgpu_scheme_from_name(args.scheme.encode())
+        ch = make_chain(args.seed, max(SMALL_BATCH_SIZES), code, seg_len=args.seg_len)
+        corrupt(ch, args.seed, rate=args.corrupt_rate)
+        print(json.dumps(small_batch_leg(ch, args.scheme)), flush=True)
+        return
     if os.environ.get("DRAND_BENCH_DRYRUN"):
         return dryrun(args)
     import torch

@@ -198,6 +198,7 @@ struct dgpu_ctx {
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
   bool kb_split = false;         // DGPU_KB_DEC=split: norms + decompression parts at the chain's snaps, per-thread inversion (A/B)
+  bool kb_norm_chain = false;    // DGPU_KB_NORM=chain: the per-thread chain writes the six norms (A/B)
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
   int rlc_descent_step = 3;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step; r04g: 3 > 2 > 5)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
@@ -852,14 +853,21 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
                            (const uint32_t*)ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
         HIP_TRY(hipGetLastError());
       } else {
-        if (kb_thread)
-          hipLaunchKernelGGL(k_kb_chain_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf);
+        const bool norm_pre = kb_thread && c->kb_norm_chain;
+        if (norm_pre)
+          hipLaunchKernelGGL(k_kb_chain_thr<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
+        else if (kb_thread)
+          hipLaunchKernelGGL(k_kb_chain_thr<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, nullptr);
         else
           hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
         HIP_TRY(hipGetLastError());
         mark(c, s, "eng_fe_kbinv");
-        hipLaunchKernelGGL(k_eng_kb_norm, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, (const uint32_t*)xbuf,
-                           pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+        if (norm_pre)
+          hipLaunchKernelGGL(k_eng_kb_norm<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
+                             (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+        else
+          hipLaunchKernelGGL(k_eng_kb_norm<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
+                             (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
         HIP_TRY(hipGetLastError());
@@ -1270,6 +1278,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
   const char* kdv = getenv("DGPU_KB_DEC");
   if (kdv && !strcmp(kdv, "split")) c->kb_split = true;
+  const char* knv = getenv("DGPU_KB_NORM");
+  if (knv) c->kb_norm_chain = !strcmp(knv, "chain");
   const char* rds = getenv("DGPU_RLC_DESCENT_STEP");
   if (rds && atoi(rds) >= 1 && atoi(rds) <= 8) c->rlc_descent_step = atoi(rds);
   const char* rlv = getenv("DGPU_RLC_LOCALIZE");

@@ -89,24 +89,21 @@ namespace dgpu {
 #endif
 // Fp2 components (comp, comp + 1; comp even) of round i's plane: one dwordx2 per limb.
 __device__ __forceinline__ fp2 kb_ld_thr(const uint32_t* xbuf, size_t i, int plane, int comp) {
-  const uint32_t* b = xbuf + kb_off(i, plane, comp);
-  fp2 v;
-#pragma unroll
-  for (int l = 0; l < FP_LIMBS; ++l) {
-    const uint2 w = *reinterpret_cast<const uint2*>(b + l * ENG_WAVE_WORDS);
-    v.c0.l[l] = w.x, v.c1.l[l] = w.y;
-  }
-  return v;
+  return kb_ld2(xbuf, i, plane, comp);
 }
 __device__ __forceinline__ void kb_st_thr(uint32_t* xbuf, size_t i, int plane, int comp, const fp2& v) {
-  uint32_t* b = xbuf + kb_off(i, plane, comp);
-#pragma unroll
-  for (int l = 0; l < FP_LIMBS; ++l) *reinterpret_cast<uint2*>(b + l * ENG_WAVE_WORDS) = make_uint2(v.c0.l[l], v.c1.l[l]);
+  kb_st2(xbuf, i, plane, comp, v);
 }
 
 // Thread = round i of the chunk: m from plane M, the six stored values to
 // planes X0.. (components 2..5, 8..11: f1, f2, f4, f5), dwordx2 per Fp2 limb.
-__global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt, uint32_t* __restrict__ xbuf) {
+// NORM (DGPU_KB_NORM=chain): at each snap also Norm(4 f1) of the stored value
+// -> nbuf ([j][limb][cnt], round-fastest, coalesced), so k_eng_kb_norm_pre
+// reads 6 x 56 B per round instead of the values' f1 halves from the blocked
+// planes.
+template <bool NORM>
+__global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt, uint32_t* __restrict__ xbuf,
+                                                                     uint32_t* __restrict__ nbuf) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cnt) return;
   kb_chain_thr(kb_ld_thr(xbuf, i, ENG_KB_PL_M, 2), kb_ld_thr(xbuf, i, ENG_KB_PL_M, 4),
@@ -117,6 +114,7 @@ __global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt,
                  kb_st_thr(xbuf, i, pl, 4, f2);
                  kb_st_thr(xbuf, i, pl, 8, f4);
                  kb_st_thr(xbuf, i, pl, 10, f5);
+                 if constexpr (NORM) st_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i, eng_kb_norm(f1));
                });
 }
 

@@ -40,46 +40,80 @@ DG_FN fp2 lt_sub32_nr(const fp2& a, const fp2& b) {
   return fp2{fp_norm(fp_sub2_lz(a.c0, b.c0)), fp_norm(fp_sub2_lz(a.c1, b.c1))};
 }
 
-DG_FN line3 lt_dbl(g2p& T, const fp& nxp, const fp& yp) {
+// Each coefficient is handed to emit(k, value) (k = 0: c0, 1: c2, 2: c3) as
+// soon as it is formed, and the statements run in the order that ends the
+// most live ranges first (old X, then Y and Z, then the temporaries), so a
+// step's line never waits in registers for the step's end: the kernel's
+// stores retire each coefficient at once (the spilled
+// live set of k_lines_thr).  Same operations and bounds as before.
+template <class Emit>
+DG_FN void lt_dbl_p(g2p& T, const fp& nxp, const fp& yp, Emit&& emit) {
   const fp2 t0 = fp2_sqr(T.y);
-  const fp2 t1 = fp2_sqr(T.z);
   const fp2 x2 = fp2_sqr(T.x);
-  const fp2 yz2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.y, T.z))), fp2_add_lz(t0, t1));
   const fp2 xy2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.x, T.y))), fp2_add_lz(x2, t0));
+  emit(1, fp2_mul_fp(fp2_carry(fp2_add_lz(fp2_add_lz(x2, x2), x2)), nxp));
+  const fp2 t1 = fp2_sqr(T.z);
+  const fp2 yz2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.y, T.z))), fp2_add_lz(t0, t1));
+  emit(2, fp2_mul_fp(yz2, yp));
   const fp2 xt1 = fp2_carry(fp2{fp_sub_lz(t1.c0, t1.c1), fp_add_lz(t1.c0, t1.c1)});
   const fp2 t2 = fp2{fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c0)), fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c1))};
-  const fp2 t3 = fp2_carry(fp2_add_lz(fp2_add_lz(t2, t2), t2));
-  line3 l;
-  l.c0 = fp2_sub(t0, t2);
-  l.c2 = fp2_mul_fp(fp2_carry(fp2_add_lz(fp2_add_lz(x2, x2), x2)), nxp);
-  l.c3 = fp2_mul_fp(yz2, yp);
-  const fp2 t2sq = fp2_sqr(t2);
-  T.x = fp2_mul(xy2, fp2_carry(fp2{fp_sub_lz(t0.c0, t3.c0), fp_sub_lz(t0.c1, t3.c1)}));
-  T.y = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(t0, t3))), fp2_carry(fp2_mulk_lz(t2sq, 12)));
+  emit(0, fp2_sub(t0, t2));
   T.z = fp2_mul(fp2_carry(fp2_mulk_lz(t0, 4)), yz2);
-  return l;
+  const fp2 t3 = fp2_carry(fp2_add_lz(fp2_add_lz(t2, t2), t2));
+  T.x = fp2_mul(xy2, fp2_carry(fp2{fp_sub_lz(t0.c0, t3.c0), fp_sub_lz(t0.c1, t3.c1)}));
+  const fp2 t2sq = fp2_sqr(t2);
+  T.y = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(t0, t3))), fp2_carry(fp2_mulk_lz(t2sq, 12)));
 }
 
 // Mixed addition T + Q (Q affine) with its chord line (pairing.cuh
-// miller_add_step's formulas; 5 of the 68 steps).
-DG_FN line3 lt_add(g2p& T, const g2a& Q, const fp& nxp, const fp& yp) {
+// miller_add_step's formulas; 5 of the 68 steps), coefficients emitted early.
+template <class Emit>
+DG_FN void lt_add_p(g2p& T, const g2a& Q, const fp& nxp, const fp& yp, Emit&& emit) {
   const fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
   const fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
+  emit(1, fp2_mul_fp(theta, nxp));
+  emit(2, fp2_mul_fp(lam, yp));
+  emit(0, fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y)));
   const fp2 C = fp2_sqr(theta);
   const fp2 D = fp2_sqr(lam);
   const fp2 E = fp2_mul(lam, D);
   const fp2 F = fp2_mul(T.z, C);
   const fp2 G = fp2_mul(T.x, D);
   const fp2 H = fp2_sub(fp2_add(E, F), fp2_dbl(G));
-  line3 l;
-  l.c0 = fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y));
-  l.c2 = fp2_mul_fp(theta, nxp);
-  l.c3 = fp2_mul_fp(lam, yp);
   const fp2 ye = fp2_mul(T.y, E);
   T.x = fp2_mul(lam, H);
   T.y = fp2_sub(fp2_mul(theta, fp2_sub(G, H)), ye);
   T.z = fp2_mul(T.z, E);
+}
+
+// The same steps returning the whole line (host emulation, tests).
+DG_FN line3 lt_dbl(g2p& T, const fp& nxp, const fp& yp) {
+  line3 l;
+  lt_dbl_p(T, nxp, yp, [&](int k, const fp2& v) { (k == 0 ? l.c0 : k == 1 ? l.c2 : l.c3) = v; });
   return l;
+}
+DG_FN line3 lt_add(g2p& T, const g2a& Q, const fp& nxp, const fp& yp) {
+  line3 l;
+  lt_add_p(T, Q, nxp, yp, [&](int k, const fp2& v) { (k == 0 ? l.c0 : k == 1 ? l.c2 : l.c3) = v; });
+  return l;
+}
+
+// One pair's 68 T-steps with the coefficients emitted one by one:
+// emit(step, k, value); returns the final T = [|x|] Q.
+template <class Emit>
+DG_FN g2p lt_pair_p(const g2a& Q, const fp& nxp, const fp& yp, Emit&& emit) {
+  g2p T{Q.x, Q.y, fp2_one()};
+  int step = 0;
+#pragma unroll 1
+  for (int i = 62; i >= 0; --i) {
+    lt_dbl_p(T, nxp, yp, [&](int k, const fp2& v) { emit(step, k, v); });
+    ++step;
+    if ((BLS_X_ABS >> i) & 1ull) {
+      lt_add_p(T, Q, nxp, yp, [&](int k, const fp2& v) { emit(step, k, v); });
+      ++step;
+    }
+  }
+  return T;
 }
 
 // One pair's 68 T-steps (63 doublings, additions at the 5 lower set bits of
@@ -151,15 +185,10 @@ __global__ void __launch_bounds__(256, DG_LINES_OCC) k_lines_thr(size_t n, size_
   }
   const size_t blk = i / ENG_ROUNDS_PER_BLOCK;
   uint32_t* base = lines + eng_blk_off(blk, ENG_LINE_STEPS, 0, (int)(i % ENG_ROUNDS_PER_BLOCK), 6 * p);
-  const g2p T = lt_pair(Q, nxp, yp, [&](int step, const line3& l) {
-    uint32_t* b = base + (size_t)step * FP_LIMBS * ENG_WAVE_WORDS;
+  const g2p T = lt_pair_p(Q, nxp, yp, [&](int step, int k, const fp2& v) {
+    uint2* b = reinterpret_cast<uint2*>(base + (size_t)step * FP_LIMBS * ENG_WAVE_WORDS) + k;
 #pragma unroll
-    for (int k = 0; k < FP_LIMBS; ++k) {
-      uint2* w = reinterpret_cast<uint2*>(b + k * ENG_WAVE_WORDS);
-      w[0] = make_uint2(l.c0.c0.l[k], l.c0.c1.l[k]);
-      w[1] = make_uint2(l.c2.c0.l[k], l.c2.c1.l[k]);
-      w[2] = make_uint2(l.c3.c0.l[k], l.c3.c1.l[k]);
-    }
+    for (int l = 0; l < FP_LIMBS; ++l) b[l * (ENG_WAVE_WORDS / 2)] = make_uint2(v.c0.l[l], v.c1.l[l]);
   });
   if (status && p == 1 && !lt_in_g2(T, Q) && status[r] == ST_OK) status[r] = ST_SUBGROUP;
 }

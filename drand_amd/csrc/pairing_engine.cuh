@@ -323,8 +323,25 @@ __device__ __forceinline__ size_t kb_off(size_t i, int plane, int comp) {
   const int g = (int)(i - blk * ENG_ROUNDS_PER_BLOCK);
   return (blk * ENG_KB_PLANES + plane) * FP_LIMBS * ENG_WAVE_WORDS + g * 12 + comp;
 }
+// Fp2 components (comp, comp + 1; comp even) of round i's plane: one dwordx2
+// per limb (8-byte aligned: g * 48 + comp * 4 bytes).  The per-thread
+// kernels' accesses; 4-byte loads of each component let a wave's loads of one
+// value spread over L2 long enough to be evicted between components (r04q:
+// k_eng_kb_norm fetched 22 KB per round for 2.7 KB of f1 values).
 __device__ __forceinline__ fp2 kb_ld2(const uint32_t* xbuf, size_t i, int plane, int comp) {
-  return fp2{ld_blk(xbuf, kb_off(i, plane, comp)), ld_blk(xbuf, kb_off(i, plane, comp + 1))};
+  const uint32_t* b = xbuf + kb_off(i, plane, comp);
+  fp2 v;
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) {
+    const uint2 w = *reinterpret_cast<const uint2*>(b + l * ENG_WAVE_WORDS);
+    v.c0.l[l] = w.x, v.c1.l[l] = w.y;
+  }
+  return v;
+}
+__device__ __forceinline__ void kb_st2(uint32_t* xbuf, size_t i, int plane, int comp, const fp2& v) {
+  uint32_t* b = xbuf + kb_off(i, plane, comp);
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) *reinterpret_cast<uint2*>(b + l * ENG_WAVE_WORDS) = make_uint2(v.c0.l[l], v.c1.l[l]);
 }
 
 // Segment [off, off + len) of ENG_PROG_FEK (gen_engine.py prog_fe_kb) on the
@@ -426,7 +443,10 @@ __global__ void __launch_bounds__(64, DG_KB_CHAIN_OCC) k_eng_kb_chain(size_t cnt
 // has already failed: its verdict stands); 1 stands in for it.  flag_every
 // (test mode, DGPU_KB_TEST_FLAG): also flag every item i with
 // i % flag_every == 0, so the fallback runs.
-__global__ void __launch_bounds__(256) k_eng_kb_norm(size_t cnt, size_t r0, const uint32_t* __restrict__ xbuf,
+// PRE (DGPU_KB_NORM=chain): the chain already wrote the norms into ebuf's
+// planes (k_kb_chain_thr<true>); each thread reads its six before writing E_j.
+template <bool PRE>
+__global__ void __launch_bounds__(256, 2) k_eng_kb_norm(size_t cnt, size_t r0, const uint32_t* __restrict__ xbuf,
                                                      uint32_t* __restrict__ pbuf, uint32_t* __restrict__ ebuf,
                                                      uint8_t* __restrict__ flags, const uint8_t* __restrict__ status,
                                                      size_t flag_every) {
@@ -436,7 +456,10 @@ __global__ void __launch_bounds__(256) k_eng_kb_norm(size_t cnt, size_t r0, cons
   bool zero = flag_every && i % flag_every == 0;
 #pragma unroll
   for (int j = 0; j < ENG_KB_NSNAP; ++j) {
-    nrm[j] = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
+    if constexpr (PRE)
+      nrm[j] = ld_soa(ebuf + (size_t)j * FP_LIMBS * cnt, cnt, i);
+    else
+      nrm[j] = eng_kb_norm(kb_ld2(xbuf, i, ENG_KB_PL_X0 + j, 2));
     if (fp_is_zero(nrm[j])) {
       nrm[j] = fp_one();
       zero = true;
@@ -481,10 +504,8 @@ __global__ void __launch_bounds__(256, DG_KB_DEC_OCC) k_eng_kb_dec(size_t cnt, u
   fp2 f0, f3;
   eng_kb_decompress(kb_ld2(xbuf, i, pl, 2), kb_ld2(xbuf, i, pl, 4), kb_ld2(xbuf, i, pl, 8), kb_ld2(xbuf, i, pl, 10),
                     ninv, f0, f3);
-  st_blk(xbuf, kb_off(i, pl, 0), f0.c0);
-  st_blk(xbuf, kb_off(i, pl, 1), f0.c1);
-  st_blk(xbuf, kb_off(i, pl, 6), f3.c0);
-  st_blk(xbuf, kb_off(i, pl, 7), f3.c1);
+  kb_st2(xbuf, i, pl, 0, f0);
+  kb_st2(xbuf, i, pl, 6, f3);
 }
 
 }  // namespace dgpu

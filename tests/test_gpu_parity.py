@@ -276,7 +276,9 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     re-run on prog_fe by k_eng_fe_fb) -- the fallback otherwise practically
     never runs -- with the 8-lane compressed chain (DGPU_KB_CHAIN=lanes)
     in place of the per-thread one, and with the decompression split at the
-    inversion (DGPU_KB_DEC=split; fallback forced and not).  20,011 rounds (a ragged last block), 1%
+    inversion (DGPU_KB_DEC=split; fallback forced and not), and with the norms
+    written by the chain or read from the planes (DGPU_KB_NORM, fallback
+    forced).  20,011 rounds (a ragged last block), 1%
     corrupted: identical reasons, equal to the construction."""
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
@@ -289,7 +291,11 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     lanes = _verify_with_env(c, {"DGPU_KB_CHAIN": "lanes"})
     split = _verify_with_env(c, {"DGPU_KB_DEC": "split"})
     split_fb = _verify_with_env(c, {"DGPU_KB_DEC": "split", "DGPU_KB_TEST_FLAG": "7"})
+    # the six norms from the chain's snaps (DGPU_KB_NORM=chain) or from the planes
+    norm_chain = _verify_with_env(c, {"DGPU_KB_NORM": "chain", "DGPU_KB_TEST_FLAG": "7"})
+    norm_planes = _verify_with_env(c, {"DGPU_KB_NORM": "planes", "DGPU_KB_TEST_FLAG": "7"})
     assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist() == split.tolist() == split_fb.tolist()
+    assert norm_chain.tolist() == norm_planes.tolist() == kb.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(kb == 0, expect)

@@ -51,10 +51,13 @@ run_step() {
     TAG=$TAG/pmc PROF_ARGS="${TRAFFIC_ARGS:---rounds 131072 --iters 1}" bash tools/gpu/pmc.sh > $O/pmc.log 2>&1 ;;
   ab)
     mkdir -p $O/ab
+    # a variant is lib.so or lib.so@KEY=VALUE (an environment knob read at dgpu_open)
     for v in $VARIANTS; do
-      name=$(basename $v .so)
-      DRAND_GPU_LIB=$PWD/$v timeout -k 10 600 python bench.py --no-cpu-baseline ${BENCH_ARGS} \
-        > $O/ab/ab_$name.json 2> $O/ab/ab_$name.err || return $?
+      lib=${v%%@*}; kv=$([ "$lib" != "$v" ] && echo "${v#*@}")
+      name=$(basename $lib .so)$([ -n "$kv" ] && echo "_${kv//=/_}")
+      ( [ -n "$kv" ] && export "$kv"
+        DRAND_GPU_LIB=$PWD/$lib timeout -k 10 600 python bench.py --no-cpu-baseline ${BENCH_ARGS} \
+          > $O/ab/ab_$name.json 2> $O/ab/ab_$name.err ) || return $?
     done
     python3 tools/ab_summary.py $O/ab ;;
   small)

@@ -46,15 +46,26 @@ DG_FN fp2 lt_sub32_nr(const fp2& a, const fp2& b) {
 // step's line never waits in registers for the step's end: the kernel's
 // stores retire each coefficient at once (the spilled
 // live set of k_lines_thr).  Same operations and bounds as before.
-template <class Emit>
-DG_FN void lt_dbl_p(g2p& T, const fp& nxp, const fp& yp, Emit&& emit) {
+// The pair's G1 point (-x_P, y_P) as held in registers (lt_pt_val) or
+// reloaded from memory at each use (lt_pt_mem: DG_LINES_PT_RELOAD, which frees
+// 28 VGPRs of the T-step loop; an empty asm on the address keeps the loads in
+// the loop).
+struct lt_pt_val {
+  fp nx_, y_;
+  DG_FN fp nx() const { return nx_; }
+  DG_FN fp y() const { return y_; }
+};
+
+template <class PT, class Emit>
+DG_FN void lt_dbl_p(g2p& T, const PT& P, Emit&& emit) {
+  const fp nxp = P.nx();
   const fp2 t0 = fp2_sqr(T.y);
   const fp2 x2 = fp2_sqr(T.x);
   const fp2 xy2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.x, T.y))), fp2_add_lz(x2, t0));
   emit(1, fp2_mul_fp(fp2_carry(fp2_add_lz(fp2_add_lz(x2, x2), x2)), nxp));
   const fp2 t1 = fp2_sqr(T.z);
   const fp2 yz2 = lt_sub32_nr(fp2_sqr(fp2_carry(fp2_add_lz(T.y, T.z))), fp2_add_lz(t0, t1));
-  emit(2, fp2_mul_fp(yz2, yp));
+  emit(2, fp2_mul_fp(yz2, P.y()));
   const fp2 xt1 = fp2_carry(fp2{fp_sub_lz(t1.c0, t1.c1), fp_add_lz(t1.c0, t1.c1)});
   const fp2 t2 = fp2{fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c0)), fp_reduce(fp_norm(fp2_mulk_lz(xt1, 12).c1))};
   emit(0, fp2_sub(t0, t2));
@@ -67,12 +78,12 @@ DG_FN void lt_dbl_p(g2p& T, const fp& nxp, const fp& yp, Emit&& emit) {
 
 // Mixed addition T + Q (Q affine) with its chord line (pairing.cuh
 // miller_add_step's formulas; 5 of the 68 steps), coefficients emitted early.
-template <class Emit>
-DG_FN void lt_add_p(g2p& T, const g2a& Q, const fp& nxp, const fp& yp, Emit&& emit) {
+template <class PT, class Emit>
+DG_FN void lt_add_p(g2p& T, const g2a& Q, const PT& P, Emit&& emit) {
   const fp2 theta = fp2_sub(T.y, fp2_mul(Q.y, T.z));
   const fp2 lam = fp2_sub(T.x, fp2_mul(Q.x, T.z));
-  emit(1, fp2_mul_fp(theta, nxp));
-  emit(2, fp2_mul_fp(lam, yp));
+  emit(1, fp2_mul_fp(theta, P.nx()));
+  emit(2, fp2_mul_fp(lam, P.y()));
   emit(0, fp2_sub(fp2_mul(theta, Q.x), fp2_mul(lam, Q.y)));
   const fp2 C = fp2_sqr(theta);
   const fp2 D = fp2_sqr(lam);
@@ -89,27 +100,35 @@ DG_FN void lt_add_p(g2p& T, const g2a& Q, const fp& nxp, const fp& yp, Emit&& em
 // The same steps returning the whole line (host emulation, tests).
 DG_FN line3 lt_dbl(g2p& T, const fp& nxp, const fp& yp) {
   line3 l;
-  lt_dbl_p(T, nxp, yp, [&](int k, const fp2& v) { (k == 0 ? l.c0 : k == 1 ? l.c2 : l.c3) = v; });
+  lt_dbl_p(T, lt_pt_val{nxp, yp}, [&](int k, const fp2& v) { (k == 0 ? l.c0 : k == 1 ? l.c2 : l.c3) = v; });
   return l;
 }
 DG_FN line3 lt_add(g2p& T, const g2a& Q, const fp& nxp, const fp& yp) {
   line3 l;
-  lt_add_p(T, Q, nxp, yp, [&](int k, const fp2& v) { (k == 0 ? l.c0 : k == 1 ? l.c2 : l.c3) = v; });
+  lt_add_p(T, Q, lt_pt_val{nxp, yp}, [&](int k, const fp2& v) { (k == 0 ? l.c0 : k == 1 ? l.c2 : l.c3) = v; });
   return l;
 }
 
 // One pair's 68 T-steps with the coefficients emitted one by one:
 // emit(step, k, value); returns the final T = [|x|] Q.
-template <class Emit>
-DG_FN g2p lt_pair_p(const g2a& Q, const fp& nxp, const fp& yp, Emit&& emit) {
-  g2p T{Q.x, Q.y, fp2_one()};
+// Q: the pair's affine G2 point as a value (lt_q_val) or reloaded at each
+// addition (DG_LINES_Q_RELOAD).
+struct lt_q_val {
+  g2a q;
+  DG_FN g2a get() const { return q; }
+};
+
+template <class QT, class PT, class Emit>
+DG_FN g2p lt_pair_p(const QT& Qs, const PT& P, Emit&& emit) {
+  const g2a Q0 = Qs.get();
+  g2p T{Q0.x, Q0.y, fp2_one()};
   int step = 0;
 #pragma unroll 1
   for (int i = 62; i >= 0; --i) {
-    lt_dbl_p(T, nxp, yp, [&](int k, const fp2& v) { emit(step, k, v); });
+    lt_dbl_p(T, P, [&](int k, const fp2& v) { emit(step, k, v); });
     ++step;
     if ((BLS_X_ABS >> i) & 1ull) {
-      lt_add_p(T, Q, nxp, yp, [&](int k, const fp2& v) { emit(step, k, v); });
+      lt_add_p(T, Qs.get(), P, [&](int k, const fp2& v) { emit(step, k, v); });
       ++step;
     }
   }
@@ -166,31 +185,64 @@ __global__ void __launch_bounds__(256, DG_LINES_OCC) k_lines_thr(size_t n, size_
   const uint32_t* qb = p ? sig_pts : h_pts;
   const size_t qs = p ? n : h_stride;
   const size_t qi = p ? r : (h_idx ? (size_t)h_idx[r] : r);
-  g2a Q;
-  Q.x.c0 = ld_soa(qb, qs, qi);
-  Q.x.c1 = ld_soa(qb + (size_t)FP_LIMBS * qs, qs, qi);
-  Q.y.c0 = ld_soa(qb + (size_t)2 * FP_LIMBS * qs, qs, qi);
-  Q.y.c1 = ld_soa(qb + (size_t)3 * FP_LIMBS * qs, qs, qi);
-  fp nxp, yp;
-  if (p == 0 && pk_items) {
-    nxp = ld_soa(pk_items, n, r);
-    yp = ld_soa(pk_items + (size_t)FP_LIMBS * n, n, r);
-  } else {
-    const int s0 = (p ? ENG_C_NXP1 : ENG_C_NXP0) - 64;
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) {
-      nxp.l[l] = consts[s0 * ENG_SLOT_WORDS + l];
-      yp.l[l] = consts[(s0 + 1) * ENG_SLOT_WORDS + l];
+#ifdef DG_LINES_Q_RELOAD
+  struct {
+    const uint32_t* qb;
+    size_t qs, qi;
+    DG_FN g2a get() const {
+      const uint32_t* b = qb;
+      asm volatile("" : "+v"(b));  // opaque per use: not hoisted out of the loop
+      g2a Q;
+      Q.x.c0 = ld_soa(b, qs, qi);
+      Q.x.c1 = ld_soa(b + (size_t)FP_LIMBS * qs, qs, qi);
+      Q.y.c0 = ld_soa(b + (size_t)2 * FP_LIMBS * qs, qs, qi);
+      Q.y.c1 = ld_soa(b + (size_t)3 * FP_LIMBS * qs, qs, qi);
+      return Q;
     }
+  } Qs{qb, qs, qi};
+#else
+  lt_q_val Qs;
+  Qs.q.x.c0 = ld_soa(qb, qs, qi);
+  Qs.q.x.c1 = ld_soa(qb + (size_t)FP_LIMBS * qs, qs, qi);
+  Qs.q.y.c0 = ld_soa(qb + (size_t)2 * FP_LIMBS * qs, qs, qi);
+  Qs.q.y.c1 = ld_soa(qb + (size_t)3 * FP_LIMBS * qs, qs, qi);
+#endif
+  // the pair's G1 point: words l * stride of pt (nx) and of pt + ystep (y)
+  const uint32_t* pt;
+  size_t stride, ystep;
+  if (p == 0 && pk_items) {
+    pt = pk_items + r, stride = n, ystep = (size_t)FP_LIMBS * n;
+  } else {
+    pt = consts + ((p ? ENG_C_NXP1 : ENG_C_NXP0) - 64) * ENG_SLOT_WORDS, stride = 1, ystep = ENG_SLOT_WORDS;
   }
   const size_t blk = i / ENG_ROUNDS_PER_BLOCK;
   uint32_t* base = lines + eng_blk_off(blk, ENG_LINE_STEPS, 0, (int)(i % ENG_ROUNDS_PER_BLOCK), 6 * p);
-  const g2p T = lt_pair_p(Q, nxp, yp, [&](int step, int k, const fp2& v) {
+#ifdef DG_LINES_PT_RELOAD
+  struct {
+    const uint32_t* pt;
+    size_t stride, ystep;
+    DG_FN fp ld(size_t off) const {
+      const uint32_t* q = pt + off;
+      asm volatile("" : "+v"(q));  // opaque per use: not hoisted out of the loop
+      fp v;
+#pragma unroll
+      for (int l = 0; l < FP_LIMBS; ++l) v.l[l] = q[l * stride];
+      return v;
+    }
+    DG_FN fp nx() const { return ld(0); }
+    DG_FN fp y() const { return ld(ystep); }
+  } P{pt, stride, ystep};
+#else
+  lt_pt_val P;
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) P.nx_.l[l] = pt[l * stride], P.y_.l[l] = pt[ystep + l * stride];
+#endif
+  const g2p T = lt_pair_p(Qs, P, [&](int step, int k, const fp2& v) {
     uint2* b = reinterpret_cast<uint2*>(base + (size_t)step * FP_LIMBS * ENG_WAVE_WORDS) + k;
 #pragma unroll
     for (int l = 0; l < FP_LIMBS; ++l) b[l * (ENG_WAVE_WORDS / 2)] = make_uint2(v.c0.l[l], v.c1.l[l]);
   });
-  if (status && p == 1 && !lt_in_g2(T, Q) && status[r] == ST_OK) status[r] = ST_SUBGROUP;
+  if (status && p == 1 && !lt_in_g2(T, Qs.get()) && status[r] == ST_OK) status[r] = ST_SUBGROUP;
 }
 #endif
 

@@ -206,6 +206,7 @@ struct dgpu_ctx {
                                  // same-box); DGPU_KB_NORM=planes: k_eng_kb_norm reads f1 from the planes (A/B)
   bool kb_dec_rows = false;      // DGPU_KB_DEC=rows: decompression with whole-row accesses (k_eng_kb_dec_rows, A/B)
   bool kb_dec_soa = false;       // DGPU_KB_DEC=soa: decompression on round-fastest planes (k_eng_kb_dec_soa, A/B)
+  bool kb_dec_image = false;     // DGPU_KB_DEC=image: decompression on a staged LDS image (k_eng_kb_dec_image, A/B)
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
   int rlc_descent_step = 3;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step; r04g: 3 > 2 > 5)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
@@ -890,6 +891,10 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
           hipLaunchKernelGGL(k_eng_kb_dec_soa, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt,
                              (const uint32_t*)xin, dsoa, (const uint32_t*)pbuf, (const uint32_t*)ebuf,
                              (const uint8_t*)flags);
+        else if (c->kb_dec_image)
+          hipLaunchKernelGGL(k_eng_kb_dec_image, dim3(grid_for(capb / ENG_ROUNDS_PER_BLOCK, KB_IMG_BLOCKS), ENG_KB_NSNAP),
+                             dim3(64), 0, s, cnt, capb / ENG_ROUNDS_PER_BLOCK, xbuf, (const uint32_t*)pbuf,
+                             (const uint32_t*)ebuf, (const uint8_t*)flags);
         else if (c->kb_dec_rows)
           hipLaunchKernelGGL(k_eng_kb_dec_rows, dim3(grid_for(capb / ENG_ROUNDS_PER_BLOCK, KB_ROW_BLOCKS), ENG_KB_NSNAP),
                              dim3(64), 0, s, cnt, capb / ENG_ROUNDS_PER_BLOCK, xbuf, (const uint32_t*)pbuf,
@@ -1308,6 +1313,7 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kdv && !strcmp(kdv, "split")) c->kb_split = true;
   if (kdv) c->kb_dec_rows = !strcmp(kdv, "rows");
   if (kdv) c->kb_dec_soa = !strcmp(kdv, "soa");
+  if (kdv) c->kb_dec_image = !strcmp(kdv, "image");
   const char* knv = getenv("DGPU_KB_NORM");
   if (knv) c->kb_norm_chain = strcmp(knv, "planes") != 0;
   const char* rds = getenv("DGPU_RLC_DESCENT_STEP");

@@ -518,6 +518,64 @@ __global__ void __launch_bounds__(256, DG_KB_DEC_OCC) k_eng_kb_dec(size_t cnt, u
   kb_st2(xbuf, i, pl, 6, f3);
 }
 
+// The decompression with the whole image staged at once (DGPU_KB_DEC=image):
+// one wave owns KB_IMG_BLOCKS blocks of one stored value; all 14 limb rows of
+// each block (3,360 contiguous bytes) are read with 16-byte loads into LDS in
+// one phase (every load in flight together), each lane takes its round's
+// f1, f2, f4, f5 from the image, decompresses, patches f0 and f3 into the
+// image, and the wave stores the rows back whole: 4 KB read and 4 KB written
+// per round, full lines, no re-read.  One wave per SIMD (33.6 KB of LDS per
+// wave; 512 VGPRs, no spills).
+constexpr int KB_IMG_BLOCKS = 10;                                   // 50 rounds per wave
+constexpr int KB_IMG_CHUNKS = FP_LIMBS * ENG_WAVE_WORDS / 4;        // 16-byte chunks per block (210)
+__global__ void __launch_bounds__(64, 1) k_eng_kb_dec_image(size_t cnt, size_t nblk, uint32_t* __restrict__ xbuf,
+                                                            const uint32_t* __restrict__ pbuf,
+                                                            const uint32_t* __restrict__ ebuf,
+                                                            const uint8_t* __restrict__ flags) {
+  __shared__ __attribute__((aligned(16))) uint32_t img[KB_IMG_BLOCKS * FP_LIMBS * ENG_WAVE_WORDS];
+  const int lane = threadIdx.x & 63;
+  const size_t j = blockIdx.y;
+  const int pl = ENG_KB_PL_X0 + (int)j;
+  const size_t blk0 = (size_t)blockIdx.x * KB_IMG_BLOCKS;
+  const int nb = (int)min((size_t)KB_IMG_BLOCKS, nblk - blk0);
+  for (int q = lane; q < nb * KB_IMG_CHUNKS; q += 64) {
+    const int r = q / KB_IMG_CHUNKS, off = q - r * KB_IMG_CHUNKS;
+    *reinterpret_cast<uint4*>(img + (size_t)r * FP_LIMBS * ENG_WAVE_WORDS + off * 4) = *reinterpret_cast<const uint4*>(
+        xbuf + ((blk0 + r) * ENG_KB_PLANES + pl) * FP_LIMBS * ENG_WAVE_WORDS + off * 4);
+  }
+  __syncthreads();
+  const int r = lane / ENG_ROUNDS_PER_BLOCK, g = lane - r * ENG_ROUNDS_PER_BLOCK;
+  const size_t i = (blk0 + r) * ENG_ROUNDS_PER_BLOCK + g;
+  const bool act = r < nb && i < cnt && !flags[i];
+  if (act) {
+    uint32_t* w = img + (size_t)r * FP_LIMBS * ENG_WAVE_WORDS + g * 12;
+    fp2 f1, f2, f4, f5;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      const uint32_t* wl = w + l * ENG_WAVE_WORDS;
+      const uint2 a = *reinterpret_cast<const uint2*>(wl + 2), b = *reinterpret_cast<const uint2*>(wl + 4);
+      const uint4 c = *reinterpret_cast<const uint4*>(wl + 8);
+      f1.c0.l[l] = a.x, f1.c1.l[l] = a.y, f2.c0.l[l] = b.x, f2.c1.l[l] = b.y;
+      f4.c0.l[l] = c.x, f4.c1.l[l] = c.y, f5.c0.l[l] = c.z, f5.c1.l[l] = c.w;
+    }
+    const fp ninv = fp_mul(ld_soa(pbuf, cnt, i), ld_soa(ebuf + j * FP_LIMBS * cnt, cnt, i));
+    fp2 f0, f3;
+    eng_kb_decompress(f1, f2, f4, f5, ninv, f0, f3);
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) {
+      uint32_t* wl = w + l * ENG_WAVE_WORDS;
+      *reinterpret_cast<uint2*>(wl) = make_uint2(f0.c0.l[l], f0.c1.l[l]);
+      *reinterpret_cast<uint2*>(wl + 6) = make_uint2(f3.c0.l[l], f3.c1.l[l]);
+    }
+  }
+  __syncthreads();
+  for (int q = lane; q < nb * KB_IMG_CHUNKS; q += 64) {
+    const int rr = q / KB_IMG_CHUNKS, off = q - rr * KB_IMG_CHUNKS;
+    *reinterpret_cast<uint4*>(xbuf + ((blk0 + rr) * ENG_KB_PLANES + pl) * FP_LIMBS * ENG_WAVE_WORDS + off * 4) =
+        *reinterpret_cast<const uint4*>(img + (size_t)rr * FP_LIMBS * ENG_WAVE_WORDS + off * 4);
+  }
+}
+
 // The decompression on round-fastest planes (DGPU_KB_DEC=soa): one thread
 // per stored value j of round i reads f1, f2, f4, f5 from xin (the chain's
 // copy, [j][8][limb][cnt]) and writes f0, f3 to dsoa ([j][4][limb][cnt]),

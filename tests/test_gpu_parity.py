@@ -300,9 +300,10 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     per_value = _verify_with_env(c, {"DGPU_KB_DEC": "values", "DGPU_KB_NORM": "planes"})
     soa = _verify_with_env(c, {"DGPU_KB_DEC": "soa", "DGPU_KB_TEST_FLAG": "7"})
     soa_nf = _verify_with_env(c, {"DGPU_KB_DEC": "soa"})
+    image = _verify_with_env(c, {"DGPU_KB_DEC": "image", "DGPU_KB_TEST_FLAG": "7"})
     assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist() == split.tolist() == split_fb.tolist()
     assert norm_chain.tolist() == norm_planes.tolist() == rows.tolist() == per_value.tolist() == kb.tolist()
-    assert soa.tolist() == soa_nf.tolist() == kb.tolist()
+    assert soa.tolist() == soa_nf.tolist() == image.tolist() == kb.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(kb == 0, expect)

@@ -104,11 +104,7 @@ constexpr size_t ENG_CHUNK_MIN = 16384;
 // values), the product of the six norms + its prefix products (k_eng_inv),
 // the six excluded products, the flag and the fallback list entry
 constexpr size_t ENG_KB_XWORDS = (size_t)ENG_KB_PLANES * 12 * FP_LIMBS;
-// (+ DGPU_KB_DEC=soa: the stored values' f1, f2, f4, f5 and the decompressed
-// f0, f3 as round-fastest planes, 12 Fp per value)
-constexpr size_t ENG_KB_SOA_WORDS = (size_t)ENG_KB_NSNAP * 12 * FP_LIMBS;
-constexpr size_t ENG_KB_BYTES_PER_ROUND =
-    ENG_KB_XWORDS * 4 + (2 + (size_t)ENG_KB_NSNAP) * FP_LIMBS * 4 + ENG_KB_SOA_WORDS * 4 + 1 + 4;
+constexpr size_t ENG_KB_BYTES_PER_ROUND = ENG_KB_XWORDS * 4 + (2 + (size_t)ENG_KB_NSNAP) * FP_LIMBS * 4 + 1 + 4;
 // engine bytes per round and lane: line buffer + f planes + N1 + Karabina state
 constexpr size_t ENG_BYTES_PER_ROUND =
     (size_t)ENG_LINE_STEPS * FP_LIMBS * 12 * 4 + 2 * FP_LIMBS * 12 * 4 + FP_LIMBS * 4 + ENG_KB_BYTES_PER_ROUND;
@@ -203,10 +199,9 @@ struct dgpu_ctx {
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
   bool kb_split = false;         // DGPU_KB_DEC=split: norms + decompression parts at the chain's snaps, per-thread inversion (A/B)
   bool kb_norm_chain = true;     // the per-thread chain writes the six norms (r05c/r05d: kbinv -17%, FE -1.5%
-                                 // same-box); DGPU_KB_NORM=planes: k_eng_kb_norm reads f1 from the planes (A/B)
-  bool kb_dec_rows = false;      // DGPU_KB_DEC=rows: decompression with whole-row accesses (k_eng_kb_dec_rows, A/B)
-  bool kb_dec_soa = false;       // DGPU_KB_DEC=soa: decompression on round-fastest planes (k_eng_kb_dec_soa, A/B)
-  bool kb_dec_image = false;     // DGPU_KB_DEC=image: decompression on a staged LDS image (k_eng_kb_dec_image, A/B)
+                                 // same-box); DGPU_KB_NORM=planes: k_eng_kb_norm reads f1 from the planes (A/B;
+                                 // the row-staged, image and round-fastest decompression variants measured in
+                                 // r05c-r05j, all slower, are in git history)
   bool rlc_localize = true;      // DGPU_RLC_LOCALIZE=0: a failing RLC root goes straight to the random-coefficient tree (A/B)
   int rlc_descent_step = 3;      // DGPU_RLC_DESCENT_STEP: tree levels per descent step (children checked: 2^step; r04g: 3 > 2 > 5)
   bool lines_thread = true;      // DGPU_LINES=engine: T-steps on the 12-lane engine (k_eng_lines, A/B)
@@ -841,13 +836,10 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
   uint32_t* pbuf = xbuf + ENG_KB_XWORDS * capb;
   uint32_t* pre = pbuf + (size_t)FP_LIMBS * capb;
   uint32_t* ebuf = pre + (size_t)FP_LIMBS * capb;
-  uint32_t* xin = ebuf + (size_t)ENG_KB_NSNAP * FP_LIMBS * capb;  // [value][8][limb][cnt] (DGPU_KB_DEC=soa)
-  uint32_t* dsoa = xin + (size_t)ENG_KB_NSNAP * 8 * FP_LIMBS * capb;  // [value][4][limb][cnt]
-  uint32_t* fb = dsoa + (size_t)ENG_KB_NSNAP * 4 * FP_LIMBS * capb;
+  uint32_t* fb = ebuf + (size_t)ENG_KB_NSNAP * FP_LIMBS * capb;
   uint8_t* flags = (uint8_t*)(fb + capb);
   const unsigned blocks = grid_for(cnt, ENG_ROUNDS_PER_BLOCK);
   const size_t inv_threads = std::max<size_t>(1, (cnt + c->kb_inv_chain - 1) / c->kb_inv_chain);
-  const bool soa = c->kb_dec_soa && !c->kb_split;
   constexpr int nseg = (int)(sizeof(ENG_PROG_FEK_OFF) / sizeof(ENG_PROG_FEK_OFF[0])) - 1;
   static_assert(nseg == 6, "segment 0 + one per exponentiation by |x|");
   for (int seg = 0; seg < nseg; ++seg) {
@@ -865,20 +857,15 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
         HIP_TRY(hipGetLastError());
       } else {
         const bool norm_pre = kb_thread && c->kb_norm_chain;
-        if (kb_thread && soa)
-          hipLaunchKernelGGL((k_kb_chain_thr<true, true>), dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf,
-                             xin);
-        else if (norm_pre)
-          hipLaunchKernelGGL((k_kb_chain_thr<true, false>), dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf,
-                             nullptr);
+        if (norm_pre)
+          hipLaunchKernelGGL(k_kb_chain_thr<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
         else if (kb_thread)
-          hipLaunchKernelGGL((k_kb_chain_thr<false, false>), dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf,
-                             nullptr, nullptr);
+          hipLaunchKernelGGL(k_kb_chain_thr<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, nullptr);
         else
           hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
         HIP_TRY(hipGetLastError());
         mark(c, s, "eng_fe_kbinv");
-        if (norm_pre || (kb_thread && soa))
+        if (norm_pre)
           hipLaunchKernelGGL(k_eng_kb_norm<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
                              (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
         else
@@ -887,32 +874,15 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
         HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
         HIP_TRY(hipGetLastError());
-        if (kb_thread && soa)
-          hipLaunchKernelGGL(k_eng_kb_dec_soa, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt,
-                             (const uint32_t*)xin, dsoa, (const uint32_t*)pbuf, (const uint32_t*)ebuf,
-                             (const uint8_t*)flags);
-        else if (c->kb_dec_image)
-          hipLaunchKernelGGL(k_eng_kb_dec_image, dim3(grid_for(capb / ENG_ROUNDS_PER_BLOCK, KB_IMG_BLOCKS), ENG_KB_NSNAP),
-                             dim3(64), 0, s, cnt, capb / ENG_ROUNDS_PER_BLOCK, xbuf, (const uint32_t*)pbuf,
-                             (const uint32_t*)ebuf, (const uint8_t*)flags);
-        else if (c->kb_dec_rows)
-          hipLaunchKernelGGL(k_eng_kb_dec_rows, dim3(grid_for(capb / ENG_ROUNDS_PER_BLOCK, KB_ROW_BLOCKS), ENG_KB_NSNAP),
-                             dim3(64), 0, s, cnt, capb / ENG_ROUNDS_PER_BLOCK, xbuf, (const uint32_t*)pbuf,
-                             (const uint32_t*)ebuf, (const uint8_t*)flags);
-        else
-          hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
+        hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
                              (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
         HIP_TRY(hipGetLastError());
       }
     }
     mark(c, s, "eng_fe");
-    // the stored values' f0, f3 from the round-fastest planes when the
-    // per-thread decompression wrote them there (segments after the first)
-    const bool seg_soa = seg > 0 && soa && c->kb_thread && cnt >= c->thr_min;
     hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
                        ENG_PROG_FEK_OFF[seg + 1] - ENG_PROG_FEK_OFF[seg], seg == 0, seg == nseg - 1, cnt, r0, consts,
-                       (const uint32_t*)f, n1inv, xbuf, flags, fb, st,
-                       seg_soa ? (const uint32_t*)dsoa : (const uint32_t*)nullptr);
+                       (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_eng_fe_fb, dim3(ENG_FB_GRID), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1inv, st,
@@ -1311,9 +1281,6 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
   const char* kdv = getenv("DGPU_KB_DEC");
   if (kdv && !strcmp(kdv, "split")) c->kb_split = true;
-  if (kdv) c->kb_dec_rows = !strcmp(kdv, "rows");
-  if (kdv) c->kb_dec_soa = !strcmp(kdv, "soa");
-  if (kdv) c->kb_dec_image = !strcmp(kdv, "image");
   const char* knv = getenv("DGPU_KB_NORM");
   if (knv) c->kb_norm_chain = strcmp(knv, "planes") != 0;
   const char* rds = getenv("DGPU_RLC_DESCENT_STEP");

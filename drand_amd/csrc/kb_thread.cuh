@@ -101,12 +101,9 @@ __device__ __forceinline__ void kb_st_thr(uint32_t* xbuf, size_t i, int plane, i
 // -> nbuf ([j][limb][cnt], round-fastest, coalesced), so k_eng_kb_norm_pre
 // reads 6 x 56 B per round instead of the values' f1 halves from the blocked
 // planes.
-// SOA (DGPU_KB_DEC=soa): and f1, f2, f4, f5 -> xin ([j][8][limb][cnt]) for
-// k_eng_kb_dec_soa, whose reads are then coalesced.
-template <bool NORM, bool SOA>
+template <bool NORM>
 __global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt, uint32_t* __restrict__ xbuf,
-                                                                     uint32_t* __restrict__ nbuf,
-                                                                     uint32_t* __restrict__ xin) {
+                                                                     uint32_t* __restrict__ nbuf) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cnt) return;
   kb_chain_thr(kb_ld_thr(xbuf, i, ENG_KB_PL_M, 2), kb_ld_thr(xbuf, i, ENG_KB_PL_M, 4),
@@ -118,17 +115,6 @@ __global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt,
                  kb_st_thr(xbuf, i, pl, 8, f4);
                  kb_st_thr(xbuf, i, pl, 10, f5);
                  if constexpr (NORM) st_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i, eng_kb_norm(f1));
-                 if constexpr (SOA) {
-                   uint32_t* x = xin + (size_t)j * 8 * FP_LIMBS * cnt;
-                   st_soa(x, cnt, i, f1.c0);
-                   st_soa(x + 1 * FP_LIMBS * cnt, cnt, i, f1.c1);
-                   st_soa(x + 2 * FP_LIMBS * cnt, cnt, i, f2.c0);
-                   st_soa(x + 3 * FP_LIMBS * cnt, cnt, i, f2.c1);
-                   st_soa(x + 4 * FP_LIMBS * cnt, cnt, i, f4.c0);
-                   st_soa(x + 5 * FP_LIMBS * cnt, cnt, i, f4.c1);
-                   st_soa(x + 6 * FP_LIMBS * cnt, cnt, i, f5.c0);
-                   st_soa(x + 7 * FP_LIMBS * cnt, cnt, i, f5.c1);
-                 }
                });
 }
 

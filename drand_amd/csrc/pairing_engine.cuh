@@ -96,7 +96,6 @@ struct eng_io {
   fp mlt{};                         // FIXED: this lane's export multiplier (P coordinate)
   bool scale = false;               // FIXED: export L.k is linear in a P coordinate
   uint32_t* xbuf = nullptr;         // Karabina FE: LD12 / ST12 address its ENG_KB_PLANES state planes instead of fbuf
-  const uint32_t* dsoa = nullptr;   // Karabina FE (DGPU_KB_DEC=soa): stored values' f0, f3 ([j][4][limb][cnt])
 };
 
 // The program interpreter (one inlined copy of the op interpreter per kernel).
@@ -155,13 +154,7 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
       ++step;
     } else if (opc == ENG_OPC_LD12) {
       const int pl = (int)b / 12;
-      // f0 (components 0, 1) and f3 (6, 7) of a stored value: decompressed on round-fastest planes
-      const bool soa = KB && io.dsoa && pl >= ENG_KB_PL_X0 && (L.k & ~1) % 6 == 0;
-      if (soa)
-        eng_st(g + (a + L.k) * ENG_SLOT_WORDS,
-               ld_soa(io.dsoa + ((size_t)(pl - ENG_KB_PL_X0) * 4 + (L.k >= 6 ? 2 : 0) + (L.k & 1)) * FP_LIMBS * io.cnt,
-                      io.cnt, L.i));
-      else if constexpr (KB) eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.xbuf, eng_blk_off(L.blk, ENG_KB_PLANES, pl, L.g, L.k)));
+      if constexpr (KB) eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.xbuf, eng_blk_off(L.blk, ENG_KB_PLANES, pl, L.g, L.k)));
       else eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.fbuf, eng_blk_off(L.blk, 2, (int)b / 12, L.g, L.k)));
     } else if (opc == ENG_OPC_ST12) {
       if (L.valid) {
@@ -362,8 +355,7 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe_seg(int off, int len, b
                                                           const uint32_t* __restrict__ fbuf,
                                                           const uint32_t* __restrict__ n1inv, uint32_t* __restrict__ xbuf,
                                                           uint8_t* __restrict__ flags, uint32_t* __restrict__ fb,
-                                                          uint8_t* __restrict__ status,
-                                                          const uint32_t* __restrict__ dsoa) {
+                                                          uint8_t* __restrict__ status) {
   __shared__ uint32_t lds[ENG_LDS_SLOTS_FE * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
@@ -378,7 +370,6 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe_seg(int off, int len, b
   asm volatile("" ::: "memory");
   eng_io io{nullptr, nullptr, nullptr, cnt};
   io.xbuf = xbuf;
-  io.dsoa = dsoa;
   eng_exec<false, false, 2, true>(ENG_PROG_FEK + off, len, g, c, L, io);
   if (last) {
     const fp v = eng_ld(g + (ENG_E_R + L.k) * ENG_SLOT_WORDS);
@@ -516,177 +507,6 @@ __global__ void __launch_bounds__(256, DG_KB_DEC_OCC) k_eng_kb_dec(size_t cnt, u
                     ninv, f0, f3);
   kb_st2(xbuf, i, pl, 0, f0);
   kb_st2(xbuf, i, pl, 6, f3);
-}
-
-// The decompression with the whole image staged at once (DGPU_KB_DEC=image):
-// one wave owns KB_IMG_BLOCKS blocks of one stored value; all 14 limb rows of
-// each block (3,360 contiguous bytes) are read with 16-byte loads into LDS in
-// one phase (every load in flight together), each lane takes its round's
-// f1, f2, f4, f5 from the image, decompresses, patches f0 and f3 into the
-// image, and the wave stores the rows back whole: 4 KB read and 4 KB written
-// per round, full lines, no re-read.  One wave per SIMD (33.6 KB of LDS per
-// wave; 512 VGPRs, no spills).
-constexpr int KB_IMG_BLOCKS = 10;                                   // 50 rounds per wave
-constexpr int KB_IMG_CHUNKS = FP_LIMBS * ENG_WAVE_WORDS / 4;        // 16-byte chunks per block (210)
-__global__ void __launch_bounds__(64, 1) k_eng_kb_dec_image(size_t cnt, size_t nblk, uint32_t* __restrict__ xbuf,
-                                                            const uint32_t* __restrict__ pbuf,
-                                                            const uint32_t* __restrict__ ebuf,
-                                                            const uint8_t* __restrict__ flags) {
-  __shared__ __attribute__((aligned(16))) uint32_t img[KB_IMG_BLOCKS * FP_LIMBS * ENG_WAVE_WORDS];
-  const int lane = threadIdx.x & 63;
-  const size_t j = blockIdx.y;
-  const int pl = ENG_KB_PL_X0 + (int)j;
-  const size_t blk0 = (size_t)blockIdx.x * KB_IMG_BLOCKS;
-  const int nb = (int)min((size_t)KB_IMG_BLOCKS, nblk - blk0);
-  for (int q = lane; q < nb * KB_IMG_CHUNKS; q += 64) {
-    const int r = q / KB_IMG_CHUNKS, off = q - r * KB_IMG_CHUNKS;
-    *reinterpret_cast<uint4*>(img + (size_t)r * FP_LIMBS * ENG_WAVE_WORDS + off * 4) = *reinterpret_cast<const uint4*>(
-        xbuf + ((blk0 + r) * ENG_KB_PLANES + pl) * FP_LIMBS * ENG_WAVE_WORDS + off * 4);
-  }
-  __syncthreads();
-  const int r = lane / ENG_ROUNDS_PER_BLOCK, g = lane - r * ENG_ROUNDS_PER_BLOCK;
-  const size_t i = (blk0 + r) * ENG_ROUNDS_PER_BLOCK + g;
-  const bool act = r < nb && i < cnt && !flags[i];
-  if (act) {
-    uint32_t* w = img + (size_t)r * FP_LIMBS * ENG_WAVE_WORDS + g * 12;
-    fp2 f1, f2, f4, f5;
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) {
-      const uint32_t* wl = w + l * ENG_WAVE_WORDS;
-      const uint2 a = *reinterpret_cast<const uint2*>(wl + 2), b = *reinterpret_cast<const uint2*>(wl + 4);
-      const uint4 c = *reinterpret_cast<const uint4*>(wl + 8);
-      f1.c0.l[l] = a.x, f1.c1.l[l] = a.y, f2.c0.l[l] = b.x, f2.c1.l[l] = b.y;
-      f4.c0.l[l] = c.x, f4.c1.l[l] = c.y, f5.c0.l[l] = c.z, f5.c1.l[l] = c.w;
-    }
-    const fp ninv = fp_mul(ld_soa(pbuf, cnt, i), ld_soa(ebuf + j * FP_LIMBS * cnt, cnt, i));
-    fp2 f0, f3;
-    eng_kb_decompress(f1, f2, f4, f5, ninv, f0, f3);
-#pragma unroll
-    for (int l = 0; l < FP_LIMBS; ++l) {
-      uint32_t* wl = w + l * ENG_WAVE_WORDS;
-      *reinterpret_cast<uint2*>(wl) = make_uint2(f0.c0.l[l], f0.c1.l[l]);
-      *reinterpret_cast<uint2*>(wl + 6) = make_uint2(f3.c0.l[l], f3.c1.l[l]);
-    }
-  }
-  __syncthreads();
-  for (int q = lane; q < nb * KB_IMG_CHUNKS; q += 64) {
-    const int rr = q / KB_IMG_CHUNKS, off = q - rr * KB_IMG_CHUNKS;
-    *reinterpret_cast<uint4*>(xbuf + ((blk0 + rr) * ENG_KB_PLANES + pl) * FP_LIMBS * ENG_WAVE_WORDS + off * 4) =
-        *reinterpret_cast<const uint4*>(img + (size_t)rr * FP_LIMBS * ENG_WAVE_WORDS + off * 4);
-  }
-}
-
-// The decompression on round-fastest planes (DGPU_KB_DEC=soa): one thread
-// per stored value j of round i reads f1, f2, f4, f5 from xin (the chain's
-// copy, [j][8][limb][cnt]) and writes f0, f3 to dsoa ([j][4][limb][cnt]),
-// which k_eng_fe_seg's LD12 reads for those components: every access is a
-// coalesced 4-byte-per-lane plane access, none touches the blocked rows.
-__global__ void __launch_bounds__(256, 2) k_eng_kb_dec_soa(size_t cnt, const uint32_t* __restrict__ xin,
-                                                           uint32_t* __restrict__ dsoa,
-                                                           const uint32_t* __restrict__ pbuf,
-                                                           const uint32_t* __restrict__ ebuf,
-                                                           const uint8_t* __restrict__ flags) {
-  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (size_t)ENG_KB_NSNAP * cnt) return;
-  const size_t j = e / cnt, i = e - j * cnt;
-  if (flags[i]) return;
-  const uint32_t* x = xin + j * 8 * FP_LIMBS * cnt;
-  auto ld = [&](int c) { return ld_soa(x + (size_t)c * FP_LIMBS * cnt, cnt, i); };
-  const fp ninv = fp_mul(ld_soa(pbuf, cnt, i), ld_soa(ebuf + j * FP_LIMBS * cnt, cnt, i));
-  fp2 f0, f3;
-  eng_kb_decompress(fp2{ld(0), ld(1)}, fp2{ld(2), ld(3)}, fp2{ld(4), ld(5)}, fp2{ld(6), ld(7)}, ninv, f0, f3);
-  uint32_t* d = dsoa + j * 4 * FP_LIMBS * cnt;
-  st_soa(d, cnt, i, f0.c0);
-  st_soa(d + 1 * FP_LIMBS * cnt, cnt, i, f0.c1);
-  st_soa(d + 2 * FP_LIMBS * cnt, cnt, i, f3.c0);
-  st_soa(d + 3 * FP_LIMBS * cnt, cnt, i, f3.c1);
-}
-
-// The decompression with whole-row accesses (DGPU_KB_DEC=rows, VERDICT r04
-// item 3).  A stored value's 12 components share 48-byte pieces of 240-byte
-// limb rows with the other 4 rounds of its block, and k_eng_kb_dec's
-// per-thread loads and stores of 8 of them (and 4 written back) touch every
-// row in small pieces: r04q counted 27 KB fetched and 21 KB written per round
-// for 2.7 KB read and 1.3 KB written.  Here one wave owns KB_ROW_BLOCKS
-// blocks (60 rounds) of one stored value (plane) and moves each limb row
-// whole: per limb the wave reads its blocks' rows with 16-byte loads into a
-// 2.9 KB LDS image, each lane picks its round's f1, f2, f4, f5 words; after
-// the decompression it re-reads each row, patches f0 and f3 into the image
-// and stores the rows back whole.  Traffic: the rows twice in, once out.
-// (The wave's LDS instructions execute in order, so the one image is reused
-// limb after limb with no barrier.)
-constexpr int KB_ROW_BLOCKS = 12;                                  // 60 rounds per wave
-constexpr int KB_ROW_CHUNKS = ENG_WAVE_WORDS / 4;                  // 16-byte chunks per limb row (15)
-__device__ __forceinline__ void kb_rows_in(const uint32_t* xbuf, size_t blk0, size_t nblk, int plane, int l,
-                                           uint32_t* img) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int q = lane; q < KB_ROW_BLOCKS * KB_ROW_CHUNKS; q += 64) {
-    const int r = q / KB_ROW_CHUNKS, off = q - r * KB_ROW_CHUNKS;
-    if (blk0 + r < nblk) {
-      const uint4 v = *reinterpret_cast<const uint4*>(xbuf + ((blk0 + r) * ENG_KB_PLANES + plane) * FP_LIMBS * ENG_WAVE_WORDS +
-                                                      l * ENG_WAVE_WORDS + off * 4);
-      *reinterpret_cast<uint4*>(img + r * ENG_WAVE_WORDS + off * 4) = v;
-    }
-  }
-}
-__device__ __forceinline__ void kb_rows_out(uint32_t* xbuf, size_t blk0, size_t nblk, int plane, int l,
-                                            const uint32_t* img) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int q = lane; q < KB_ROW_BLOCKS * KB_ROW_CHUNKS; q += 64) {
-    const int r = q / KB_ROW_CHUNKS, off = q - r * KB_ROW_CHUNKS;
-    if (blk0 + r < nblk)
-      *reinterpret_cast<uint4*>(xbuf + ((blk0 + r) * ENG_KB_PLANES + plane) * FP_LIMBS * ENG_WAVE_WORDS +
-                                l * ENG_WAVE_WORDS + off * 4) = *reinterpret_cast<const uint4*>(img + r * ENG_WAVE_WORDS + off * 4);
-  }
-}
-// grid: (groups of KB_ROW_BLOCKS blocks) x ENG_KB_NSNAP values; 64 threads.
-// nblk: blocks of the chunk capacity (the planes' extent); lanes 60..63 and
-// rounds >= cnt carry no value (their rows are copied back unchanged).
-__global__ void __launch_bounds__(64, 2) k_eng_kb_dec_rows(size_t cnt, size_t nblk, uint32_t* __restrict__ xbuf,
-                                                        const uint32_t* __restrict__ pbuf,
-                                                        const uint32_t* __restrict__ ebuf,
-                                                        const uint8_t* __restrict__ flags) {
-  __shared__ __attribute__((aligned(16))) uint32_t img[KB_ROW_BLOCKS * ENG_WAVE_WORDS];
-  const int lane = threadIdx.x & 63;
-  const size_t j = blockIdx.y;
-  const int pl = ENG_KB_PL_X0 + (int)j;
-  const size_t blk0 = (size_t)blockIdx.x * KB_ROW_BLOCKS;
-  const int r = lane / ENG_ROUNDS_PER_BLOCK, g = lane - r * ENG_ROUNDS_PER_BLOCK;
-  const size_t i = (blk0 + r) * ENG_ROUNDS_PER_BLOCK + g;
-  const bool act = lane < KB_ROW_BLOCKS * ENG_ROUNDS_PER_BLOCK && i < cnt && !flags[i];
-  const uint32_t* w = img + r * ENG_WAVE_WORDS + g * 12;
-  fp2 f1, f2, f4, f5;
-#pragma unroll
-  for (int l = 0; l < FP_LIMBS; ++l) {
-    kb_rows_in(xbuf, blk0, nblk, pl, l, img);
-    asm volatile("" ::: "memory");
-    if (lane < KB_ROW_BLOCKS * ENG_ROUNDS_PER_BLOCK) {
-      const uint2 a = *reinterpret_cast<const uint2*>(w + 2), b = *reinterpret_cast<const uint2*>(w + 4);
-      const uint4 c = *reinterpret_cast<const uint4*>(w + 8);
-      f1.c0.l[l] = a.x, f1.c1.l[l] = a.y, f2.c0.l[l] = b.x, f2.c1.l[l] = b.y;
-      f4.c0.l[l] = c.x, f4.c1.l[l] = c.y, f5.c0.l[l] = c.z, f5.c1.l[l] = c.w;
-    }
-    asm volatile("" ::: "memory");
-  }
-  fp2 f0 = {}, f3 = {};
-  if (act) {
-    const fp ninv = fp_mul(ld_soa(pbuf, cnt, i), ld_soa(ebuf + j * FP_LIMBS * cnt, cnt, i));
-    eng_kb_decompress(f1, f2, f4, f5, ninv, f0, f3);
-  }
-#pragma unroll
-  for (int l = 0; l < FP_LIMBS; ++l) {
-    kb_rows_in(xbuf, blk0, nblk, pl, l, img);
-    asm volatile("" ::: "memory");
-    if (act) {
-      *reinterpret_cast<uint2*>(img + r * ENG_WAVE_WORDS + g * 12) = make_uint2(f0.c0.l[l], f0.c1.l[l]);
-      *reinterpret_cast<uint2*>(img + r * ENG_WAVE_WORDS + g * 12 + 6) = make_uint2(f3.c0.l[l], f3.c1.l[l]);
-    }
-    asm volatile("" ::: "memory");
-    kb_rows_out(xbuf, blk0, nblk, pl, l, img);
-    asm volatile("" ::: "memory");
-  }
 }
 
 }  // namespace dgpu

@@ -278,8 +278,7 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     in place of the per-thread one, and with the decompression split at the
     inversion (DGPU_KB_DEC=split; fallback forced and not), and with the norms
     written by the chain or read from the planes (DGPU_KB_NORM, fallback
-    forced), and with the decompression moving whole limb rows or per value
-    (DGPU_KB_DEC=rows / values) or on round-fastest planes (DGPU_KB_DEC=soa).  20,011 rounds (a ragged last block), 1%
+    forced).  20,011 rounds (a ragged last block), 1%
     corrupted: identical reasons, equal to the construction."""
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
@@ -295,15 +294,8 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     # the six norms from the chain's snaps (DGPU_KB_NORM=chain) or from the planes
     norm_chain = _verify_with_env(c, {"DGPU_KB_NORM": "chain", "DGPU_KB_TEST_FLAG": "7"})
     norm_planes = _verify_with_env(c, {"DGPU_KB_NORM": "planes", "DGPU_KB_TEST_FLAG": "7"})
-    # the decompression with whole-row accesses (DGPU_KB_DEC=rows) or per value
-    rows = _verify_with_env(c, {"DGPU_KB_DEC": "rows", "DGPU_KB_NORM": "chain", "DGPU_KB_TEST_FLAG": "7"})
-    per_value = _verify_with_env(c, {"DGPU_KB_DEC": "values", "DGPU_KB_NORM": "planes"})
-    soa = _verify_with_env(c, {"DGPU_KB_DEC": "soa", "DGPU_KB_TEST_FLAG": "7"})
-    soa_nf = _verify_with_env(c, {"DGPU_KB_DEC": "soa"})
-    image = _verify_with_env(c, {"DGPU_KB_DEC": "image", "DGPU_KB_TEST_FLAG": "7"})
     assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist() == split.tolist() == split_fb.tolist()
-    assert norm_chain.tolist() == norm_planes.tolist() == rows.tolist() == per_value.tolist() == kb.tolist()
-    assert soa.tolist() == soa_nf.tolist() == image.tolist() == kb.tolist()
+    assert norm_chain.tolist() == norm_planes.tolist() == kb.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(kb == 0, expect)

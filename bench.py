@@ -270,6 +270,14 @@ def stage_times(lib, ctx, step, passes=1):
     return out
 
 
+def coll_device(dev):
+    """Where the bench's own small collectives run: the GPU over RCCL, the CPU
+    when the process group is gloo (DRAND_BENCH_BACKEND=gloo: several ranks
+    rehearsed on one GPU)."""
+    import torch.distributed as dist
+    return "cpu" if dist.is_initialized() and dist.get_backend() == "gloo" else dev
+
+
 def timed(step, steps, world, dev, after=None):
     """barrier + synchronize, K steps (+ `after`, the exchange step),
     synchronize + barrier; max over ranks."""
@@ -285,7 +293,7 @@ def timed(step, steps, world, dev, after=None):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=coll_device(dev))
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()), res
@@ -369,7 +377,7 @@ def recover_leg(args, world, rank, local, n_total, steps, warmup, cpu_seconds):
     ok = d_ok.cpu().numpy().astype(bool)
     out = d_out.cpu().numpy()
     mism = int((ok != expect_ok).sum()) + int((out[ok & expect_ok] != expect[ok & expect_ok]).any(axis=1).sum())
-    mism_t = torch.tensor([mism], device=dev)
+    mism_t = torch.tensor([mism], device=coll_device(dev))
     if world > 1:
         dist.all_reduce(mism_t)
     res = {"metric": "recovered beacon rounds/sec, t-of-n threshold recovery (VerifyPartial x t, Lagrange, "
@@ -924,9 +932,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DRAND_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+    # devices round-robin; collectives over gloo on the CPU); the default is
+    # one rank per GPU over RCCL ("nccl")
+    backend = os.environ.get("DRAND_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     try:

@@ -33,6 +33,8 @@ def gather_verdict_bits(local_bits, n_local, n_total, world, rank, device=None):
     sizes = [shard_range(n_total, world, r) for r in range(world)]
     max_bytes = max((hi - lo + 7) // 8 for lo, hi in sizes)
     dev = local_bits.device if device is None else device
+    if dist.get_backend() == "gloo":  # CPU collectives (tests, one-GPU rehearsals)
+        dev = torch.device("cpu")
     buf = torch.zeros(max_bytes, dtype=torch.uint8, device=dev)
     buf[: local_bits.numel()] = local_bits
     out = [torch.zeros(max_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]

@@ -220,7 +220,9 @@ struct dgpu_ctx {
   // classes, and the compact batch of rounds that take the exact path
   DevBuf grp_wtab, rec_cls, rec_x_list, rec_x_msgs, rec_x_parts, rec_x_plen, rec_x_out, rec_x_ok, rec_x_st;
   DevBuf rec_tab, rec_tabz, rec_tabpre;  // the batched check's shared affine window tables
+  DevBuf rec_tab_rows;                   // ... as 224-byte rows (the gather layout; r05l)
   bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
+  bool recover_rows = true;      // the MSM gathers its window tables as rows (DGPU_RECOVER_ROWS=0: SoA planes, A/B)
   // DGPU_ENG_FUSED_PROBE=1 (A/B probe only): dynamic LDS padding that puts
   // k_eng_lines and k_eng_miller at the occupancy a fused lines+Miller kernel
   // would have (74 slots per group: 22,064 B per block, 7 blocks per CU)
@@ -1305,6 +1307,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   }
   const char* rcv = getenv("DGPU_RECOVER");
   if (rcv && !strcmp(rcv, "exact")) c->recover_exact = true;
+  const char* rrv = getenv("DGPU_RECOVER_ROWS");
+  if (rrv) c->recover_rows = !strcmp(rrv, "1");
   const char* fev = getenv("DGPU_FE");
   if (fev && !strcmp(fev, "gs")) c->fe_gs = true;
   const char* kic = getenv("DGPU_KB_INV_CHAIN");
@@ -1347,7 +1351,7 @@ void dgpu_close(dgpu_ctx* c) {
                     &c->rec_pk, &c->rec_idx, &c->rec_lam, &c->rec_out, &c->rec_ok, &c->rec_pts, &c->rec_vpk,
                     &c->rec_st, &c->rec_sel, &c->rec_part, &c->grp_wtab, &c->rec_cls, &c->rec_x_list,
                     &c->rec_x_msgs, &c->rec_x_parts, &c->rec_x_plen, &c->rec_x_out, &c->rec_x_ok, &c->rec_x_st,
-                    &c->rec_tab, &c->rec_tabz, &c->rec_tabpre,
+                    &c->rec_tab, &c->rec_tabz, &c->rec_tabpre, &c->rec_tab_rows,
                     &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb, &c->l2_kb,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
                     &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs,
@@ -1995,8 +1999,17 @@ static int recover_device_locked(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_
     hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((ne + 15) / 16, 256)), dim3(256), 0, s, ne, tab,
                        (const uint32_t*)c->rec_tabz.p, (uint32_t*)c->rec_tabpre.p);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_recover_msm_aff, dim3(grid_for(5 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t,
-                       (const uint8_t*)d_ok, (const uint64_t*)dig, (const uint32_t*)tab, part, 5);
+    if (c->recover_rows) {  // the entries as 224-byte rows for the gathers
+      if ((rc = c->rec_tab_rows.ensure(ne * G2A_WORDS * 4))) return rc;
+      hipLaunchKernelGGL(k_recover_tab_rows, dim3(grid_for(ne, 256)), dim3(256), 0, s, ne, (const uint32_t*)tab,
+                         (uint32_t*)c->rec_tab_rows.p);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_recover_msm_aff<true>, dim3(grid_for(5 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t,
+                         (const uint8_t*)d_ok, (const uint64_t*)dig, (const uint32_t*)c->rec_tab_rows.p, part, 5);
+    } else {
+      hipLaunchKernelGGL(k_recover_msm_aff<false>, dim3(grid_for(5 * n_rounds, 256)), dim3(256), 0, s, n_rounds, t,
+                         (const uint8_t*)d_ok, (const uint64_t*)dig, (const uint32_t*)tab, part, 5);
+    }
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_recover_finish, dim3(grid_for(n_rounds, 64)), dim3(64), 0, s, n_rounds, (const uint8_t*)d_ok,

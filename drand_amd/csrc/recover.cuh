@@ -382,6 +382,41 @@ __global__ void __launch_bounds__(256, 2) k_recover_tables(size_t n_rounds, int 
   }
 }
 
+// The affine table entries transposed to rows (AoS, G2A_WORDS = 56 words,
+// 224 contiguous bytes: x.c0, x.c1, y.c0, y.c1), one thread per entry: the
+// window additions gather one row (two cache lines) per entry instead of
+// one word from each of 56 SoA planes (the RLC root MSM's layout, k_msm_aos).
+__global__ void __launch_bounds__(256) k_recover_tab_rows(size_t ne, const uint32_t* __restrict__ tab,
+                                                          uint32_t* __restrict__ rows) {
+  const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  const g2a q = ld_g2a(tab, ne, e);
+  uint4* o = reinterpret_cast<uint4*>(rows + e * G2A_WORDS);
+  const fp* c[4] = {&q.x.c0, &q.x.c1, &q.y.c0, &q.y.c1};
+#pragma unroll
+  for (int k = 0; k < G2A_WORDS / 4; ++k) {
+    uint32_t w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = c[(4 * k + u) / FP_LIMBS]->l[(4 * k + u) % FP_LIMBS];
+    o[k] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+__device__ __forceinline__ g2a recover_ld_row(const uint32_t* __restrict__ rows, size_t e) {
+  const uint4* p = reinterpret_cast<const uint4*>(rows + e * G2A_WORDS);
+  g2a q;
+  fp* c[4] = {&q.x.c0, &q.x.c1, &q.y.c0, &q.y.c1};
+#pragma unroll
+  for (int k = 0; k < G2A_WORDS / 4; ++k) {
+    const uint4 v = p[k];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) c[(4 * k + u) / FP_LIMBS]->l[(4 * k + u) % FP_LIMBS] = w[u];
+  }
+  return q;
+}
+
+// ROWS: the table as rows (k_recover_tab_rows), else the SoA planes.
+template <bool ROWS>
 __global__ void __launch_bounds__(256, 2) k_recover_msm_aff(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
                                                           const uint64_t* __restrict__ digits,
                                                           const uint32_t* __restrict__ tab,
@@ -405,7 +440,8 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm_aff(size_t n_rounds, int
     for (int j = 0; j < t; ++j) {
       const int dg = win4_digit64(d[RECOVER_SLOTS * j], w);
       const int mag = dg < 0 ? -dg : dg;
-      g2a e = ld_g2a(tab, N, base + (size_t)j * 8 + ((mag - 1) & 7));
+      const size_t ei = base + (size_t)j * 8 + ((mag - 1) & 7);
+      g2a e = ROWS ? recover_ld_row(tab, ei) : ld_g2a(tab, N, ei);
       e.y = fp2_cmov(e.y, fp2_neg(e.y), dg < 0);
       acc = g2_cmov(acc, g2_add_affine_body(acc, e), mag != 0);
     }

@@ -122,3 +122,36 @@ def test_recover_at_defaults(name):
     for c, s, v in zip(g["cases"], sigs, valid):
         assert v == c["valid"], c["kind"]
         assert (s.hex() if s else None) == c["recovered"], c["kind"]
+
+
+@pytest.mark.parametrize("rows", ["0", "1"])
+def test_recover_batched_check_table_layouts(rows):
+    """The batched recovery check (no per-partial statuses requested) with its
+    window tables gathered from SoA planes or from 224-byte rows
+    (DGPU_RECOVER_ROWS): recovered signatures equal the t=17-of-32 and
+    t=12-of-20 fixtures case by case."""
+    from drand_amd import _lib
+    from drand_amd.threshold import pack_partials, unpack_recovered
+    for name in ("recover_t17_n32.json", "recover_t12_n20.json"):
+        g = load_golden(name)
+        commits = np.frombuffer(b"".join(bytes.fromhex(x) for x in g["commits"]), dtype=np.uint8).copy()
+        msgs = [bytes.fromhex(c["msg"]) for c in g["cases"]]
+        partials = [[bytes.fromhex(p) for p in c["partials"]] for c in g["cases"]]
+        mb, buf, plen, m, stride = pack_partials(msgs, partials)
+        nr = len(msgs)
+        out = np.zeros(nr * 96, dtype=np.uint8)
+        ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
+        saved = os.environ.get("DGPU_RECOVER_ROWS")
+        os.environ["DGPU_RECOVER_ROWS"] = rows
+        try:
+            with _default_ctx() as ctx:
+                _lib.check(ctx.lib.dgpu_set_group(ctx.handle, len(g["commits"]), g["n"], _lib.ptr(commits)))
+                _lib.check(ctx.lib.dgpu_recover_batch(ctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
+                                                      _lib.ptr(plen), _lib.ptr(out), _lib.ptr(ok), None))
+        finally:
+            if saved is None:
+                del os.environ["DGPU_RECOVER_ROWS"]
+            else:
+                os.environ["DGPU_RECOVER_ROWS"] = saved
+        sigs, _ = unpack_recovered(out, ok, None, partials, m)
+        assert [s.hex() if s else None for s in sigs] == [c["recovered"] for c in g["cases"]], name

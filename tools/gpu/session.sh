@@ -51,11 +51,11 @@ run_step() {
     TAG=$TAG/pmc PROF_ARGS="${TRAFFIC_ARGS:---rounds 131072 --iters 1}" bash tools/gpu/pmc.sh > $O/pmc.log 2>&1 ;;
   ab)
     mkdir -p $O/ab
-    # a variant is lib.so or lib.so@KEY=VALUE (an environment knob read at dgpu_open)
+    # a variant is lib.so or lib.so@KEY=VALUE[@KEY=VALUE...] (environment knobs read at dgpu_open)
     for v in $VARIANTS; do
-      lib=${v%%@*}; kv=$([ "$lib" != "$v" ] && echo "${v#*@}")
-      name=$(basename $lib .so)$([ -n "$kv" ] && echo "_${kv//=/_}")
-      ( [ -n "$kv" ] && export "$kv"
+      lib=${v%%@*}; kvs=$([ "$lib" != "$v" ] && echo "${v#*@}" | tr '@' ' ')
+      name=$(basename $lib .so)$(for kv in $kvs; do echo -n "_${kv//=/_}"; done)
+      ( for kv in $kvs; do export "$kv"; done
         DRAND_GPU_LIB=$PWD/$lib timeout -k 10 600 python bench.py --no-cpu-baseline ${BENCH_ARGS} \
           > $O/ab/ab_$name.json 2> $O/ab/ab_$name.err ) || return $?
     done

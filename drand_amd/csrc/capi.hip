@@ -185,7 +185,7 @@ struct dgpu_ctx {
   DevBuf rlc_conf, rlc_fsum;
   // RLC root by bucket MSM (rlc_msm.cuh): AoS points, flags, counts / offsets /
   // cursors, bucket lists, bucket sums, per-run window sums
-  DevBuf msm_aos, msm_flags, msm_counts, msm_list, msm_buckets, msm_runs, msm_root;
+  DevBuf msm_aos, msm_flags, msm_counts, msm_list, msm_buckets, msm_runs, msm_root, msm_part;
   // pairing engine (per-round mode): per-chunk lines / f / norms
   DevBuf eng_lines, eng_f, eng_n1, eng_kb;
   // second lane's scratch (same roles as h_pts .. eng_kb)
@@ -222,6 +222,8 @@ struct dgpu_ctx {
   DevBuf rec_tab, rec_tabz, rec_tabpre;  // the batched check's shared affine window tables
   DevBuf rec_tab_rows;                   // ... as 224-byte rows (the gather layout; r05l)
   bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
+  bool msm_seg = true;           // load-balanced bucket sums (k_msm_bucket_seg); DGPU_MSM_SEG=0: one thread per bucket (A/B)
+  int n_cu = 256;                // compute units (the load-balanced sums launch one wave per SIMD slot)
   bool recover_rows = true;      // the MSM gathers its window tables as rows (DGPU_RECOVER_ROWS=0: SoA planes, A/B)
   // DGPU_ENG_FUSED_PROBE=1 (A/B probe only): dynamic LDS padding that puts
   // k_eng_lines and k_eng_miller at the occupancy a fused lines+Miller kernel
@@ -525,7 +527,7 @@ int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* r
   if (n > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "RLC batch too large (%zu)", n);
   int rc;
   if ((rc = c->msm_aos.ensure(2 * n * M::AFF * 4)) || (rc = c->msm_flags.ensure(n)) ||
-      (rc = c->msm_counts.ensure(3 * MSM_KEYS * 4)) || (rc = c->msm_list.ensure(MSM_MW * n * 4 + 4)) ||
+      (rc = c->msm_counts.ensure(3 * MSM_KEYS * 4)) || (rc = c->msm_list.ensure(2 * MSM_MW * n * 4 + 4)) ||
       (rc = c->msm_buckets.ensure(MSM_KEYS * M::JAC * 4)) ||
       (rc = c->msm_runs.ensure(2 * (size_t)MSM_MW * MSM_RUNS * M::JAC * 4)))
     return rc;
@@ -535,6 +537,10 @@ int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* r
   uint32_t* offsets = counts + MSM_KEYS;
   uint32_t* cursor = offsets + MSM_KEYS;
   uint32_t* list = (uint32_t*)c->msm_list.p;
+  uint32_t* keys = c->msm_seg ? list + MSM_MW * n : nullptr;  // the key of every list entry
+  // load-balanced sums: 4 SIMDs x 2 resident waves (launch bounds 256, 2) per CU
+  const size_t seg_threads = (size_t)c->n_cu * 4 * 2 * 64;
+  if (c->msm_seg && (rc = c->msm_part.ensure(2 * seg_threads * M::JAC * 4))) return rc;
   mark(c, s, stage);
   hipLaunchKernelGGL(k_msm_aos<Gr>, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)rlc_rpts(c, n, M::JAC),
                      (const uint32_t*)c->sig_pts.p, (const uint8_t*)c->status.p, aos, flags);
@@ -545,11 +551,21 @@ int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* r
   hipLaunchKernelGGL(k_msm_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)counts, offsets, cursor);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_msm_scatter, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.seed, (const uint8_t*)flags, cursor,
-                     list);
+                     list, keys);
   HIP_TRY(hipGetLastError());
   uint32_t* buckets = (uint32_t*)c->msm_buckets.p;
-  hipLaunchKernelGGL(k_msm_bucket<Gr>, dim3(grid_for(MSM_KEYS, B)), dim3(B), 0, s, n, (const uint32_t*)offsets,
-                     (const uint32_t*)counts, (const uint32_t*)list, (const uint32_t*)aos, buckets);
+  if (c->msm_seg) {
+    uint32_t* part = (uint32_t*)c->msm_part.p;
+    hipLaunchKernelGGL(k_msm_bucket_seg<Gr>, dim3(grid_for(seg_threads, B)), dim3(B), 0, s, n, seg_threads,
+                       (const uint32_t*)offsets, (const uint32_t*)counts, (const uint32_t*)list, (const uint32_t*)keys,
+                       (const uint32_t*)aos, buckets, part);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_msm_fixup<Gr>, dim3(grid_for(MSM_KEYS, B)), dim3(B), 0, s, seg_threads,
+                       (const uint32_t*)offsets, (const uint32_t*)counts, (const uint32_t*)part, buckets);
+  } else {
+    hipLaunchKernelGGL(k_msm_bucket<Gr>, dim3(grid_for(MSM_KEYS, B)), dim3(B), 0, s, n, (const uint32_t*)offsets,
+                       (const uint32_t*)counts, (const uint32_t*)list, (const uint32_t*)aos, buckets);
+  }
   HIP_TRY(hipGetLastError());
   uint32_t* runs = (uint32_t*)c->msm_runs.p;
   uint32_t* runs2 = runs + (size_t)MSM_MW * MSM_RUNS * M::JAC;
@@ -1273,6 +1289,9 @@ int dgpu_open(int device, dgpu_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   dgpu_ctx* c = new dgpu_ctx();
   c->device = device;
+  c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  const char* msv = getenv("DGPU_MSM_SEG");
+  if (msv && !strcmp(msv, "0")) c->msm_seg = false;
   const char* lv = getenv("DGPU_LANES");
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
   const char* lsv = getenv("DGPU_LANE_SLICES");
@@ -1354,7 +1373,7 @@ void dgpu_close(dgpu_ctx* c) {
                     &c->rec_tab, &c->rec_tabz, &c->rec_tabpre, &c->rec_tab_rows,
                     &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb, &c->l2_kb,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
-                    &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs,
+                    &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs, &c->msm_part,
                     &c->msm_root,
                     &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->in_rounds, &c->in_sigs,
                     &c->in_sig_len, &c->in_prev, &c->in_prev_len, &c->in_msgs, &c->in_msg_len, &c->out_bits,

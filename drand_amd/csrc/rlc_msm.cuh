@@ -21,8 +21,10 @@
 //                 gathers read two cache lines instead of 56) + usable flags
 //   k_msm_count   bucket sizes (atomics)
 //   k_msm_scan    exclusive prefix sums (one block)
-//   k_msm_scatter point indices into their buckets (atomics on cursors)
-//   k_msm_bucket  one thread per bucket: sum of its points (mixed additions)
+//   k_msm_scatter point indices (and keys) into their buckets (atomics on cursors)
+//   k_msm_bucket_seg  equal ranges of the sorted list per thread: sums of its runs of
+//                 equal key (mixed additions); k_msm_fixup joins runs cut by a range
+//                 boundary (DGPU_MSM_SEG=0: k_msm_bucket, one thread per bucket)
 //   k_msm_window  one thread per run of MSM_RUN buckets: sum_k k B_k of the run
 //   k_sum_level   pairwise tree over the runs of each (MSM, window)
 //   k_msm_root    MSM_m = W_m0 + 2^16 W_m1; P = MSM_0 + endo(MSM_1), S = MSM_2 + endo(MSM_3)
@@ -190,7 +192,8 @@ __global__ void __launch_bounds__(1024) k_msm_scan(const uint32_t* __restrict__ 
 }
 
 __global__ void __launch_bounds__(256) k_msm_scatter(size_t n, uint64_t seed, const uint8_t* __restrict__ flags,
-                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ list) {
+                                                     uint32_t* __restrict__ cursor, uint32_t* __restrict__ list,
+                                                     uint32_t* __restrict__ keys) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t z = rlc_coeff(seed, i);
@@ -198,7 +201,11 @@ __global__ void __launch_bounds__(256) k_msm_scatter(size_t n, uint64_t seed, co
 #pragma unroll
   for (int mw = 0; mw < MSM_MW; ++mw) {
     const int b = msm_bucket(z, f, mw >> 1, mw & 1);
-    if (b >= 0) list[atomicAdd(cursor + b, 1u)] = (uint32_t)i;
+    if (b >= 0) {
+      const uint32_t pos = atomicAdd(cursor + b, 1u);
+      list[pos] = (uint32_t)i;
+      if (keys) keys[pos] = (uint32_t)b;  // the load-balanced sums read the key per entry
+    }
   }
 }
 
@@ -217,6 +224,88 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket(size_t n, const uint32_t*
   typename Gr::jac acc = Gr::inf();
 #pragma unroll 1
   for (uint32_t p = 0; p < cnt; ++p) acc = Gr::add_aff_body(acc, M::ld_row(src + (size_t)list[o + p] * M::AFF));
+  M::st_jac(buckets, MSM_KEYS, b, acc);
+}
+
+// Load-balanced bucket sums (the default).  One thread per bucket leaves a
+// wave running as long as its largest bucket: at 10M rounds the bucket sizes
+// are Poisson(~153), and the maximum over a wave's 64 buckets is ~183, so
+// about 16% of the lanes' addition slots are idle.  Here the sorted list
+// (keys ascending, k_msm_scatter) is cut into T equal ranges of
+// S = ceil(L / T) entries, T = one resident wave per SIMD slot, and every
+// thread runs exactly S mixed additions over the runs of equal key in its
+// range.  A run that is a whole bucket goes to buckets[key]; a run cut by the
+// range's start goes to part slot A[t], one cut only by its end to B[t]
+// (at most one of each per thread); k_msm_fixup joins the pieces:
+// bucket = B[t0] + A[t0 + 1] + ... + A[t1] with t0, t1 the ranges holding the
+// bucket's first and last entries.
+template <class Gr>
+__device__ __forceinline__ void msm_seg_emit(uint32_t key, size_t s, size_t e, size_t t, size_t T,
+                                             const uint32_t* __restrict__ offsets,
+                                             const uint32_t* __restrict__ counts, const typename Gr::jac& acc,
+                                             uint32_t* __restrict__ buckets, uint32_t* __restrict__ part) {
+  using M = GrMem<Gr>;
+  const size_t o = offsets[key], c = counts[key];
+  const bool whole = s <= o && e >= o + c;
+  // cut at the start: A[t]; cut at the end only: B[t]; else the whole bucket (one store sequence)
+  M::st_jac(whole ? buckets : part, whole ? MSM_KEYS : 2 * T, whole ? key : (s > o ? t : T + t), acc);
+}
+
+template <class Gr>
+__global__ void __launch_bounds__(256, 2) k_msm_bucket_seg(size_t n, size_t T, const uint32_t* __restrict__ offsets,
+                                                         const uint32_t* __restrict__ counts,
+                                                         const uint32_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ aos,
+                                                         uint32_t* __restrict__ buckets, uint32_t* __restrict__ part) {
+  using M = GrMem<Gr>;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const size_t L = (size_t)offsets[MSM_KEYS - 1] + counts[MSM_KEYS - 1];
+  const size_t S = (L + T - 1) / T;
+  const size_t p0 = t * S;
+  if (p0 >= L) return;
+  const size_t p1 = p0 + S < L ? p0 + S : L;
+  uint32_t key = keys[p0];
+  size_t s = p0;
+  typename Gr::jac acc = Gr::inf();
+#pragma unroll 1
+  for (size_t p = p0; p < p1; ++p) {
+    const uint32_t k = keys[p];
+    if (k != key) {
+      msm_seg_emit<Gr>(key, s, p, t, T, offsets, counts, acc, buckets, part);
+      key = k;
+      s = p;
+      acc = Gr::inf();
+    }
+    const uint32_t* src = aos + ((key >> (MSM_C + 2)) ? n * M::AFF : 0);  // MSMs 2, 3: the signatures
+    acc = Gr::add_aff_body(acc, M::ld_row(src + (size_t)list[p] * M::AFF));
+  }
+  msm_seg_emit<Gr>(key, s, p1, t, T, offsets, counts, acc, buckets, part);
+}
+
+// One thread per bucket: empty -> identity; a bucket spread over ranges
+// t0 < t1 -> B[t0] + A[t0 + 1] + ... + A[t1]; a bucket inside one range was
+// written whole by k_msm_bucket_seg.
+template <class Gr>
+__global__ void __launch_bounds__(256) k_msm_fixup(size_t T, const uint32_t* __restrict__ offsets,
+                                                   const uint32_t* __restrict__ counts,
+                                                   const uint32_t* __restrict__ part, uint32_t* __restrict__ buckets) {
+  using M = GrMem<Gr>;
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= MSM_KEYS) return;
+  const size_t c = counts[b];
+  if (c == 0) {
+    M::st_jac(buckets, MSM_KEYS, b, Gr::inf());
+    return;
+  }
+  const size_t L = (size_t)offsets[MSM_KEYS - 1] + counts[MSM_KEYS - 1];
+  const size_t S = (L + T - 1) / T;
+  const size_t o = offsets[b], t0 = o / S, t1 = (o + c - 1) / S;
+  if (t0 == t1) return;
+  typename Gr::jac acc = M::ld_jac(part, 2 * T, T + t0);
+#pragma unroll 1
+  for (size_t t = t0 + 1; t <= t1; ++t) acc = Gr::add(acc, M::ld_jac(part, 2 * T, t));
   M::st_jac(buckets, MSM_KEYS, b, acc);
 }
 

@@ -43,6 +43,18 @@ def hostsim():
     return ctypes.CDLL(HOSTSIM)
 
 
+@pytest.fixture(autouse=True)
+def _torch_before_library(request):
+    """GPU tests: initialise torch's HIP state before any library context.  A
+    process whose first HIP user was the library (a test opening its own
+    dgpu contexts) saw torch._C._cuda_init() fail with "No HIP GPUs are
+    available" in later torch tests (gpurun_out/r05n)."""
+    if request.node.get_closest_marker("gpu"):
+        import torch
+        torch.cuda.init()
+    yield
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     from drand_amd.chain import get_context

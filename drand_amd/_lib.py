@@ -4,6 +4,7 @@ The product path has no CPU fallback: if the library is missing or no gfx950
 GPU is available, opening a context raises DrandGPUError.
 """
 import ctypes
+import sys
 import os
 import threading
 
@@ -162,6 +163,12 @@ class Context:
     """One GPU context (dgpu_ctx*).  Thread-safe: the library serializes."""
 
     def __init__(self, device=0):
+        # torch bundles its own HIP runtime under the system one's SONAME: a
+        # process that uses both must let torch initialise HIP first, or torch
+        # later finds no GPU (INTEGRATION.md, Python callers)
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_available():
+            torch.cuda.init()
         self.lib = load()
         h = ctypes.c_void_p()
         check(self.lib.dgpu_open(device, ctypes.byref(h)))

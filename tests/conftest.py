@@ -43,13 +43,17 @@ def hostsim():
     return ctypes.CDLL(HOSTSIM)
 
 
-@pytest.fixture(autouse=True)
+@pytest.fixture(scope="session", autouse=True)
 def _torch_before_library(request):
-    """GPU tests: initialise torch's HIP state before any library context.  A
-    process whose first HIP user was the library (a test opening its own
-    dgpu contexts) saw torch._C._cuda_init() fail with "No HIP GPUs are
-    available" in later torch tests (gpurun_out/r05n)."""
-    if request.node.get_closest_marker("gpu"):
+    """GPU sessions: initialise torch's HIP state before any library context.
+    torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's): when
+    torch loads first, the library binds to torch's runtime; when the library
+    initialises HIP first, torch later runs on the system runtime and
+    torch._C._cuda_init() fails with "No HIP GPUs are available"
+    (gpurun_out/r05n, r05u).  Session-scoped and autouse, so it runs before
+    the session's gpu_ctx whatever test comes first; a session without GPU
+    tests never touches torch here."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
         import torch
         torch.cuda.init()
     yield

@@ -365,3 +365,29 @@ def test_null_stream_is_the_default_stream(mode, gpu_ctx):
     assert np.array_equal(r == 0, expect) and set(np.unique(r)) <= {0, 1, 2, 3, 4}
     # dgpu_synchronize: the host-side wait a caller without HIP (cgo) uses
     _lib.check(gpu_ctx.lib.dgpu_synchronize(gpu_ctx.handle))
+
+
+def test_empty_batches_are_no_ops(gpu_ctx):
+    """n = 0 on the batch entry points (CheckPastBeacons over an empty range,
+    an empty tryNode window): DGPU_OK, nothing written, NULL record arrays
+    accepted.  G2 and G1 schemes, per-round and RLC, host and device entry
+    points, raw-message verify and recovery with zero rounds."""
+    from drand_amd import _lib
+    from drand_amd.synth import make_chain
+    lib, h = gpu_ctx.lib, gpu_ctx.handle
+    bits = np.full(2, 0xAB, dtype=np.uint8)
+    reason = np.full(2, 0xCD, dtype=np.uint8)
+    for code in (_lib.SCHEME_CHAINED, _lib.SCHEME_UNCHAINED_G1):
+        pk = np.frombuffer(make_chain(72, 2, code, seg_len=2).pk, dtype=np.uint8).copy()
+        for mode in (_lib.MODE_PER_ROUND, _lib.MODE_RLC):
+            _lib.check(lib.dgpu_verify_beacons(h, code, _lib.ptr(pk), pk.size, 0, None, None, 96, None, None, 96, None,
+                                               mode, 7, _lib.ptr(bits), _lib.ptr(reason)))
+            _lib.check(lib.dgpu_verify_beacons_device(h, code, _lib.ptr(pk), pk.size, 0, None, None, 96, None, None, 96,
+                                                      None, mode, 7, None, None, None))
+            _lib.check(lib.dgpu_verify_recovered(h, code, _lib.ptr(pk), pk.size, 0, None, 32, None, None, 96, None,
+                                                 mode, 7, _lib.ptr(bits), _lib.ptr(reason)))
+    g = load_golden("recover_t3_n8.json")
+    commits = np.frombuffer(b"".join(bytes.fromhex(x) for x in g["commits"]), dtype=np.uint8).copy()
+    _lib.check(lib.dgpu_set_group(h, len(g["commits"]), g["n"], _lib.ptr(commits)))
+    _lib.check(lib.dgpu_recover_batch(h, 0, None, 8, None, 96, None, None, _lib.ptr(bits), None))
+    assert bits.tolist() == [0xAB, 0xAB] and reason.tolist() == [0xCD, 0xCD]

@@ -2082,9 +2082,9 @@ extern "C" {
 int dgpu_recover_batch_device(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msgs32, size_t m,
                               const uint8_t* d_partials, size_t partial_stride, const uint32_t* d_partial_len,
                               uint8_t* d_out_sigs96, uint8_t* d_ok, uint8_t* d_status, void* stream) {
-  if (!c || !d_msgs32 || !d_partials || !d_partial_len || !d_out_sigs96 || !d_ok)
-    return set_err(DGPU_EINVAL, "null argument");
-  if (n_rounds == 0) return DGPU_OK;
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  if (n_rounds == 0) return DGPU_OK;  // an empty batch: no-op, NULL buffers accepted (as the verify entry points)
+  if (!d_msgs32 || !d_partials || !d_partial_len || !d_out_sigs96 || !d_ok) return set_err(DGPU_EINVAL, "null argument");
   if (m == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
@@ -2097,8 +2097,9 @@ int dgpu_recover_batch_device(dgpu_ctx* c, size_t n_rounds, const uint8_t* d_msg
 int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size_t m, const uint8_t* partials,
                        size_t partial_stride, const uint32_t* partial_len, uint8_t* out_sigs96, uint8_t* ok_bits,
                        uint8_t* partial_valid) {
-  if (!c || !msgs32 || !partials || !partial_len || !out_sigs96 || !ok_bits) return set_err(DGPU_EINVAL, "null argument");
-  if (n_rounds == 0) return DGPU_OK;
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  if (n_rounds == 0) return DGPU_OK;  // an empty batch: no-op, NULL buffers accepted (as the verify entry points)
+  if (!msgs32 || !partials || !partial_len || !out_sigs96 || !ok_bits) return set_err(DGPU_EINVAL, "null argument");
   if (m == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->grp_t) return set_err(DGPU_ENOKEY, "no threshold group installed (dgpu_set_group)");
@@ -2137,8 +2138,9 @@ int dgpu_recover_batch(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size
 
 int dgpu_make_partials(dgpu_ctx* c, size_t n_rounds, const uint8_t* msgs32, size_t m, const uint32_t* sign_idx,
                        const uint32_t* label, const uint8_t* shares_be32, size_t n_shares, uint8_t* out98) {
-  if (!c || !msgs32 || !sign_idx || !label || !shares_be32 || !out98) return set_err(DGPU_EINVAL, "null argument");
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
   if (n_rounds == 0 || m == 0) return DGPU_OK;
+  if (!msgs32 || !sign_idx || !label || !shares_be32 || !out98) return set_err(DGPU_EINVAL, "null argument");
   const size_t items = n_rounds * m;
   for (size_t i = 0; i < items; ++i)
     if (sign_idx[i] >= n_shares || label[i] > 0xFFFF) return set_err(DGPU_EINVAL, "bad share index at item %zu", i);

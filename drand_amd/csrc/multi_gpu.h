@@ -397,8 +397,9 @@ int dgpu_multi_set_group(dgpu_multi* m, int t, int n, const uint8_t* commits48) 
 int dgpu_recover_multi(dgpu_multi* m, size_t n_rounds, const uint8_t* msgs32, size_t m_slots, const uint8_t* partials,
                        size_t partial_stride, const uint32_t* partial_len, uint8_t* out_sigs96, uint8_t* ok_bits,
                        uint8_t* partial_valid) {
-  if (!m || !msgs32 || !partials || !partial_len || !out_sigs96 || !ok_bits) return set_err(DGPU_EINVAL, "null argument");
-  if (n_rounds == 0) return DGPU_OK;
+  if (!m) return set_err(DGPU_EINVAL, "null multi handle");
+  if (n_rounds == 0) return DGPU_OK;  // an empty batch: no-op, NULL buffers accepted
+  if (!msgs32 || !partials || !partial_len || !out_sigs96 || !ok_bits) return set_err(DGPU_EINVAL, "null argument");
   if (m_slots == 0 || partial_stride < 98) return set_err(DGPU_EINVAL, "need m >= 1 partial slots and stride >= 98");
   const size_t items = n_rounds * m_slots;
   for (size_t i = 0; i < items; ++i)

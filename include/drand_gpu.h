@@ -87,6 +87,11 @@ enum {
 
 enum { DGPU_MODE_PER_ROUND = 0, DGPU_MODE_RLC = 1 };
 
+/* Empty batches: every batch entry point (verify, verify_recovered, recover,
+ * their _device and _multi forms) returns DGPU_OK for n = 0 rounds without
+ * reading or writing any buffer, and accepts NULL record / output pointers
+ * then (tests/test_gpu_boundary.py::test_empty_batches_are_no_ops). */
+
 typedef struct dgpu_ctx dgpu_ctx;
 
 int dgpu_abi_version(void);

@@ -524,7 +524,8 @@ int rlc_root_msm_t(dgpu_ctx* c, const verify_args& a, hipStream_t s, uint32_t* r
   using M = GrMem<Gr>;
   const unsigned B = 256;
   const size_t n = a.n;
-  if (n > 0xFFFFFFFFull) return set_err(DGPU_EINVAL, "RLC batch too large (%zu)", n);
+  // list positions and bucket offsets are 32-bit: up to MSM_MW entries per round
+  if (n > 0xFFFFFFFFull / MSM_MW) return set_err(DGPU_EINVAL, "RLC batch too large for one MSM (%zu rounds)", n);
   int rc;
   if ((rc = c->msm_aos.ensure(2 * n * M::AFF * 4)) || (rc = c->msm_flags.ensure(n)) ||
       (rc = c->msm_counts.ensure(3 * MSM_KEYS * 4)) || (rc = c->msm_list.ensure(2 * MSM_MW * n * 4 + 4)) ||

@@ -222,6 +222,7 @@ struct dgpu_ctx {
   DevBuf rec_tab, rec_tabz, rec_tabpre;  // the batched check's shared affine window tables
   DevBuf rec_tab_rows;                   // ... as 224-byte rows (the gather layout; r05l)
   bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
+  bool dec_overlap = true;       // one-lane per-round calls decode on stream2 beside the hash (DGPU_DEC_OVERLAP=0: off)
   bool msm_seg = true;           // load-balanced bucket sums (k_msm_bucket_seg); DGPU_MSM_SEG=0: one thread per bucket (A/B)
   int n_cu = 256;                // compute units (the load-balanced sums launch one wave per SIMD slot)
   bool recover_rows = true;      // the MSM gathers its window tables as rows (DGPU_RECOVER_ROWS=0: SoA planes, A/B)
@@ -1024,8 +1025,12 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
 
 // Per-round G2 path, first half of one lane: hash-to-G2 (field, SSWU, finish),
 // batch affine, signature decode of `n` items into the lane's buffers.
+// s_dec (optional): the signature decode runs on that stream, beside the hash
+// chain on s (it reads only the records and writes sig_pts and the statuses);
+// s waits for it before returning.
 int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src& m, const uint8_t* sigs,
-                        size_t sig_stride, const uint32_t* sig_len, uint8_t* st, hipStream_t s) {
+                        size_t sig_stride, const uint32_t* sig_len, uint8_t* st, hipStream_t s,
+                        hipStream_t s_dec = nullptr) {
   const unsigned B = 256;
   int rc;
   if ((rc = L.h_pts->ensure(n * G2A_WORDS * 4)) || (rc = L.sig_pts->ensure(n * G2A_WORDS * 4)) ||
@@ -1036,6 +1041,10 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   uint32_t* sg = (uint32_t*)L.sig_pts->p;
   uint32_t* u = (uint32_t*)L.h_tmp->p;
   uint32_t* q = u + 4 * FP_WORDS * n;
+  if (s_dec) {
+    HIP_TRY(hipEventRecord(c->lane_ev[0], s));
+    HIP_TRY(hipStreamWaitEvent(s_dec, c->lane_ev[0], 0));
+  }
   mark(c, s, "hash_to_g2");
   hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, m, u);
   HIP_TRY(hipGetLastError());
@@ -1048,15 +1057,20 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
                      (const uint32_t*)L.h_z->p, (uint32_t*)L.h_pre->p);
   HIP_TRY(hipGetLastError());
-  mark(c, s, "decode_g2");
+  const hipStream_t sd = s_dec ? s_dec : s;
+  if (!s_dec) mark(c, s, "decode_g2");
   // membership of the signature: checked by the lines kernel (eng_pairing_locked sig_subgroup)
   if (c->decode_subgroup)
-    hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m, sg,
+    hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, B)), dim3(B), 0, sd, n, sigs, sig_stride, sig_len, m, sg,
                        st);
   else
-    hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, sigs, sig_stride, sig_len, m, 0, sg,
+    hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, sd, n, sigs, sig_stride, sig_len, m, 0, sg,
                        st);
   HIP_TRY(hipGetLastError());
+  if (s_dec) {
+    HIP_TRY(hipEventRecord(c->lane_ev[1], s_dec));
+    HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
+  }
   return DGPU_OK;
 }
 
@@ -1138,7 +1152,10 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   const bool two = c->lanes > 1 && !c->profile && n >= LANE_MIN;
   const size_t slices = two ? std::max<size_t>(2, c->lane_slices) : 1;
   const size_t n0 = two ? ((n / slices + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
-  if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s))) return rc;
+  // one lane: the decode overlaps the hash on the second stream (small calls:
+  // the decode's ~0.9 ms leaves the critical path; DGPU_DEC_OVERLAP=0 off)
+  const hipStream_t s_dec = (!two && c->dec_overlap && !c->profile) ? c->stream2 : nullptr;
+  if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec))) return rc;
   const bool sub = !c->decode_subgroup;
   if (!two)
     return eng_pairing_locked(c, consts, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
@@ -1291,6 +1308,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   dgpu_ctx* c = new dgpu_ctx();
   c->device = device;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  const char* dov = getenv("DGPU_DEC_OVERLAP");
+  if (dov && !strcmp(dov, "0")) c->dec_overlap = false;
   const char* msv = getenv("DGPU_MSM_SEG");
   if (msv && !strcmp(msv, "0")) c->msm_seg = false;
   const char* lv = getenv("DGPU_LANES");

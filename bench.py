@@ -87,6 +87,8 @@ def parse(argv=None):
                          "DGPU_MULTI_ALLOW_SAME_DEVICE=1)")
     ap.add_argument("--abi-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-small-batch", action="store_true", help="skip the small-batch latency leg")
+    ap.add_argument("--small-batch-sizes", default=None,
+                    help="comma-separated call sizes for the small-batch leg (default 1,8,64,500,4096)")
     ap.add_argument("--small-batch-only", action="store_true",
                     help="only the small-batch latency leg (host records, n = 1 .. 4096) on a 4096-round chain")
     ap.add_argument("--dry-run", action="store_true",
@@ -920,9 +922,10 @@ def main():
         from drand_amd import _lib
         from drand_amd.synth import corrupt, make_chain
         code = _lib.load().dgpu_scheme_from_name(args.scheme.encode())
-        ch = make_chain(args.seed, max(SMALL_BATCH_SIZES), code, seg_len=args.seg_len)
+        sizes = tuple(int(x) for x in args.small_batch_sizes.split(",")) if args.small_batch_sizes else SMALL_BATCH_SIZES
+        ch = make_chain(args.seed, max(sizes), code, seg_len=args.seg_len)
         corrupt(ch, args.seed, rate=args.corrupt_rate)
-        print(json.dumps(small_batch_leg(ch, args.scheme)), flush=True)
+        print(json.dumps(small_batch_leg(ch, args.scheme, sizes=sizes)), flush=True)
         return
     if os.environ.get("DRAND_BENCH_DRYRUN"):
         return dryrun(args)

@@ -191,6 +191,8 @@ struct dgpu_ctx {
   // second lane's scratch (same roles as h_pts .. eng_kb)
   DevBuf l2_h_pts, l2_sig_pts, l2_h_z, l2_h_pre, l2_h_tmp, l2_lines, l2_f, l2_n1, l2_kb;
   bool fe_gs = false;            // DGPU_FE=gs: the Granger-Scott FE kernel instead of the Karabina chain (A/B)
+  size_t fe_gs_max = 16384;      // DGPU_FE_GS_MAX=<items>: pairing calls up to this size take the Granger-Scott FE
+                                 // (one launch, no batched inversions: the latency path; 0 = always Karabina)
   size_t kb_inv_chain = 16;      // DGPU_KB_INV_CHAIN: norms per k_eng_inv thread in the Karabina FE (A/B)
   size_t kb_test_flag = 0;       // DGPU_KB_TEST_FLAG=k (tests): flag every k-th item so the fallback runs
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
@@ -222,6 +224,9 @@ struct dgpu_ctx {
   DevBuf rec_tab, rec_tabz, rec_tabpre;  // the batched check's shared affine window tables
   DevBuf rec_tab_rows;                   // ... as 224-byte rows (the gather layout; r05l)
   bool recover_exact = false;    // DGPU_RECOVER=exact: every round on the per-partial path (A/B)
+  size_t cof_engine_max = 16384;  // DGPU_COF_ENGINE_MAX=<rounds>: calls up to this size clear the hash cofactor on
+                                 // the engine ladder (k_cof_*; 0 = always k_h2c_finish)
+  DevBuf cof_tmp;                // its scratch planes
   bool dec_overlap = true;       // one-lane per-round calls decode on stream2 beside the hash (DGPU_DEC_OVERLAP=0: off)
   bool msm_seg = true;           // load-balanced bucket sums (k_msm_bucket_seg); DGPU_MSM_SEG=0: one thread per bucket (A/B)
   int n_cu = 256;                // compute units (the load-balanced sums launch one wave per SIMD slot)
@@ -387,7 +392,8 @@ int decode_g2_key_locked(dgpu_ctx* c, key_entry* e, const uint8_t* pk) {
   }
   hipLaunchKernelGGL(k_eng_lines, dim3(1), dim3(ENG_BLOCK), 0, s, (size_t)1, (size_t)0, (size_t)1,
                      (const uint32_t*)d_pk, (size_t)1, (const uint32_t*)nullptr, (const uint32_t*)d_g2,
-                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)e->table.p, (uint8_t*)nullptr);
+                     (const uint32_t*)nullptr, (const uint32_t*)unit.p, (uint32_t*)e->table.p, (uint8_t*)nullptr,
+                     (uint32_t*)nullptr);
   err = hipGetLastError();
   if (err == hipSuccess) err = hipStreamSynchronize(s);
   unit.release();
@@ -923,6 +929,9 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
   DevBuf* b_n1 = L ? L->n1 : &c->eng_n1;
   DevBuf* b_kb = L ? L->kb : &c->eng_kb;
   const bool need_lines = !(fixed_table && c->fused_fixed);
+  // small calls: the Granger-Scott FE (one launch; the Karabina side's five
+  // chain / norm / batched-inversion / decompression rounds are latency there)
+  const bool fe_gs = c->fe_gs || n <= c->fe_gs_max;
   int rc;
   size_t cap = 0, cap_blk = 0;
   for (;;) {
@@ -932,7 +941,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
     cap = std::min(n, (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK * ENG_ROUNDS_PER_BLOCK);
     cap_blk = (cap + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK;  // blocked layouts
     // the Karabina planes are wave-blocked: whole blocks of 5 rounds (cap may be n, not a multiple of 5)
-    rc = c->fe_gs ? DGPU_OK : b_kb->ensure(cap_blk * ENG_ROUNDS_PER_BLOCK * ENG_KB_BYTES_PER_ROUND);
+    rc = fe_gs ? DGPU_OK : b_kb->ensure(cap_blk * ENG_ROUNDS_PER_BLOCK * ENG_KB_BYTES_PER_ROUND);
     if (!rc && need_lines) rc = b_lines->ensure(cap_blk * (size_t)ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4);
     if (!rc) rc = b_f->ensure(cap_blk * 2 * FP_LIMBS * ENG_WAVE_WORDS * 4);
     if (!rc) rc = b_n1->ensure(cap * FP_LIMBS * 4);
@@ -973,7 +982,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                              sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
         else
           hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, r0, cnt, h, h_stride, h_idx, sg,
-                           pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
+                           pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr, (uint32_t*)nullptr);
       }
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_miller");
@@ -984,7 +993,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
     mark(c, s, "eng_inv");
     hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, n1, pre, st);
     HIP_TRY(hipGetLastError());
-    if (c->fe_gs) {
+    if (fe_gs) {
       mark(c, s, "eng_fe");
       hipLaunchKernelGGL(k_eng_fe, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1, st);
       HIP_TRY(hipGetLastError());
@@ -1028,9 +1037,12 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
 // s_dec (optional): the signature decode runs on that stream, beside the hash
 // chain on s (it reads only the records and writes sig_pts and the statuses);
 // s waits for it before returning.
+// consts (the key's engine constants; optional): calls of at most
+// cof_engine_max rounds clear the cofactor on the engine ladder
+// (pairing_engine.cuh k_cof_*) instead of k_h2c_finish.
 int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src& m, const uint8_t* sigs,
                         size_t sig_stride, const uint32_t* sig_len, uint8_t* st, hipStream_t s,
-                        hipStream_t s_dec = nullptr) {
+                        hipStream_t s_dec = nullptr, const uint32_t* consts = nullptr) {
   const unsigned B = 256;
   int rc;
   if ((rc = L.h_pts->ensure(n * G2A_WORDS * 4)) || (rc = L.sig_pts->ensure(n * G2A_WORDS * 4)) ||
@@ -1050,8 +1062,35 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
-                     (uint32_t*)L.h_z->p);
+  if (consts && n <= c->cof_engine_max) {
+    const unsigned blocks = grid_for(n, ENG_ROUNDS_PER_BLOCK);
+    if ((rc = c->cof_tmp.ensure((size_t)COF_PLANES * FP_WORDS * n * 4)) ||
+        (rc = L.lines->ensure((size_t)blocks * ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4)))
+      return rc;
+    uint32_t* w = (uint32_t*)c->cof_tmp.p;
+    uint32_t* pa = w + (size_t)G2J_WORDS * n;
+    uint32_t* psia = pa + (size_t)G2A_WORDS * n;
+    uint32_t* t1 = psia + (size_t)G2A_WORDS * n;
+    uint32_t* t0a = t1 + (size_t)12 * FP_WORDS * n;
+    uint32_t* t2 = t0a + (size_t)G2A_WORDS * n;
+    uint32_t* lines = (uint32_t*)L.lines->p;
+    hipLaunchKernelGGL(k_cof_prep, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, w);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, (size_t)0, n,
+                       (const uint32_t*)pa, n, (const uint32_t*)nullptr, (const uint32_t*)psia, (const uint32_t*)nullptr,
+                       consts, lines, (uint8_t*)nullptr, t1);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_cof_mid, dim3(grid_for(n, B)), dim3(B), 0, s, n, w);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, (size_t)0, n,
+                       (const uint32_t*)t0a, n, (const uint32_t*)nullptr, (const uint32_t*)t0a, (const uint32_t*)nullptr,
+                       consts, lines, (uint8_t*)nullptr, t2);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_cof_final, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)w, h, (uint32_t*)L.h_z->p);
+  } else {
+    hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
+                       (uint32_t*)L.h_z->p);
+  }
   HIP_TRY(hipGetLastError());
   mark(c, s, "h_affine");
   hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
@@ -1155,7 +1194,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   // one lane: the decode overlaps the hash on the second stream (small calls:
   // the decode's ~0.9 ms leaves the critical path; DGPU_DEC_OVERLAP=0 off)
   const hipStream_t s_dec = (!two && c->dec_overlap && !c->profile) ? c->stream2 : nullptr;
-  if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec))) return rc;
+  if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec, consts))) return rc;
   const bool sub = !c->decode_subgroup;
   if (!two)
     return eng_pairing_locked(c, consts, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
@@ -1308,6 +1347,10 @@ int dgpu_open(int device, dgpu_ctx** out) {
   dgpu_ctx* c = new dgpu_ctx();
   c->device = device;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  const char* fgv = getenv("DGPU_FE_GS_MAX");
+  if (fgv && atol(fgv) >= 0) c->fe_gs_max = (size_t)atol(fgv);
+  const char* cev = getenv("DGPU_COF_ENGINE_MAX");
+  if (cev && atol(cev) >= 0) c->cof_engine_max = (size_t)atol(cev);
   const char* dov = getenv("DGPU_DEC_OVERLAP");
   if (dov && !strcmp(dov, "0")) c->dec_overlap = false;
   const char* msv = getenv("DGPU_MSM_SEG");
@@ -1393,7 +1436,7 @@ void dgpu_close(dgpu_ctx* c) {
                     &c->rec_tab, &c->rec_tabz, &c->rec_tabpre, &c->rec_tab_rows,
                     &c->eng_consts, &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb, &c->l2_kb,
                     &c->rlc_tree, &c->rlc_idx, &c->rlc_fail, &c->rlc_h, &c->rlc_s, &c->rlc_st, &c->rlc_root,
-                    &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs, &c->msm_part,
+                    &c->msm_aos, &c->msm_flags, &c->msm_counts, &c->msm_list, &c->msm_buckets, &c->msm_runs, &c->msm_part, &c->cof_tmp,
                     &c->msm_root,
                     &c->h_pts, &c->sig_pts, &c->status, &c->h_z, &c->h_pre, &c->h_tmp, &c->in_rounds, &c->in_sigs,
                     &c->in_sig_len, &c->in_prev, &c->in_prev_len, &c->in_msgs, &c->in_msg_len, &c->out_bits,

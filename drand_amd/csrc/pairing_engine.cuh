@@ -199,7 +199,8 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
                                                          const uint32_t* __restrict__ pk_items,
                                                          const uint32_t* __restrict__ consts,
                                                          uint32_t* __restrict__ lines,
-                                                         uint8_t* __restrict__ status) {
+                                                         uint8_t* __restrict__ status,
+                                                         uint32_t* __restrict__ t_out) {
   __shared__ uint32_t lds[ENG_LDS_SLOTS_LINES * ENG_SLOT_WORDS];
   uint32_t* c = lds;
   eng_load_consts(c, consts);
@@ -231,6 +232,72 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
     const bool in_g2 = (gm & 0xFull) == 0xFull && (gm & 0x30ull) != 0x30ull;
     if (L.valid && L.k == 0 && !in_g2 && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_SUBGROUP;
   }
+  if (t_out && L.valid) {  // T of both pairs (homogeneous X, Y, Z): [12 fp][cnt], lane k = 6 pair + component
+    const int pr = L.k / 6, comp = L.k - 6 * pr;
+    st_soa(t_out + (size_t)L.k * FP_LIMBS * cnt, cnt, L.i, eng_ld(g + (pr * ENG_LINE_PAIR_SLOTS + comp) * ENG_SLOT_WORDS));
+  }
+}
+
+// ---------------------------------------------------------------- small-batch cofactor clearing
+// For a call of a few thousand rounds k_h2c_finish is one thread's 126
+// sequential doublings per round (~4.4 ms at n = 1).  Its two ladders run
+// instead on the 12-lane LINES program, whose T after the loop is [|x|]Q
+// (k_eng_lines' t_out; the line coefficients go to a scratch buffer):
+//   k_cof_prep   P = Q0 + Q1 (Jacobian kept); P and psi(P) affine
+//   k_eng_lines  T0 = [|x|]P, T1 = [|x|]psi(P)            (homogeneous)
+//   k_cof_mid    T0 affine: the second pass's input
+//   k_eng_lines  T2 = [|x|]T0 = [x^2]P
+//   k_cof_final  h_eff P = T2 + T0 - P - T1 - psi(P) + psi^2(2P)
+// with [x]P = -T0, [x]psi(P) = -T1: RFC 9380 G.3's [x^2 - x - 1]P +
+// [x - 1]psi(P) + psi^2(2P) regrouped, written as k_h2c_finish writes it
+// (X, Y to h_out, Z to z_out).  Exceptional ladder steps need P of order
+// below 2^64 + 1 -- a hash output is not (every point the ladder meets is
+// then a nonzero multiple of a large-order point); the additions here are
+// the complete g2_add.
+// Scratch planes (stride n): pj [6] | pa [4] | psia [4] | t1 [12] | t0a [4] | t2 [12]
+constexpr int COF_PLANES = 6 + 4 + 4 + 12 + 4 + 12;
+__device__ __forceinline__ g2j cof_homog_to_jac(const uint32_t* t, size_t n, size_t i, int pr) {
+  const uint32_t* b = t + (size_t)pr * 6 * FP_LIMBS * n;
+  const fp2 X{ld_soa(b, n, i), ld_soa(b + FP_LIMBS * n, n, i)};
+  const fp2 Y{ld_soa(b + 2 * FP_LIMBS * n, n, i), ld_soa(b + 3 * FP_LIMBS * n, n, i)};
+  const fp2 Z{ld_soa(b + 4 * FP_LIMBS * n, n, i), ld_soa(b + 5 * FP_LIMBS * n, n, i)};
+  return g2j{fp2_mul(X, Z), fp2_mul(Y, fp2_sqr(Z)), Z};  // x = X/Z = XZ/Z^2, y = Y/Z = YZ^2/Z^3
+}
+__global__ void __launch_bounds__(256) k_cof_prep(size_t n, const uint32_t* __restrict__ q, uint32_t* __restrict__ w) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const g2j P = g2_add(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i));
+  st_g2j(w, n, i, P);
+  const g2a a = g2_to_affine(P);
+  st_g2a(w + G2J_WORDS * n, n, i, a);
+  const g2j s = g2_psi(g2_from_affine(a));  // Z = conj(1) = 1: still affine
+  st_g2a(w + (G2J_WORDS + G2A_WORDS) * n, n, i, g2a{s.x, s.y});
+}
+__global__ void __launch_bounds__(256) k_cof_mid(size_t n, uint32_t* __restrict__ w) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* t1 = w + (G2J_WORDS + 2 * G2A_WORDS) * n;
+  const fp2 zi = fp2_inv(fp2{ld_soa(t1 + 4 * FP_LIMBS * n, n, i), ld_soa(t1 + 5 * FP_LIMBS * n, n, i)});
+  const fp2 X{ld_soa(t1, n, i), ld_soa(t1 + FP_LIMBS * n, n, i)};
+  const fp2 Y{ld_soa(t1 + 2 * FP_LIMBS * n, n, i), ld_soa(t1 + 3 * FP_LIMBS * n, n, i)};
+  st_g2a(w + (G2J_WORDS + 2 * G2A_WORDS + 12 * FP_WORDS) * n, n, i, g2a{fp2_mul(X, zi), fp2_mul(Y, zi)});
+}
+__global__ void __launch_bounds__(256) k_cof_final(size_t n, const uint32_t* __restrict__ w, uint32_t* __restrict__ h_out,
+                                                   uint32_t* __restrict__ z_out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* t1 = w + (G2J_WORDS + 2 * G2A_WORDS) * n;
+  const uint32_t* t2 = t1 + (12 * FP_WORDS + G2A_WORDS) * n;
+  const g2j P = ld_g2j(w, n, i);
+  g2j h = g2_add(cof_homog_to_jac(t2, n, i, 0), cof_homog_to_jac(t1, n, i, 0));  // [x^2]P - [x]P
+  h = g2_add(h, g2_neg(P));
+  h = g2_add(h, g2_neg(cof_homog_to_jac(t1, n, i, 1)));                            // + [x]psi(P)
+  const g2j sp = g2_psi(P);
+  h = g2_add(h, g2_neg(sp));
+  h = g2_add(h, g2_psi2(g2_dbl(P)));
+  st_g2a(h_out, n, i, g2a{h.x, h.y});
+  st_fp(z_out, n, i, h.z.c0);
+  st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
 }
 
 // ---------------------------------------------------------------- k_eng_miller

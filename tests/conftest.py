@@ -18,6 +18,13 @@ os.environ.setdefault("DGPU_RLC_MIN", "0")
 # per-thread kernels the bulk path uses.  Tests that compare the two kernel
 # families set it (or DGPU_LINES / DGPU_KB_CHAIN) on their own contexts.
 os.environ.setdefault("DGPU_THR_MIN", "0")
+# Likewise calls up to 16Ki rounds clear the hash cofactor on the engine
+# ladder (DGPU_COF_ENGINE_MAX) and take the Granger-Scott final
+# exponentiation (DGPU_FE_GS_MAX); the suite turns both latency paths off so
+# its small batches run k_h2c_finish and the Karabina FE of the bulk path.
+# tests/test_gpu_defaults.py runs the library defaults (both paths on).
+os.environ.setdefault("DGPU_COF_ENGINE_MAX", "0")
+os.environ.setdefault("DGPU_FE_GS_MAX", "0")
 HOSTSIM = os.path.join(ROOT, "tests", "hostsim", "libdrand_hostsim.so")
 
 

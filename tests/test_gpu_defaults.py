@@ -1,10 +1,12 @@
 """The shipped kernel-selection thresholds: tests/conftest.py
-sets DGPU_THR_MIN=0 and DGPU_RLC_MIN=0 for the suite so that its small
-batches run the per-thread kernels and the RLC pipeline the bulk path uses.
+sets DGPU_THR_MIN=0, DGPU_RLC_MIN=0, DGPU_COF_ENGINE_MAX=0 and DGPU_FE_GS_MAX=0
+for the suite so that its small batches run the per-thread kernels, the RLC
+pipeline, k_h2c_finish and the Karabina FE the bulk path uses.
 These tests open fresh contexts at the library's defaults instead
 (DGPU_THR_MIN=65536: pairing chunks under 64Ki items on the 12-lane lines and
 8-lane chain; DGPU_RLC_MIN=131072: smaller RLC-mode calls on the per-round
-path) for the pipelines the chained-G2 default tests in test_gpu_parity.py
+path; DGPU_COF_ENGINE_MAX=16384 / DGPU_FE_GS_MAX=16384: small calls clear the
+hash cofactor on the engine ladder and take the Granger-Scott FE) for the pipelines the chained-G2 default tests in test_gpu_parity.py
 do not cover: G1 signatures per round and in RLC mode (a call above the RLC
 threshold, so the combination runs with its node checks on the lane
 kernels), and threshold recovery.  Verdicts equal the construction / golden
@@ -23,14 +25,16 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-DEFAULTS = {"DGPU_THR_MIN": "65536", "DGPU_RLC_MIN": "131072"}
+DEFAULTS = {"DGPU_THR_MIN": "65536", "DGPU_RLC_MIN": "131072", "DGPU_COF_ENGINE_MAX": "16384",
+            "DGPU_FE_GS_MAX": "16384"}
 
 
 @contextlib.contextmanager
-def _default_ctx():
+def _default_ctx(extra=None):
     from drand_amd import _lib
-    saved = {k: os.environ.get(k) for k in DEFAULTS}
-    os.environ.update(DEFAULTS)
+    env = dict(DEFAULTS, **(extra or {}))
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         ctx = _lib.Context(0)
     finally:
@@ -155,3 +159,23 @@ def test_recover_batched_check_table_layouts(rows):
                 os.environ["DGPU_RECOVER_ROWS"] = saved
         sigs, _ = unpack_recovered(out, ok, None, partials, m)
         assert [s.hex() if s else None for s in sigs] == [c["recovered"] for c in g["cases"]], name
+
+
+@pytest.mark.parametrize("cof_max,fe_max", [("0", "0"), ("16384", "0"), ("0", "16384"), ("16384", "16384")])
+@pytest.mark.parametrize("n", [1, 7, 4099])
+def test_small_calls_latency_paths(cof_max, fe_max, n):
+    """The small-call latency paths, each on and off: per-round calls up to
+    DGPU_COF_ENGINE_MAX rounds clear the hash's cofactor on the 12-lane
+    ladder (pairing_engine.cuh k_cof_*) instead of k_h2c_finish, and pairing
+    calls up to DGPU_FE_GS_MAX items take the Granger-Scott FE instead of the
+    Karabina side.  A chained chain with 1% corrupted rounds gives the
+    construction's verdicts in every combination."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    c = make_chain(97 + n, n, _lib.SCHEME_CHAINED, seg_len=min(64, n))
+    bad = corrupt(c, 97, rate=1e-2) if n > 50 else {}
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    with _default_ctx({"DGPU_COF_ENGINE_MAX": cof_max, "DGPU_FE_GS_MAX": fe_max}) as ctx:
+        per = _verify(ctx, _lib.SCHEME_CHAINED, c, _lib.MODE_PER_ROUND)
+    assert np.array_equal(per == 0, expect)

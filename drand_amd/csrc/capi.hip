@@ -169,6 +169,7 @@ struct dgpu_ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // second lane of the per-round G2 path
   hipEvent_t lane_ev[2] = {nullptr, nullptr};
+  hipEvent_t cof_ev[2] = {nullptr, nullptr};  // the small-call cofactor path's second-stream join
   // end of the last call's enqueued work: every call orders its stream after it
   hipEvent_t done = nullptr;
   std::mutex mu;
@@ -1053,9 +1054,21 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   uint32_t* sg = (uint32_t*)L.sig_pts->p;
   uint32_t* u = (uint32_t*)L.h_tmp->p;
   uint32_t* q = u + 4 * FP_WORDS * n;
-  if (s_dec) {
+  // membership of the signature: checked by the lines kernel (eng_pairing_locked sig_subgroup)
+  auto decode = [&](hipStream_t sd) {
+    if (c->decode_subgroup)
+      hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, B)), dim3(B), 0, sd, n, sigs, sig_stride, sig_len, m,
+                         sg, st);
+    else
+      hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, sd, n, sigs, sig_stride, sig_len, m, 0,
+                         sg, st);
+    return hipGetLastError();
+  };
+  if (s_dec) {  // first in the second stream's queue: it runs beside the whole hash chain
     HIP_TRY(hipEventRecord(c->lane_ev[0], s));
     HIP_TRY(hipStreamWaitEvent(s_dec, c->lane_ev[0], 0));
+    HIP_TRY(decode(s_dec));
+    HIP_TRY(hipEventRecord(c->lane_ev[1], s_dec));
   }
   mark(c, s, "hash_to_g2");
   hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, m, u);
@@ -1082,10 +1095,21 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_cof_mid, dim3(grid_for(n, B)), dim3(B), 0, s, n, w);
     HIP_TRY(hipGetLastError());
+    // U (everything but [x^2]P) on the second stream beside the second pass
+    const bool side = s_dec != nullptr;
+    const hipStream_t su = side ? s_dec : s;
+    if (side) {
+      HIP_TRY(hipEventRecord(c->cof_ev[0], s));
+      HIP_TRY(hipStreamWaitEvent(su, c->cof_ev[0], 0));
+    }
+    hipLaunchKernelGGL(k_cof_partial, dim3(grid_for(n, B)), dim3(B), 0, su, n, w);
+    HIP_TRY(hipGetLastError());
+    if (side) HIP_TRY(hipEventRecord(c->cof_ev[1], su));
     hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, (size_t)0, n,
                        (const uint32_t*)t0a, n, (const uint32_t*)nullptr, (const uint32_t*)t0a, (const uint32_t*)nullptr,
                        consts, lines, (uint8_t*)nullptr, t2);
     HIP_TRY(hipGetLastError());
+    if (side) HIP_TRY(hipStreamWaitEvent(s, c->cof_ev[1], 0));
     hipLaunchKernelGGL(k_cof_final, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)w, h, (uint32_t*)L.h_z->p);
   } else {
     hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
@@ -1096,19 +1120,11 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   hipLaunchKernelGGL(k_g2_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
                      (const uint32_t*)L.h_z->p, (uint32_t*)L.h_pre->p);
   HIP_TRY(hipGetLastError());
-  const hipStream_t sd = s_dec ? s_dec : s;
-  if (!s_dec) mark(c, s, "decode_g2");
-  // membership of the signature: checked by the lines kernel (eng_pairing_locked sig_subgroup)
-  if (c->decode_subgroup)
-    hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, B)), dim3(B), 0, sd, n, sigs, sig_stride, sig_len, m, sg,
-                       st);
-  else
-    hipLaunchKernelGGL(k_decode_g2_sigs, dim3(grid_for(n, B)), dim3(B), 0, sd, n, sigs, sig_stride, sig_len, m, 0, sg,
-                       st);
-  HIP_TRY(hipGetLastError());
   if (s_dec) {
-    HIP_TRY(hipEventRecord(c->lane_ev[1], s_dec));
-    HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
+    HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));  // the decode (queued first on s_dec)
+  } else {
+    mark(c, s, "decode_g2");
+    HIP_TRY(decode(s));
   }
   return DGPU_OK;
 }
@@ -1401,6 +1417,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[1], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->cof_ev[0], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->cof_ev[1], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     dgpu_close(c);
@@ -1423,6 +1441,8 @@ void dgpu_close(dgpu_ctx* c) {
   if (c->done) hipEventSynchronize(c->done);
   for (hipEvent_t e : c->ev) hipEventDestroy(e);
   for (hipEvent_t e : c->lane_ev)
+    if (e) hipEventDestroy(e);
+  for (hipEvent_t e : c->cof_ev)
     if (e) hipEventDestroy(e);
   if (c->done) hipEventDestroy(c->done);
   for (key_entry& k : c->keys) {

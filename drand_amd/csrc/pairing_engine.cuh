@@ -246,16 +246,16 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_lines(size_t n, size_t r0,
 //   k_cof_prep   P = Q0 + Q1 (Jacobian kept); P and psi(P) affine
 //   k_eng_lines  T0 = [|x|]P, T1 = [|x|]psi(P)            (homogeneous)
 //   k_cof_mid    T0 affine: the second pass's input
-//   k_eng_lines  T2 = [|x|]T0 = [x^2]P
-//   k_cof_final  h_eff P = T2 + T0 - P - T1 - psi(P) + psi^2(2P)
+//   k_eng_lines  T2 = [|x|]T0 = [x^2]P    beside   k_cof_partial  U = T0 - P - T1 - psi(P) + psi^2(2P)
+//   k_cof_final  h_eff P = T2 + U
 // with [x]P = -T0, [x]psi(P) = -T1: RFC 9380 G.3's [x^2 - x - 1]P +
 // [x - 1]psi(P) + psi^2(2P) regrouped, written as k_h2c_finish writes it
 // (X, Y to h_out, Z to z_out).  Exceptional ladder steps need P of order
 // below 2^64 + 1 -- a hash output is not (every point the ladder meets is
 // then a nonzero multiple of a large-order point); the additions here are
 // the complete g2_add.
-// Scratch planes (stride n): pj [6] | pa [4] | psia [4] | t1 [12] | t0a [4] | t2 [12]
-constexpr int COF_PLANES = 6 + 4 + 4 + 12 + 4 + 12;
+// Scratch planes (stride n): pj [6] | pa [4] | psia [4] | t1 [12] | t0a [4] | t2 [12] | u [6]
+constexpr int COF_PLANES = 6 + 4 + 4 + 12 + 4 + 12 + 6;
 __device__ __forceinline__ g2j cof_homog_to_jac(const uint32_t* t, size_t n, size_t i, int pr) {
   const uint32_t* b = t + (size_t)pr * 6 * FP_LIMBS * n;
   const fp2 X{ld_soa(b, n, i), ld_soa(b + FP_LIMBS * n, n, i)};
@@ -282,19 +282,26 @@ __global__ void __launch_bounds__(256) k_cof_mid(size_t n, uint32_t* __restrict_
   const fp2 Y{ld_soa(t1 + 2 * FP_LIMBS * n, n, i), ld_soa(t1 + 3 * FP_LIMBS * n, n, i)};
   st_g2a(w + (G2J_WORDS + 2 * G2A_WORDS + 12 * FP_WORDS) * n, n, i, g2a{fp2_mul(X, zi), fp2_mul(Y, zi)});
 }
+// U = T0 - P - T1 - psi(P) + psi^2(2P): everything but [x^2]P, from the
+// first pass alone -- it runs on a second stream beside the second pass
+__global__ void __launch_bounds__(256) k_cof_partial(size_t n, uint32_t* __restrict__ w) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* t1 = w + (G2J_WORDS + 2 * G2A_WORDS) * n;
+  const g2j P = ld_g2j(w, n, i);
+  g2j u = g2_add(cof_homog_to_jac(t1, n, i, 0), g2_neg(P));                       // -[x]P - P
+  u = g2_add(u, g2_neg(cof_homog_to_jac(t1, n, i, 1)));                            // + [x]psi(P)
+  u = g2_add(u, g2_neg(g2_psi(P)));
+  u = g2_add(u, g2_psi2(g2_dbl(P)));
+  st_g2j(w + (G2J_WORDS + 3 * G2A_WORDS + 24 * FP_WORDS) * n, n, i, u);
+}
+// h_eff P = [x^2]P + U
 __global__ void __launch_bounds__(256) k_cof_final(size_t n, const uint32_t* __restrict__ w, uint32_t* __restrict__ h_out,
                                                    uint32_t* __restrict__ z_out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t* t1 = w + (G2J_WORDS + 2 * G2A_WORDS) * n;
-  const uint32_t* t2 = t1 + (12 * FP_WORDS + G2A_WORDS) * n;
-  const g2j P = ld_g2j(w, n, i);
-  g2j h = g2_add(cof_homog_to_jac(t2, n, i, 0), cof_homog_to_jac(t1, n, i, 0));  // [x^2]P - [x]P
-  h = g2_add(h, g2_neg(P));
-  h = g2_add(h, g2_neg(cof_homog_to_jac(t1, n, i, 1)));                            // + [x]psi(P)
-  const g2j sp = g2_psi(P);
-  h = g2_add(h, g2_neg(sp));
-  h = g2_add(h, g2_psi2(g2_dbl(P)));
+  const uint32_t* t2 = w + (G2J_WORDS + 3 * G2A_WORDS + 12 * FP_WORDS) * n;
+  const g2j h = g2_add(cof_homog_to_jac(t2, n, i, 0), ld_g2j(t2 + 12 * FP_WORDS * n, n, i));
   st_g2a(h_out, n, i, g2a{h.x, h.y});
   st_fp(z_out, n, i, h.z.c0);
   st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);

@@ -441,10 +441,18 @@ def small_batch_leg(chain, scheme, sizes=SMALL_BATCH_SIZES, budget_s=20.0):
         k = 8
         sub = [np.ascontiguousarray(a[:k]) for a in (chain.rounds, chain.sigs, chain.sig_len, chain.prev,
                                                      chain.prev_len)]
-        c_ref.verify_batch(code == _lib.SCHEME_CHAINED, chain.pk, *sub, 1)  # warm
+        g1 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
+
+        def cpu():
+            if g1:  # G1 signatures: the restatement's own entry (G2 key, RFC 9380 or drand DST)
+                return c_ref.verify_batch_g1(code == _lib.SCHEME_G1_RFC9380, chain.pk, sub[0], sub[1], sub[2], 1)
+            return c_ref.verify_batch(code == _lib.SCHEME_CHAINED, chain.pk, *sub, 1)
+        cpu()  # warm
         t0 = time.perf_counter()
-        c_ref.verify_batch(code == _lib.SCHEME_CHAINED, chain.pk, *sub, 1)
+        ref = cpu()
         cpu_ms_per_round = (time.perf_counter() - t0) * 1e3 / k
+        if int((ref != 0).sum()) > k // 2:  # a timing of rejected records would be meaningless
+            raise RuntimeError("C port rejected the sample")
     except Exception as e:  # reported, never fatal
         log(f"small-batch: no C port timing ({e!r})")
     rows = []

@@ -1017,6 +1017,16 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
     return rc;
   uint32_t* h = (uint32_t*)c->h_pts.p;
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
+  // the signature decode beside the hash on the second stream (as the G2 path, g2_lane_hash_locked)
+  const bool side = c->dec_overlap && !c->profile;
+  if (side) {
+    HIP_TRY(hipEventRecord(c->lane_ev[0], s));
+    HIP_TRY(hipStreamWaitEvent(c->stream2, c->lane_ev[0], 0));
+    hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, c->stream2, n, a.sigs, a.sig_stride,
+                       a.sig_len, a.m, sg, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->lane_ev[1], c->stream2));
+  }
   mark(c, s, "hash_to_g1");
   hipLaunchKernelGGL(k_hash_to_g1_beacons, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.m,
                      a.scheme == DGPU_SCHEME_G1_RFC9380 ? 1 : 0, h, (uint32_t*)c->h_z.p);
@@ -1025,10 +1035,14 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
   hipLaunchKernelGGL(k_g1_batch_affine, dim3(grid_for((n + 15) / 16, B)), dim3(B), 0, s, n, h,
                      (const uint32_t*)c->h_z.p, (uint32_t*)c->h_pre.p);
   HIP_TRY(hipGetLastError());
-  mark(c, s, "decode_g1");
-  hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
-                     sg, st);
-  HIP_TRY(hipGetLastError());
+  if (side) {
+    HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
+  } else {
+    mark(c, s, "decode_g1");
+    hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
+                       sg, st);
+    HIP_TRY(hipGetLastError());
+  }
   return eng_pairing_locked(c, (const uint32_t*)key->consts.p, n, h, sg, st, s, 0, nullptr, nullptr,
                             (const uint32_t*)key->table.p);
 }

@@ -438,7 +438,7 @@ def small_batch_leg(chain, scheme, sizes=SMALL_BATCH_SIZES, budget_s=20.0):
     try:
         from oracle import c_ref
         c_ref.load()
-        k = 8
+        k = min(8, len(chain))  # a chain of fewer records (--small-batch-sizes 1) times what it has
         sub = [np.ascontiguousarray(a[:k]) for a in (chain.rounds, chain.sigs, chain.sig_len, chain.prev,
                                                      chain.prev_len)]
         g1 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
@@ -931,7 +931,7 @@ def main():
         from drand_amd.synth import corrupt, make_chain
         code = _lib.load().dgpu_scheme_from_name(args.scheme.encode())
         sizes = tuple(int(x) for x in args.small_batch_sizes.split(",")) if args.small_batch_sizes else SMALL_BATCH_SIZES
-        ch = make_chain(args.seed, max(sizes), code, seg_len=args.seg_len)
+        ch = make_chain(args.seed, max(max(sizes), 8), code, seg_len=args.seg_len)  # >= 8 for the CPU sample
         corrupt(ch, args.seed, rate=args.corrupt_rate)
         print(json.dumps(small_batch_leg(ch, args.scheme, sizes=sizes)), flush=True)
         return

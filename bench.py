@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--leg-steps", type=int, default=2, help="timed steps of each extra leg")
     ap.add_argument("--no-ingest", action="store_true", help="skip the bolt-store check-chain ingest leg")
     ap.add_argument("--ingest-rounds", type=int, default=1_000_000)
+    ap.add_argument("--ingest-only", action="store_true",
+                    help="only the bolt-store ingest leg, once per window size in --ingest-windows")
+    ap.add_argument("--ingest-windows", default="262144", help="comma-separated CheckPastBeacons window sizes")
     ap.add_argument("--mode", choices=["per-round", "rlc", "recover"], default="per-round",
                     help="per-round: configs[1] / the metric; rlc: configs[2] (random linear combination + "
                          "bisection); recover: configs[4] (t-of-n threshold recovery, n=32, t=17)")
@@ -500,7 +503,7 @@ def _hex_rows(a, lens):
     return [bytes(hx[i, :2 * int(lens[i])]) for i in range(a.shape[0])]
 
 
-def ingest_leg(chain, n_rows, scheme, window=1 << 18):
+def ingest_leg(chain, n_rows, scheme, window=1 << 18, windows=None):
     """The bulk check-chain path end to end from a drand bolt store: n_rows
     rounds of the bench chain written (outside the timed region, with the
     test writer tests/bolt_writer.py) as Beacon.Marshal rows keyed by
@@ -537,6 +540,13 @@ def ingest_leg(chain, n_rows, scheme, window=1 << 18):
     v = Verifier(get_scheme_by_id_with_default(scheme))
     try:
         check_past_beacons(bs, v, chain.pk, 1 << 16, window=1 << 16)  # warm: key decode, buffers, page cache
+        sweep = {}
+        for w in windows or ():  # --ingest-only: the same file at other window sizes
+            check_past_beacons(bs, v, chain.pk, 10 ** 12, window=w)
+            t0 = time.perf_counter()
+            check_past_beacons(bs, v, chain.pk, 10 ** 12, window=w)
+            sweep[w] = n / (time.perf_counter() - t0)
+            log(f"ingest window {w}: {sweep[w]:.0f} rounds/s")
         t0 = time.perf_counter()
         faulty = check_past_beacons(bs, v, chain.pk, 10 ** 12, window=window)
         el = time.perf_counter() - t0
@@ -550,6 +560,8 @@ def ingest_leg(chain, n_rows, scheme, window=1 << 18):
                "decode_only_rounds_per_s": n / t_dec, "file_bytes": os.path.getsize(path),
                "write_s": t_write, "decode_threads": ingest.DECODE_THREADS,
                "api": "sync.check_past_beacons(BoltStore) -> native scan/decode -> dgpu_verify_beacons"}
+        if sweep:
+            res["window_sweep"] = {str(k): v for k, v in sweep.items()}
     finally:
         bs.close()
         os.remove(path)
@@ -934,6 +946,15 @@ def main():
         ch = make_chain(args.seed, max(max(sizes), 8), code, seg_len=args.seg_len)  # >= 8 for the CPU sample
         corrupt(ch, args.seed, rate=args.corrupt_rate)
         print(json.dumps(small_batch_leg(ch, args.scheme, sizes=sizes)), flush=True)
+        return
+    if args.ingest_only:
+        from drand_amd import _lib
+        from drand_amd.synth import corrupt, make_chain
+        code = _lib.load().dgpu_scheme_from_name(args.scheme.encode())
+        ch = make_chain(args.seed, args.ingest_rounds, code, seg_len=args.seg_len)
+        _EXPECT[id(ch)] = {i: False for i in corrupt(ch, args.seed, rate=args.corrupt_rate)}
+        ws = [int(x) for x in args.ingest_windows.split(",")]
+        print(json.dumps(ingest_leg(ch, args.ingest_rounds, args.scheme, window=ws[0], windows=ws)), flush=True)
         return
     if os.environ.get("DRAND_BENCH_DRYRUN"):
         return dryrun(args)

@@ -925,6 +925,60 @@ extern "C" int hs_eng_pairing(const uint8_t* pk48, const uint8_t* msg32, const u
   return one ? 1 : 0;
 }
 
+// One pass of the LINES program over the pairs (a, b) (k_eng_lines with
+// t_out): T of each pair after the loop, homogeneous (X, Y, Z) in the pair's
+// slots 0..5, as Jacobian (XZ, YZ^2, Z) -- pairing_engine.cuh cof_homog_to_jac.
+static void host_lines_T(const g2a& a, const g2a& b, g2j out[2]) {
+  static HostGroup G;
+  G = HostGroup();
+  g1a dummy{C_G1_X, C_G1_Y};
+  host_consts(G, dummy);
+  const g2a q[2] = {a, b};
+  for (int p = 0; p < 2; ++p) {
+    const fp v[4] = {q[p].x.c0, q[p].x.c1, q[p].y.c0, q[p].y.c1};
+    for (int comp = 0; comp < 4; ++comp) {
+      G.set(p * ENG_LINE_PAIR_SLOTS + comp, v[comp]);
+      G.set(p * ENG_LINE_PAIR_SLOTS + 6 + comp, v[comp]);
+    }
+    G.set(p * ENG_LINE_PAIR_SLOTS + 4, fp_one());
+    G.set(p * ENG_LINE_PAIR_SLOTS + 5, fp_zero());
+  }
+  G.set(ENG_L_NXP0, fp_neg(C_G1_X));
+  G.set(ENG_L_YP0, C_G1_Y);
+  G.step = 0;
+  host_exec(G, ENG_PROG_LINES, ENG_PROG_LINES_LEN);
+  for (int p = 0; p < 2; ++p) {
+    auto at = [&](int comp) { return G.get(p * ENG_LINE_PAIR_SLOTS + comp); };
+    const fp2 X{at(0), at(1)}, Y{at(2), at(3)}, Z{at(4), at(5)};
+    out[p] = g2j{fp2_mul(X, Z), fp2_mul(Y, fp2_sqr(Z)), Z};
+  }
+}
+
+// The small-call cofactor clearing (capi.hip g2_lane_hash_locked with
+// consts: k_cof_prep -> k_eng_lines -> k_cof_mid -> k_eng_lines beside
+// k_cof_partial -> k_cof_final) on the host emulation: H(msg) compressed, to
+// compare with hs_hash_to_g2 (k_h2c_finish's per-thread ladders).
+extern "C" void hs_eng_cof_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  fp2 u0, u1;
+  hash_to_field_g2(u0, u1, m);
+  const g2j P = g2_add(map_to_curve_sswu_iso3_body(u0), map_to_curve_sswu_iso3_body(u1));  // k_cof_prep
+  const g2a pa = g2_to_affine(P);
+  const g2j ps = g2_psi(g2_from_affine(pa));
+  g2j T[2], T2[2];
+  host_lines_T(pa, g2a{ps.x, ps.y}, T);  // T0 = [|x|]P, T1 = [|x|]psi(P)
+  const g2a t0a = g2_to_affine(T[0]);    // k_cof_mid
+  host_lines_T(t0a, t0a, T2);            // T2 = [x^2]P
+  g2j u = g2_add(T[0], g2_neg(P));       // k_cof_partial
+  u = g2_add(u, g2_neg(T[1]));
+  u = g2_add(u, g2_neg(g2_psi(P)));
+  u = g2_add(u, g2_psi2(g2_dbl(P)));
+  const g2j h = g2_add(T2[0], u);        // k_cof_final
+  const bool inf = g2_is_inf(h);
+  g2_compress(out96, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h), inf);
+}
+
 // engine.cuh eng_kb_dec_parts + eng_kb_dec_finish (the split used by
 // k_kb_chain_pre_thr / k_kb_dec_thr) == eng_kb_decompress on n random
 // inputs; returns the number of disagreements.

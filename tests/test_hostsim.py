@@ -396,3 +396,16 @@ def test_thread_kb_chain_matches_lane_chain(hostsim):
     finally:
         hostsim.hs_eng_set_kb_thread(0)
         hostsim.hs_eng_set_fe_kb(0)
+
+
+def test_engine_cofactor_ladder_matches_golden_hash(hostsim):
+    """The small-call cofactor clearing (two passes of the LINES program,
+    whose T after the loop is [|x|]Q, composed as k_cof_partial / k_cof_final
+    compose it) gives the golden H(m) -- the vectors k_h2c_finish's
+    per-thread ladders are pinned to (hash_to_g2.json, from the oracle
+    pinned by key/curve_test.go:10-30)."""
+    cases = load_golden("hash_to_g2.json")["cases"]
+    for c in cases:
+        o = buf(96)
+        hostsim.hs_eng_cof_hash_to_g2(bytes.fromhex(c["msg"]), o)
+        assert o.raw.hex() == c["h"]

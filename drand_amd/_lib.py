@@ -11,6 +11,13 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DRAND_GPU_LIB selects an alternative in-tree build (A/B experiments only)
 LIB_PATH = os.environ.get("DRAND_GPU_LIB") or os.path.join(_HERE, "libdrand_gpu.so")
+# The same sources built with -DDG_AB_KNOBS (__graft_entry__.build): the only
+# build that reads the A/B variant knobs and test hooks (AB_KNOBS) from the
+# environment.  Tests open it for those variants; the product never loads it.
+AB_LIB_PATH = os.path.join(_HERE, "libdrand_gpu_ab.so")
+AB_KNOBS = frozenset({"DGPU_DEC_OVERLAP", "DGPU_MSM_SEG", "DGPU_LANE_SLICES", "DGPU_KB_NORM", "DGPU_RLC_DESCENT_STEP",
+                      "DGPU_RLC_LOCALIZE", "DGPU_G1_LINES", "DGPU_SUBGROUP", "DGPU_RECOVER", "DGPU_RECOVER_ROWS",
+                      "DGPU_KB_INV_CHAIN", "DGPU_KB_TEST_FLAG", "DGPU_TEST_ALLOC_CAP"})
 
 DGPU_OK = 0
 DGPU_EINVAL = -1
@@ -73,6 +80,8 @@ SYMBOLS = [
     ("dgpu_hash_to_curve", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _c.c_size_t, _P, _P]),
     ("dgpu_sign", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _P, _c.c_size_t, _P, _P]),
     ("dgpu_decode_g1_points", _c.c_int, [_P, _c.c_size_t, _P, _P, _P]),
+    ("dgpu_decode_signatures", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _c.c_size_t, _P, _P, _P]),
+    ("dgpu_decode_pubkey", _c.c_int, [_P, _c.c_int, _P, _c.c_size_t, _P]),
     ("dgpu_multi_open", _c.c_int, [_c.c_int, _P, _c.POINTER(_P)]),
     ("dgpu_multi_close", None, [_P]),
     ("dgpu_multi_context", _c.c_int, [_P, _c.c_int, _c.POINTER(_P)]),
@@ -91,17 +100,17 @@ class DrandGPUError(RuntimeError):
         self.code = code
 
 
-_lib = None
+_libs = {}
 _lib_lock = threading.Lock()
 
 
 def load(path=None):
-    """Load libdrand_gpu.so and bind every declared symbol (raises if absent)."""
-    global _lib
+    """Load libdrand_gpu.so (or the build at `path`) once and bind every
+    declared symbol (raises if absent)."""
+    p = path or LIB_PATH
     with _lib_lock:
-        if _lib is not None and path is None:
-            return _lib
-        p = path or LIB_PATH
+        if p in _libs:
+            return _libs[p]
         if not os.path.exists(p):
             raise DrandGPUError(DGPU_EDEVICE, f"{p} not built (run __graft_entry__.build())")
         lib = ctypes.CDLL(p)
@@ -111,14 +120,15 @@ def load(path=None):
             fn.argtypes = args
         if lib.dgpu_abi_version() != ABI_VERSION:
             raise DrandGPUError(DGPU_EINVAL, "ABI version mismatch")
-        if path is None:
-            _lib = lib
+        _libs[p] = lib
         return lib
 
 
-def check(rc):
+def check(rc, lib=None):
+    """Raise DrandGPUError for a failed call; the message is the failing
+    library's thread-local dgpu_last_error (pass `lib` for a non-default build)."""
     if rc != DGPU_OK:
-        lib = load()
+        lib = lib or load()
         raise DrandGPUError(rc, lib.dgpu_last_error().decode(errors="replace"))
     return rc
 
@@ -162,16 +172,16 @@ def ptr(buf):
 class Context:
     """One GPU context (dgpu_ctx*).  Thread-safe: the library serializes."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, lib_path=None):
         # torch bundles its own HIP runtime under the system one's SONAME: a
         # process that uses both must let torch initialise HIP first, or torch
         # later finds no GPU (INTEGRATION.md, Python callers)
         torch = sys.modules.get("torch")
         if torch is not None and torch.cuda.is_available():
             torch.cuda.init()
-        self.lib = load()
+        self.lib = load(lib_path)
         h = ctypes.c_void_p()
-        check(self.lib.dgpu_open(device, ctypes.byref(h)))
+        check(self.lib.dgpu_open(device, ctypes.byref(h)), self.lib)
         self.handle = h
         self.device = device
 

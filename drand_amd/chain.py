@@ -276,6 +276,54 @@ def decode_g1_points(points, device=0):
     return rc.tolist(), coords
 
 
+def _be_coords(xy, k):
+    return tuple(int.from_bytes(bytes(xy[48 * j:48 * j + 48]), "big") for j in range(k))
+
+
+def decode_signatures(scheme, sigs, device=0):
+    """The scheme's signature decoder (the UnmarshalBinary inside bls.Verify,
+    chain/verify.go:44): returns (reasons, points) with points[i] = (x, y)
+    ints on G1 or ((x0, x1), (y0, y1)) on G2 for decoded records, else None."""
+    ctx = get_context(device)
+    code = scheme_code(scheme)
+    n = len(sigs)
+    g1 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
+    stride = max([96] + [len(s) for s in sigs])
+    buf = np.zeros((max(n, 1), stride), dtype=np.uint8)
+    ln = np.zeros(max(n, 1), dtype=np.uint32)
+    for i, s in enumerate(sigs):
+        buf[i, :len(s)] = np.frombuffer(bytes(s), dtype=np.uint8)
+        ln[i] = len(s)
+    w = 96 if g1 else 192
+    reason = np.zeros(max(n, 1), dtype=np.uint8)
+    xy = np.zeros(max(n, 1) * w, dtype=np.uint8)
+    if n:
+        _lib.check(ctx.lib.dgpu_decode_signatures(ctx.handle, code, n, _lib.ptr(buf), stride, _lib.ptr(ln),
+                                                  _lib.ptr(reason), _lib.ptr(xy)))
+    pts = []
+    for i in range(n):
+        if reason[i] != _lib.REASON_OK:
+            pts.append(None)
+            continue
+        c = _be_coords(xy[i * w:(i + 1) * w], w // 48)
+        pts.append(c if g1 else ((c[0], c[1]), (c[2], c[3])))
+    return reason[:n].tolist(), pts
+
+
+def decode_pubkey(scheme, pk, device=0):
+    """The scheme's public-key decoder (chain/convert.go:20-23): the affine key
+    point ((x, y) on G1, ((x0, x1), (y0, y1)) on G2); raises DrandGPUError
+    (DGPU_EINVAL) when the key is rejected."""
+    ctx = get_context(device)
+    code = scheme_code(scheme)
+    b = np.frombuffer(bytes(pk), dtype=np.uint8).copy()
+    g2 = code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
+    xy = np.zeros(192, dtype=np.uint8)
+    _lib.check(ctx.lib.dgpu_decode_pubkey(ctx.handle, code, _lib.ptr(b), len(pk), _lib.ptr(xy)))
+    c = _be_coords(xy, 4 if g2 else 2)
+    return ((c[0], c[1]), (c[2], c[3])) if g2 else c
+
+
 def hash_to_g2(msgs, device=0):
     """kyber G2 Hash (R) of 32-byte messages -> 96-byte compressed points (parity surface)."""
     ctx = get_context(device)

@@ -51,11 +51,20 @@ int set_err(int code, const char* fmt, ...) {
 // Grow-only device scratch buffer.  Growth frees the old allocation only
 // after the device is idle: a kernel enqueued earlier (this call or an
 // earlier asynchronous one) may still read it.
+#ifdef DG_AB_KNOBS
+// test hook of the A/B build (DGPU_TEST_ALLOC_CAP=<bytes>): larger requests
+// fail as an out-of-memory hipMalloc would (the engine chunk's retry path)
+size_t g_test_alloc_cap = 0;
+#endif
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
   int ensure(size_t bytes) {
     if (bytes <= cap) return DGPU_OK;
+#ifdef DG_AB_KNOBS
+    if (g_test_alloc_cap && bytes > g_test_alloc_cap)
+      return set_err(DGPU_ENOMEM, "hipMalloc(%zu): test cap %zu", bytes, g_test_alloc_cap);
+#endif
     if (p) {
       hipDeviceSynchronize();
       hipFree(p);
@@ -199,8 +208,8 @@ struct dgpu_ctx {
   int lanes = 2;                 // DGPU_LANES=1: one stream (A/B)
   size_t lane_slices = 2;        // DGPU_LANE_SLICES: slices of a two-lane batch, alternating between the lanes
   size_t eng_chunk = ENG_CHUNK;  // DGPU_ENG_CHUNK=<rounds> or sized from free HBM
+  size_t chunk_retries = 0;      // engine-chunk halvings after an out-of-memory allocation (eng_pairing_locked)
   bool kb_thread = true;         // DGPU_KB_CHAIN=lanes: the 8-lane compressed chain (k_eng_kb_chain, A/B)
-  bool kb_split = false;         // DGPU_KB_DEC=split: norms + decompression parts at the chain's snaps, per-thread inversion (A/B)
   bool kb_norm_chain = true;     // the per-thread chain writes the six norms (r05c/r05d: kbinv -17%, FE -1.5%
                                  // same-box); DGPU_KB_NORM=planes: k_eng_kb_norm reads f1 from the planes (A/B;
                                  // the row-staged, image and round-fastest decompression variants measured in
@@ -232,10 +241,6 @@ struct dgpu_ctx {
   bool msm_seg = true;           // load-balanced bucket sums (k_msm_bucket_seg); DGPU_MSM_SEG=0: one thread per bucket (A/B)
   int n_cu = 256;                // compute units (the load-balanced sums launch one wave per SIMD slot)
   bool recover_rows = true;      // the MSM gathers its window tables as rows (DGPU_RECOVER_ROWS=0: SoA planes, A/B)
-  // DGPU_ENG_FUSED_PROBE=1 (A/B probe only): dynamic LDS padding that puts
-  // k_eng_lines and k_eng_miller at the occupancy a fused lines+Miller kernel
-  // would have (74 slots per group: 22,064 B per block, 7 blocks per CU)
-  unsigned lds_pad_lines = 0, lds_pad_miller = 0;
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call (event pool;
@@ -266,6 +271,22 @@ struct stream_order {
   hipStream_t s;
   stream_order(dgpu_ctx* c_, hipStream_t s_) : c(c_), s(s_) { hipStreamWaitEvent(s, c->done, 0); }
   ~stream_order() { hipEventRecord(c->done, s); }
+};
+
+// A fork to a side stream (the decode beside the hash, the cofactor's U):
+// however the function returns, the main stream ends up waiting for all the
+// side stream's work, so the call's `done` event (recorded on the main
+// stream) covers it (an early return after the fork left a
+// decode running unjoined).  release() once the function has joined itself.
+struct side_join {
+  hipStream_t side, main;
+  hipEvent_t ev;
+  bool armed;
+  side_join(hipStream_t side_, hipStream_t main_, hipEvent_t ev_) : side(side_), main(main_), ev(ev_), armed(side_ != nullptr) {}
+  void release() { armed = false; }
+  ~side_join() {
+    if (armed && hipEventRecord(ev, side) == hipSuccess) (void)hipStreamWaitEvent(main, ev, 0);
+  }
 };
 
 // The stream a *_device entry point enqueues on: the caller's, and NULL is
@@ -850,10 +871,10 @@ int rlc_resolve_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, 
 // 2b): segment 0 (easy part), then per exponentiation by |x| the compressed
 // chain, its six stored values' norms, the batched inversion of their
 // products (divsteps, fp.cuh fp_inv), the decompression, and the next 12-lane
-// segment (DGPU_KB_DEC=split: norms and decompression parts formed at the
-// chain's snaps, k_kb_chain_pre_thr, then one thread per round inverting and
-// decompressing, k_kb_dec_thr -- measured slower); last, the Granger-Scott
-// kernel for the listed blocks with a flagged item.  capb: the chunk capacity
+// segment (the split at the inversion -- parts formed at the chain's snaps,
+// one thread per round inverting and decompressing -- measured slower, r04j,
+// and removed in round 6); last, the Granger-Scott kernel for the listed
+// blocks with a flagged item.  capb: the chunk capacity
 // rounded up to whole blocks of 5 rounds (>= cnt); kb: ENG_KB_BYTES_PER_ROUND
 // x capb bytes.
 int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t capb, size_t r0, uint32_t* f,
@@ -873,38 +894,27 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
     if (seg > 0) {
       mark(c, s, "eng_fe_chain");
       const bool kb_thread = c->kb_thread && cnt >= c->thr_min;
-      if (kb_thread && c->kb_split) {
-        // chain with the norms (to ebuf's planes) and decompression parts
-        // formed at the snaps; then per thread one inversion + decompression
-        hipLaunchKernelGGL(k_kb_chain_pre_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
-        HIP_TRY(hipGetLastError());
-        mark(c, s, "eng_fe_kbinv");
-        hipLaunchKernelGGL(k_kb_dec_thr, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0, xbuf,
-                           (const uint32_t*)ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
-        HIP_TRY(hipGetLastError());
-      } else {
-        const bool norm_pre = kb_thread && c->kb_norm_chain;
-        if (norm_pre)
-          hipLaunchKernelGGL(k_kb_chain_thr<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
-        else if (kb_thread)
-          hipLaunchKernelGGL(k_kb_chain_thr<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, nullptr);
-        else
-          hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
-        HIP_TRY(hipGetLastError());
-        mark(c, s, "eng_fe_kbinv");
-        if (norm_pre)
-          hipLaunchKernelGGL(k_eng_kb_norm<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
-                             (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
-        else
-          hipLaunchKernelGGL(k_eng_kb_norm<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
-                             (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
-                             (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
-        HIP_TRY(hipGetLastError());
-      }
+      const bool norm_pre = kb_thread && c->kb_norm_chain;
+      if (norm_pre)
+        hipLaunchKernelGGL(k_kb_chain_thr<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
+      else if (kb_thread)
+        hipLaunchKernelGGL(k_kb_chain_thr<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, nullptr);
+      else
+        hipLaunchKernelGGL(k_eng_kb_chain, dim3(grid_for(cnt, 8)), dim3(64), 0, s, cnt, xbuf);
+      HIP_TRY(hipGetLastError());
+      mark(c, s, "eng_fe_kbinv");
+      if (norm_pre)
+        hipLaunchKernelGGL(k_eng_kb_norm<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
+                           (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+      else
+        hipLaunchKernelGGL(k_eng_kb_norm<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, r0,
+                           (const uint32_t*)xbuf, pbuf, ebuf, flags, (const uint8_t*)st, c->kb_test_flag);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_eng_inv, dim3(grid_for(inv_threads, 256)), dim3(256), 0, s, cnt, r0, pbuf, pre, st);
+      HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(k_eng_kb_dec, dim3(grid_for((size_t)ENG_KB_NSNAP * cnt, 256)), dim3(256), 0, s, cnt, xbuf,
+                         (const uint32_t*)pbuf, (const uint32_t*)ebuf, (const uint8_t*)flags);
+      HIP_TRY(hipGetLastError());
     }
     mark(c, s, "eng_fe");
     hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
@@ -935,6 +945,7 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
   const bool fe_gs = c->fe_gs || n <= c->fe_gs_max;
   int rc;
   size_t cap = 0, cap_blk = 0;
+  bool retried = false;
   for (;;) {
     // equal chunks of at most eng_chunk items (whole 5-item blocks): no short tail launch
     const size_t nchunks = (n + c->eng_chunk - 1) / c->eng_chunk;
@@ -948,12 +959,19 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
     if (!rc) rc = b_n1->ensure(cap * FP_LIMBS * 4);
     if (rc != DGPU_ENOMEM || c->eng_chunk <= ENG_CHUNK_MIN || cap <= ENG_CHUNK_MIN) break;
     // HBM is shared (other contexts, torch): the chunk was sized from the free
-    // memory at dgpu_open; halve it for this context and retry
-    hipDeviceSynchronize();
+    // memory at dgpu_open; halve it for this context and retry.
+    // The buffers may still be read by this context's earlier work (its two
+    // streams and the call's stream); nothing else has to wait.
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream2));
     for (DevBuf* b : {b_kb, b_lines, b_f, b_n1}) b->release();
     c->eng_chunk = std::max(ENG_CHUNK_MIN, c->eng_chunk / 2);
+    ++c->chunk_retries;
+    retried = true;
   }
   if (rc) return rc;
+  if (retried) g_last_error.clear();  // the failed attempt's message is stale
   // k_eng_inv's prefix products reuse the line buffer (or f, on the fused path)
   uint32_t* lines = need_lines ? (uint32_t*)b_lines->p : nullptr;
   uint32_t* f = (uint32_t*)b_f->p;
@@ -982,12 +1000,12 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
           hipLaunchKernelGGL(k_lines_thr, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, n, r0, cnt, h, h_stride, h_idx,
                              sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
         else
-          hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, r0, cnt, h, h_stride, h_idx, sg,
+          hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
                            pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr, (uint32_t*)nullptr);
       }
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_miller");
-      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_miller, s, cnt, consts, lines, f, n1);
+      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
       HIP_TRY(hipGetLastError());
     }
     const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
@@ -1018,7 +1036,8 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
   uint32_t* h = (uint32_t*)c->h_pts.p;
   uint32_t* sg = (uint32_t*)c->sig_pts.p;
   // the signature decode beside the hash on the second stream (as the G2 path, g2_lane_hash_locked)
-  const bool side = c->dec_overlap && !c->profile;
+  const bool side = c->dec_overlap && c->lanes > 1 && !c->profile;
+  side_join join(side ? c->stream2 : nullptr, s, c->lane_ev[1]);
   if (side) {
     HIP_TRY(hipEventRecord(c->lane_ev[0], s));
     HIP_TRY(hipStreamWaitEvent(c->stream2, c->lane_ev[0], 0));
@@ -1037,6 +1056,7 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
   HIP_TRY(hipGetLastError());
   if (side) {
     HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));
+    join.release();
   } else {
     mark(c, s, "decode_g1");
     hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.sigs, a.sig_stride, a.sig_len, a.m,
@@ -1078,6 +1098,12 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
                          sg, st);
     return hipGetLastError();
   };
+  const bool cof_engine = consts && n <= c->cof_engine_max;
+  const unsigned cof_blocks = grid_for(n, ENG_ROUNDS_PER_BLOCK);
+  if (cof_engine && ((rc = c->cof_tmp.ensure((size_t)COF_PLANES * FP_WORDS * n * 4)) ||
+                     (rc = L.lines->ensure((size_t)cof_blocks * ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4))))
+    return rc;  // allocated before the fork: a failure here leaves nothing on the side stream
+  side_join join(s_dec, s, c->lane_ev[1]);
   if (s_dec) {  // first in the second stream's queue: it runs beside the whole hash chain
     HIP_TRY(hipEventRecord(c->lane_ev[0], s));
     HIP_TRY(hipStreamWaitEvent(s_dec, c->lane_ev[0], 0));
@@ -1089,11 +1115,8 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
   HIP_TRY(hipGetLastError());
-  if (consts && n <= c->cof_engine_max) {
-    const unsigned blocks = grid_for(n, ENG_ROUNDS_PER_BLOCK);
-    if ((rc = c->cof_tmp.ensure((size_t)COF_PLANES * FP_WORDS * n * 4)) ||
-        (rc = L.lines->ensure((size_t)blocks * ENG_LINE_STEPS * FP_LIMBS * ENG_WAVE_WORDS * 4)))
-      return rc;
+  if (cof_engine) {
+    const unsigned blocks = cof_blocks;
     uint32_t* w = (uint32_t*)c->cof_tmp.p;
     uint32_t* pa = w + (size_t)G2J_WORDS * n;
     uint32_t* psia = pa + (size_t)G2A_WORDS * n;
@@ -1103,7 +1126,7 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
     uint32_t* lines = (uint32_t*)L.lines->p;
     hipLaunchKernelGGL(k_cof_prep, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, w);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, (size_t)0, n,
+    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, (size_t)0, n,
                        (const uint32_t*)pa, n, (const uint32_t*)nullptr, (const uint32_t*)psia, (const uint32_t*)nullptr,
                        consts, lines, (uint8_t*)nullptr, t1);
     HIP_TRY(hipGetLastError());
@@ -1119,7 +1142,7 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
     hipLaunchKernelGGL(k_cof_partial, dim3(grid_for(n, B)), dim3(B), 0, su, n, w);
     HIP_TRY(hipGetLastError());
     if (side) HIP_TRY(hipEventRecord(c->cof_ev[1], su));
-    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), c->lds_pad_lines, s, n, (size_t)0, n,
+    hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, (size_t)0, n,
                        (const uint32_t*)t0a, n, (const uint32_t*)nullptr, (const uint32_t*)t0a, (const uint32_t*)nullptr,
                        consts, lines, (uint8_t*)nullptr, t2);
     HIP_TRY(hipGetLastError());
@@ -1136,6 +1159,7 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   HIP_TRY(hipGetLastError());
   if (s_dec) {
     HIP_TRY(hipStreamWaitEvent(s, c->lane_ev[1], 0));  // the decode (queued first on s_dec)
+    join.release();
   } else {
     mark(c, s, "decode_g2");
     HIP_TRY(decode(s));
@@ -1223,7 +1247,8 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   const size_t n0 = two ? ((n / slices + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
   // one lane: the decode overlaps the hash on the second stream (small calls:
   // the decode's ~0.9 ms leaves the critical path; DGPU_DEC_OVERLAP=0 off)
-  const hipStream_t s_dec = (!two && c->dec_overlap && !c->profile) ? c->stream2 : nullptr;
+  // (DGPU_LANES=1 keeps the whole call on one stream: no decode beside the hash either)
+  const hipStream_t s_dec = (!two && c->lanes > 1 && c->dec_overlap && !c->profile) ? c->stream2 : nullptr;
   if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec, consts))) return rc;
   const bool sub = !c->decode_subgroup;
   if (!two)
@@ -1377,56 +1402,58 @@ int dgpu_open(int device, dgpu_ctx** out) {
   dgpu_ctx* c = new dgpu_ctx();
   c->device = device;
   c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  // Shipped thresholds and the documented kernel-family switches
+  // (include/drand_gpu.h dgpu_open); nothing else is read from the
+  // environment by the shipped library.
   const char* fgv = getenv("DGPU_FE_GS_MAX");
   if (fgv && atol(fgv) >= 0) c->fe_gs_max = (size_t)atol(fgv);
   const char* cev = getenv("DGPU_COF_ENGINE_MAX");
   if (cev && atol(cev) >= 0) c->cof_engine_max = (size_t)atol(cev);
-  const char* dov = getenv("DGPU_DEC_OVERLAP");
-  if (dov && !strcmp(dov, "0")) c->dec_overlap = false;
-  const char* msv = getenv("DGPU_MSM_SEG");
-  if (msv && !strcmp(msv, "0")) c->msm_seg = false;
   const char* lv = getenv("DGPU_LANES");
   if (lv && !strcmp(lv, "1")) c->lanes = 1;
-  const char* lsv = getenv("DGPU_LANE_SLICES");
-  if (lsv && atol(lsv) >= 2 && atol(lsv) <= 64) c->lane_slices = (size_t)atol(lsv);
   const char* ec = getenv("DGPU_ENG_CHUNK");
   c->eng_chunk = (ec && atol(ec) >= 4096) ? (size_t)atol(ec) : size_engine_chunk(c->lanes);
   const char* kcv = getenv("DGPU_KB_CHAIN");
   if (kcv && !strcmp(kcv, "lanes")) c->kb_thread = false;
-  const char* kdv = getenv("DGPU_KB_DEC");
-  if (kdv && !strcmp(kdv, "split")) c->kb_split = true;
-  const char* knv = getenv("DGPU_KB_NORM");
-  if (knv) c->kb_norm_chain = strcmp(knv, "planes") != 0;
-  const char* rds = getenv("DGPU_RLC_DESCENT_STEP");
-  if (rds && atoi(rds) >= 1 && atoi(rds) <= 8) c->rlc_descent_step = atoi(rds);
-  const char* rlv = getenv("DGPU_RLC_LOCALIZE");
-  if (rlv && !strcmp(rlv, "0")) c->rlc_localize = false;
   const char* lnv = getenv("DGPU_LINES");
   if (lnv && !strcmp(lnv, "engine")) c->lines_thread = false;
   const char* tmv = getenv("DGPU_THR_MIN");
   if (tmv && atol(tmv) >= 0) c->thr_min = (size_t)atol(tmv);
   const char* rmv = getenv("DGPU_RLC_MIN");
   if (rmv && atol(rmv) >= 0) c->rlc_min = (size_t)atol(rmv);
+  const char* fev = getenv("DGPU_FE");
+  if (fev && !strcmp(fev, "gs")) c->fe_gs = true;
+#ifdef DG_AB_KNOBS
+  // Variants measured and not shipped, tuning knobs and test hooks: read only
+  // by the A/B build (drand_amd/libdrand_gpu_ab.so, __graft_entry__.build;
+  // tools/build_variant.sh), never by the shipped library.
+  const char* dov = getenv("DGPU_DEC_OVERLAP");
+  if (dov && !strcmp(dov, "0")) c->dec_overlap = false;
+  const char* msv = getenv("DGPU_MSM_SEG");
+  if (msv && !strcmp(msv, "0")) c->msm_seg = false;
+  const char* lsv = getenv("DGPU_LANE_SLICES");
+  if (lsv && atol(lsv) >= 2 && atol(lsv) <= 64) c->lane_slices = (size_t)atol(lsv);
+  const char* knv = getenv("DGPU_KB_NORM");
+  if (knv) c->kb_norm_chain = strcmp(knv, "planes") != 0;
+  const char* rds = getenv("DGPU_RLC_DESCENT_STEP");
+  if (rds && atoi(rds) >= 1 && atoi(rds) <= 8) c->rlc_descent_step = atoi(rds);
+  const char* rlv = getenv("DGPU_RLC_LOCALIZE");
+  if (rlv && !strcmp(rlv, "0")) c->rlc_localize = false;
   const char* gl = getenv("DGPU_G1_LINES");
   if (gl && !strcmp(gl, "buffer")) c->fused_fixed = false;
   const char* sgv = getenv("DGPU_SUBGROUP");
   if (sgv && !strcmp(sgv, "decode")) c->decode_subgroup = true;
-  const char* fpv = getenv("DGPU_ENG_FUSED_PROBE");
-  if (fpv && !strcmp(fpv, "1")) {
-    const unsigned fused = (ENG_NCONST + 5 * 74) * ENG_SLOT_WORDS * 4;
-    c->lds_pad_lines = fused - ENG_LDS_SLOTS_LINES * ENG_SLOT_WORDS * 4;
-    c->lds_pad_miller = fused - ENG_LDS_SLOTS_MILLER * ENG_SLOT_WORDS * 4;
-  }
   const char* rcv = getenv("DGPU_RECOVER");
   if (rcv && !strcmp(rcv, "exact")) c->recover_exact = true;
   const char* rrv = getenv("DGPU_RECOVER_ROWS");
-  if (rrv) c->recover_rows = !strcmp(rrv, "1");
-  const char* fev = getenv("DGPU_FE");
-  if (fev && !strcmp(fev, "gs")) c->fe_gs = true;
+  if (rrv && !strcmp(rrv, "0")) c->recover_rows = false;
   const char* kic = getenv("DGPU_KB_INV_CHAIN");
   if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
   const char* ktf = getenv("DGPU_KB_TEST_FLAG");
   if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
+  const char* tac = getenv("DGPU_TEST_ALLOC_CAP");
+  if (tac && atol(tac) >= 0) g_test_alloc_cap = (size_t)atol(tac);
+#endif
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->lane_ev[0], hipEventDisableTiming);
@@ -1833,6 +1860,90 @@ int dgpu_decode_g1_points(dgpu_ctx* c, size_t n, const uint8_t* in48, int* rc_ou
   HIP_TRY(hipMemcpyAsync(rc_out, d_rc, n * 4, hipMemcpyDeviceToHost, s));
   if (xy96) HIP_TRY(hipMemcpyAsync(xy96, d_xy, n * 96, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+int dgpu_decode_signatures(dgpu_ctx* c, int scheme, size_t n, const uint8_t* sigs, size_t sig_stride,
+                           const uint32_t* sig_len, uint8_t* reason, uint8_t* xy) {
+  if (!c) return set_err(DGPU_EINVAL, "null ctx");
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  if (n == 0) return DGPU_OK;
+  if (!sig_len || !reason || (!sigs && sig_stride)) return set_err(DGPU_EINVAL, "null argument");
+  const bool g1 = sig_on_g1(scheme);
+  const size_t want = g1 ? 48 : 96;
+  for (size_t i = 0; i < n; ++i)
+    if (sig_len[i] == want && sig_stride < want) return set_err(DGPU_EINVAL, "sig_stride %zu < %zu", sig_stride, want);
+  const int nfp = g1 ? 2 : 4;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  c->rlc_pending = false;
+  hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  int rc;
+  if ((rc = c->in_sigs.ensure(n * sig_stride + 1)) || (rc = c->in_sig_len.ensure(n * 4)) ||
+      (rc = c->sig_pts.ensure(n * nfp * FP_WORDS * 4)) || (rc = c->status.ensure(n)) ||
+      (rc = c->misc.ensure(n * nfp * 48)))
+    return rc;
+  if (sig_stride) HIP_TRY(hipMemcpyAsync(c->in_sigs.p, sigs, n * sig_stride, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(c->in_sig_len.p, sig_len, n * 4, hipMemcpyHostToDevice, s));
+  const msg_src m = beacon_src(nullptr, nullptr, 0, nullptr, false);  // no message part: never a bad record
+  const uint8_t* d_sigs = (const uint8_t*)c->in_sigs.p;
+  const uint32_t* d_len = (const uint32_t*)c->in_sig_len.p;
+  uint32_t* pts = (uint32_t*)c->sig_pts.p;
+  uint8_t* st = (uint8_t*)c->status.p;
+  if (g1)
+    hipLaunchKernelGGL(k_decode_g1_sigs, dim3(grid_for(n, 256)), dim3(256), 0, s, n, d_sigs, sig_stride, d_len, m, pts,
+                       st);
+  else
+    hipLaunchKernelGGL(k_decode_g2_sigs_sub, dim3(grid_for(n, 256)), dim3(256), 0, s, n, d_sigs, sig_stride, d_len, m,
+                       pts, st);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(reason, st, n, hipMemcpyDeviceToHost, s));
+  if (xy) {
+    hipLaunchKernelGGL(k_fp_soa_to_be48, dim3(grid_for(n * nfp, 256)), dim3(256), 0, s, n, nfp, (const uint32_t*)pts, 0,
+                       (uint8_t*)c->misc.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(xy, c->misc.p, n * nfp * 48, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+int dgpu_decode_pubkey(dgpu_ctx* c, int scheme, const uint8_t* pk, size_t len, uint8_t* xy) {
+  if (!c || !pk) return set_err(DGPU_EINVAL, "null argument");
+  if (!scheme_known(scheme)) return set_err(DGPU_EINVAL, "bad scheme %d", scheme);
+  const bool g2key = sig_on_g1(scheme);
+  const size_t want = g2key ? 96 : 48;
+  if (len != want)
+    return set_err(DGPU_EINVAL, "public key must be %zu bytes (compressed %s), got %zu", want, g2key ? "G2" : "G1", len);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  int rc;
+  if ((rc = c->misc.ensure(4096))) return rc;
+  uint8_t* aux = (uint8_t*)c->misc.p;
+  uint8_t* d_in = aux;                      // 96 B
+  uint32_t* d_pt = (uint32_t*)(aux + 128);  // stride-1 affine point (<= 224 B)
+  int* d_rc = (int*)(aux + 512);
+  uint8_t* d_xy = aux + 1024;               // <= 192 B
+  HIP_TRY(hipMemcpyAsync(d_in, pk, want, hipMemcpyHostToDevice, s));
+  if (g2key)
+    hipLaunchKernelGGL(k_decode_g2_pk, dim3(1), dim3(64), 0, s, (const uint8_t*)d_in, d_pt, d_rc);
+  else
+    hipLaunchKernelGGL(k_decode_g1_pk, dim3(1), dim3(64), 0, s, (const uint8_t*)d_in, d_pt, d_rc);
+  HIP_TRY(hipGetLastError());
+  const int nfp = g2key ? 4 : 2;
+  hipLaunchKernelGGL(k_fp_soa_to_be48, dim3(1), dim3(64), 0, s, (size_t)1, nfp, (const uint32_t*)d_pt, g2key ? 0 : 1,
+                     d_xy);
+  HIP_TRY(hipGetLastError());
+  int drc = -1;
+  uint8_t host[192];
+  HIP_TRY(hipMemcpyAsync(&drc, d_rc, sizeof drc, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(host, d_xy, (size_t)nfp * 48, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (drc != DEC_OK) return set_err(DGPU_EINVAL, "public key rejected (decode code %d)", drc);
+  if (xy) memcpy(xy, host, (size_t)nfp * 48);
   return DGPU_OK;
 }
 

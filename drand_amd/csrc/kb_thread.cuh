@@ -118,81 +118,5 @@ __global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt,
                });
 }
 
-// Exponentiation side in two per-thread kernels (DGPU_KB_DEC=split, A/B; the
-// default is k_kb_chain_thr -> k_eng_kb_norm -> k_eng_inv -> k_eng_kb_dec).
-// Measured same-box at 2M rounds (profiles/r04/r04j_kb_split_ab.txt): the
-// snaps' extra work costs the chain 16.7 ms, the per-thread decompression
-// saves 14.7: 1.1% slower in rounds/s.
-//
-// k_kb_chain_pre_thr: the chain of k_kb_chain_thr, and at each snap, from the
-// registers, Norm(4 f1) -> nbuf ([j][limb][cnt]) and the decompression parts
-// n, v (engine.cuh eng_kb_dec_parts) into the value's f0 and f3 slots.
-#ifndef DG_KB_PRE_OCC
-#define DG_KB_PRE_OCC 2
-#endif
-__global__ void __launch_bounds__(256, DG_KB_PRE_OCC) k_kb_chain_pre_thr(size_t cnt, uint32_t* __restrict__ xbuf,
-                                                                        uint32_t* __restrict__ nbuf) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cnt) return;
-  kb_chain_thr(kb_ld_thr(xbuf, i, ENG_KB_PL_M, 2), kb_ld_thr(xbuf, i, ENG_KB_PL_M, 4),
-               kb_ld_thr(xbuf, i, ENG_KB_PL_M, 8), kb_ld_thr(xbuf, i, ENG_KB_PL_M, 10),
-               [&](int j, const fp2& f1, const fp2& f2, const fp2& f4, const fp2& f5) {
-                 const int pl = ENG_KB_PL_X0 + j;
-                 kb_st_thr(xbuf, i, pl, 2, f1);
-                 kb_st_thr(xbuf, i, pl, 4, f2);
-                 kb_st_thr(xbuf, i, pl, 8, f4);
-                 kb_st_thr(xbuf, i, pl, 10, f5);
-                 st_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i, eng_kb_norm(f1));
-                 fp2 n, v;
-                 eng_kb_dec_parts(f1, f2, f4, f5, n, v);
-                 kb_st_thr(xbuf, i, pl, 0, n);
-                 kb_st_thr(xbuf, i, pl, 6, v);
-               });
-}
-
-// k_kb_dec_thr: one thread per round, the six norms' product P inverted in
-// the thread by divsteps (fp.cuh fp_inv; no batch across threads), then
-// backwards 1 / N_j = P^-1 prefix_(j-1) prod_(k>j) N_k and f3, f0 from f1
-// and the stored parts (eng_kb_dec_finish).  A zero norm (f1 = 0) flags the
-// item for the Granger-Scott fallback unless it has already failed
-// (k_eng_kb_norm's rule); flagged items are not decompressed.  flag_every:
-// DGPU_KB_TEST_FLAG.
-#ifndef DG_KB_DECT_OCC
-#define DG_KB_DECT_OCC 2
-#endif
-__global__ void __launch_bounds__(256, DG_KB_DECT_OCC) k_kb_dec_thr(size_t cnt, size_t r0, uint32_t* __restrict__ xbuf,
-                                                   const uint32_t* __restrict__ nbuf, uint8_t* __restrict__ flags,
-                                                   const uint8_t* __restrict__ status, size_t flag_every) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= cnt) return;
-  auto norm = [&](int j) { return ld_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i); };
-  bool zero = flag_every && i % flag_every == 0;
-  fp pre[ENG_KB_NSNAP - 1];  // prefix products N_0 .. N_j
-  fp acc;
-#pragma unroll
-  for (int j = 0; j < ENG_KB_NSNAP; ++j) {
-    const fp nj = norm(j);
-    zero = zero || fp_is_zero(nj);
-    acc = j ? fp_mul(acc, nj) : nj;
-    if (j < ENG_KB_NSNAP - 1) pre[j] = acc;
-  }
-  if (zero) {
-    if (status[r0 + i] == ST_OK) flags[i] = 1;
-    return;
-  }
-  if (flags[i]) return;  // flagged at an earlier exponentiation: the fallback recomputes it
-  fp pinv = fp_inv(acc);  // every N_j nonzero here; after value j: 1 / (N_0 ... N_(j-1))
-#pragma unroll
-  for (int j = ENG_KB_NSNAP - 1; j >= 0; --j) {
-    const int pl = ENG_KB_PL_X0 + j;
-    const fp ninv = j ? fp_mul(pinv, pre[j - 1]) : pinv;
-    if (j) pinv = fp_mul(pinv, norm(j));
-    fp2 f0, f3;
-    eng_kb_dec_finish(kb_ld_thr(xbuf, i, pl, 2), kb_ld_thr(xbuf, i, pl, 0), kb_ld_thr(xbuf, i, pl, 6), ninv, f0, f3);
-    kb_st_thr(xbuf, i, pl, 0, f0);
-    kb_st_thr(xbuf, i, pl, 6, f3);
-  }
-}
-
 }  // namespace dgpu
 #endif

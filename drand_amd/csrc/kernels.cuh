@@ -409,4 +409,19 @@ __global__ void k_decode_g1_pk(const uint8_t* __restrict__ in48, uint32_t* __res
   *rc = r;
 }
 
+// Decoded points (SoA, nfp Fp coordinates of stride n, Montgomery) -> canonical
+// big-endian 48-byte coordinates, item-major: out + (i nfp + j) 48.  neg_first:
+// coordinate 0 is stored negated (k_decode_g1_pk's (-x, y)).  The decode
+// entry points' readout (dgpu_decode_signatures / dgpu_decode_pubkey).
+__global__ void __launch_bounds__(256) k_fp_soa_to_be48(size_t n, int nfp, const uint32_t* __restrict__ pts,
+                                                        int neg_first, uint8_t* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * (size_t)nfp) return;
+  const size_t i = t / (size_t)nfp;
+  const int j = (int)(t - i * (size_t)nfp);
+  fp v = ld_fp(pts + (size_t)j * FP_WORDS * n, n, i);
+  if (neg_first && j == 0) v = fp_neg(v);
+  fp_std_to_be48(fp_from_mont(v), out + t * 48);
+}
+
 }  // namespace dgpu

@@ -62,11 +62,12 @@ class Chain:
                       bytes(self.sigs[i, : self.sig_len[i]]))
 
 
-def make_chain(seed, n, scheme_code=_lib.SCHEME_CHAINED, seg_len=64, device=0, start_round=1):
-    """n rounds starting at `start_round`, in segments of `seg_len` rounds."""
+def make_chain(seed, n, scheme_code=_lib.SCHEME_CHAINED, seg_len=64, device=0, start_round=1, sk=None):
+    """n rounds starting at `start_round`, in segments of `seg_len` rounds;
+    signed with derive_secret(seed), or with the secret `sk` when given."""
     ctx = get_context(device)
     lib = ctx.lib
-    sk = derive_secret(seed).to_bytes(32, "big")
+    sk = (derive_secret(seed) if sk is None else sk).to_bytes(32, "big")
     on_g1 = scheme_code in (_lib.SCHEME_UNCHAINED_G1, _lib.SCHEME_G1_RFC9380)
     pk = np.zeros(96 if on_g1 else 48, dtype=np.uint8)
     skb = np.frombuffer(sk, dtype=np.uint8).copy()

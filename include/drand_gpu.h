@@ -99,22 +99,26 @@ const char *dgpu_last_error(void);
 
 /* Open device `device` (HIP ordinal).  Replaces nothing in the reference: the
  * Go side would hold one context per GPU inside crypto/gpu.BatchVerifier.
- * Read once here: DGPU_LANES=1 keeps large per-round G2 batches on one stream
- * (default: two streams over the batch halves; verdicts are identical), and
- * DGPU_G1_LINES=buffer runs the on-G1 fixed-Q lines through a line buffer
- * (default: formed inside the Miller kernel; verdicts are identical);
- * DGPU_LINES=engine and DGPU_KB_CHAIN=lanes run the Miller loops' T-steps and
- * the final exponentiation's compressed chains on the 12- / 8-lane engine
- * instead of one thread per item (default; verdicts are identical);
- * DGPU_THR_MIN=<items> (default 65536): pairing batches (per-round chunks
- * and RLC node checks) on fewer items take those engine kernels, which fill
- * the chip and cut the per-item latency at small sizes;
- * DGPU_RLC_MIN=<rounds> (default 131072): DGPU_MODE_RLC batches of fewer
- * rounds run the per-round path instead (identical verdicts and reasons;
- * below that size the combination's fixed costs make it the slower one);
- * DGPU_KB_DEC=split forms the Karabina decompression parts inside the chain
- * (A/B, measured slower); DGPU_FE=gs runs the Granger-Scott final
- * exponentiation (A/B). */
+ * The environment is read once here, and only these shipped thresholds and
+ * kernel-family switches (verdicts are identical under every setting):
+ *   DGPU_THR_MIN=<items> (default 65536): pairing batches (per-round chunks
+ *     and RLC node checks) on fewer items take the 12- / 8-lane engine
+ *     kernels, which fill the chip and cut the per-item latency at small sizes;
+ *   DGPU_RLC_MIN=<rounds> (default 131072): DGPU_MODE_RLC batches of fewer
+ *     rounds run the per-round path (below that size the combination's fixed
+ *     costs make it the slower one);
+ *   DGPU_COF_ENGINE_MAX=<rounds>, DGPU_FE_GS_MAX=<items> (default 16384
+ *     each): the small-call latency path (hash cofactor on the engine ladder,
+ *     Granger-Scott final exponentiation); 0 turns it off;
+ *   DGPU_ENG_CHUNK=<rounds>: engine chunk size (default: 1Mi, or what half
+ *     the free HBM holds);
+ *   DGPU_LANES=1: the whole call on one stream (default: two streams over
+ *     the halves of a large per-round G2 batch, the decode beside the hash);
+ *   DGPU_LINES=engine, DGPU_KB_CHAIN=lanes: the Miller loops' T-steps / the
+ *     final exponentiation's compressed chains on the 12- / 8-lane engine at
+ *     every size; DGPU_FE=gs: the Granger-Scott final exponentiation.
+ * Variants measured and not shipped, and test hooks, are read only by the
+ * A/B build of the same sources (-DDG_AB_KNOBS, drand_amd/libdrand_gpu_ab.so). */
 int dgpu_open(int device, dgpu_ctx **out);
 void dgpu_close(dgpu_ctx *ctx);
 
@@ -267,6 +271,26 @@ int dgpu_sign(dgpu_ctx *ctx, int scheme, const uint8_t *sk_be32, size_t n, const
  * point at infinity, other values an error (flags, x >= p, not on the curve,
  * not in the subgroup); xy96 (optional) = canonical big-endian x || y. */
 int dgpu_decode_g1_points(dgpu_ctx *ctx, size_t n, const uint8_t *in48, int *rc_out, uint8_t *xy96);
+
+/* The scheme's signature decoder alone (Beacon.Signature -> SigGroup point:
+ * the UnmarshalBinary inside bls.Verify (R), chain/verify.go:44): n records
+ * as in dgpu_verify_beacons (sig_len[i] bytes at sigs + i*sig_stride; any
+ * length other than 48 -- G1-signature schemes -- or 96 is a decode error),
+ * decoded with the subgroup check by the same kernels the verify paths run
+ * (k_decode_g1_sigs; k_decode_g2_sigs_sub).  reason: n bytes of
+ * DGPU_REASON_DECODE / _SUBGROUP / _INFINITY or 0; xy (optional): canonical
+ * big-endian affine coordinates, 96 bytes per record on G1 (x || y) and 192
+ * on G2 (x.c0 || x.c1 || y.c0 || y.c1), zero unless the record decoded. */
+int dgpu_decode_signatures(dgpu_ctx *ctx, int scheme, size_t n, const uint8_t *sigs, size_t sig_stride,
+                           const uint32_t *sig_len, uint8_t *reason, uint8_t *xy);
+
+/* The scheme's public-key decoder (chain.Info.PublicKey, chain/convert.go:20-23;
+ * the decode dgpu_set_pubkey / dgpu_verify_beacons run on a key-cache miss):
+ * 48-byte compressed G1 for the G2-signature schemes, 96-byte compressed G2
+ * for the G1-signature schemes, subgroup-checked.  DGPU_EINVAL if rejected;
+ * xy (optional): the affine point as dgpu_decode_signatures writes it (96
+ * bytes for a G1 key, 192 for a G2 key).  The key cache is not touched. */
+int dgpu_decode_pubkey(dgpu_ctx *ctx, int scheme, const uint8_t *pk, size_t len, uint8_t *xy);
 
 /* Hash-to-G2 of n 32-byte messages with drand's DST (kyber G2 Hash (R)),
  * compressed to 96 bytes each: the parity surface for hash-to-curve. */

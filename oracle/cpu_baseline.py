@@ -46,11 +46,20 @@ def _quota_and_projection(out, run_k, seconds, rate_hint):
     the reference's verifier with GOMAXPROCS = the host core count."""
     out["projected_all_host_cores_value"] = out["single_core_value"] * out["host_cores"]
     qt = quota_threads(out)
-    if qt >= out["cores"]:
+    if qt >= out["threads"]:
         return
     k = int(max(qt, seconds / 2 * rate_hint))
     _, wall, cpu_s = _timed(lambda: run_k(k))
     out["quota_threads"] = {"threads": qt, "value": k / wall, "wall_s": wall, "effective_parallelism": cpu_s / wall}
+
+
+def _label_cores(out, threads):
+    """`cores` is the parallelism the run measurably got (CPU seconds / wall:
+    ~15.9 under the GPU box's 16-core cgroup quota, whatever the thread
+    count); the threads started and the host / affinity / quota views are
+    kept beside it."""
+    out["threads"] = threads
+    out["cores"] = round(out["effective_parallelism"], 2)
 
 
 def _timed(fn):
@@ -107,6 +116,7 @@ def run(chain, seconds, cores, expect_valid=None):
            "cpu_s": cpu_s, "effective_parallelism": cpu_s / wall,
            "single_core_ms_per_round": per * 1e3, "single_core_value": 1.0 / per}
     out.update(host_cores())
+    _label_cores(out, cores)
     _quota_and_projection(out, lambda k: verify(sub_of(pick(k)), quota_threads(out)), seconds, sample / wall)
     if expect_valid is not None:
         out["sample_verdict_mismatches"] = int(((reason == 0) != expect_valid[idx]).sum())
@@ -208,6 +218,7 @@ def run_recover(commits, t, n, msgs, parts, expect_sigs, seconds, cores):
                "effective_parallelism": cpu_s / wall, "single_core_ms_per_round": w1 * 1e3,
                "single_core_value": 1.0 / w1, "sample_mismatches": mism}
         out.update(host_cores())
+        _label_cores(out, cores)
         _quota_and_projection(out, lambda k: run_idx(pick(k), quota_threads(out)), seconds, sample / wall)
         return out
     except (OSError, AttributeError):

@@ -66,6 +66,25 @@ def _torch_before_library(request):
     yield
 
 
+def open_ctx(env, device=0):
+    """A fresh library context opened under the environment `env` (the
+    library reads its knobs at dgpu_open).  Knobs of variants not shipped and
+    test hooks (_lib.AB_KNOBS) are read only by the A/B build
+    (drand_amd/libdrand_gpu_ab.so), so such an env opens that build."""
+    from drand_amd import _lib
+    ab = any(k in _lib.AB_KNOBS for k in env)
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return _lib.Context(device, lib_path=_lib.AB_LIB_PATH if ab else None)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     from drand_amd.chain import get_context

@@ -152,6 +152,65 @@ def group_keys():
     dump("group_toml_keys.json", {"source": "deploy/latest/group.toml", "keys": out})
 
 
+def _decode_entry(data, g2):
+    """Oracle decode of a compressed point (kilic FromCompressed rules (R) +
+    subgroup): coordinates as hex of canonical big-endian x || y (G2: x.c0,
+    x.c1, y.c0, y.c1), or the error class."""
+    try:
+        pt = B.g2_decompress(data) if g2 else B.g1_decompress(data)
+    except B.DecodeError as e:
+        return {"decodes": False, "reason": 2 if "subgroup" in str(e) else 1, "error": str(e)}
+    if pt is None:
+        return {"decodes": False, "reason": 4, "error": "infinity"}
+    if g2:
+        (x0, x1), (y0, y1) = pt
+        coords = [x0, x1, y0, y1]
+    else:
+        coords = list(pt)
+    return {"decodes": True, "reason": 0, "xy": b"".join(B.fp_to_bytes(v) for v in coords).hex(),
+            "recompressed": (B.g2_compress(pt) if g2 else B.g1_compress(pt)).hex()}
+
+
+def legacy_encodings():
+    """Decode-only encodings the reference holds for the G1-signature layout
+    (VERDICT r05 item 5): test/test-integration/test.json's
+    48-byte G1 Signature and Previous and 96-byte G2 Public (the old
+    keys-on-G2 layout; its message/hash predates RFC 9380, so only the
+    encodings are pinned, no verdict), and demo/docker/data's five 48-byte G1
+    node keys (group.toml, 808x.public).  Each also in mutated forms
+    (compression flag cleared, sign flipped, x >= p) with the oracle's class."""
+    ref = "/root/reference"
+    tj = os.path.join(ref, "test/test-integration/test.json")
+    if not os.path.exists(tj):
+        print("reference absent; keeping existing reference_legacy_encodings.json")
+        return
+    t = json.load(open(tj))
+    items = [{"source": "test/test-integration/test.json:Signature", "group": "g1", "hex": t["Signature"]},
+             {"source": "test/test-integration/test.json:Previous", "group": "g1", "hex": t["Previous"]},
+             {"source": "test/test-integration/test.json:Public", "group": "g2", "hex": t["Public"]}]
+    seen = set()
+    data = os.path.join(ref, "demo/docker/data")
+    for fn in ["group.toml"] + sorted(f for f in os.listdir(data) if f.endswith(".public")):
+        for k in re.findall(r'Key\s*=\s*"([0-9a-f]{96})"', open(os.path.join(data, fn)).read()):
+            if k not in seen:
+                seen.add(k)
+                items.append({"source": "demo/docker/data/" + fn, "group": "g1", "hex": k})
+    out = []
+    for it in items:
+        raw = bytes.fromhex(it["hex"])
+        g2 = it["group"] == "g2"
+        out.append(dict(it, kind="as_stored", **_decode_entry(raw, g2)))
+        L = len(raw)
+        muts = {"flag_clear": bytes([raw[0] & 0x7F]) + raw[1:], "sign_flip": bytes([raw[0] ^ 0x20]) + raw[1:],
+                "x_ge_p": bytes([0x80 | 0x1F | (raw[0] & 0x20)]) + b"\xff" * (L - 1),
+                "x_bit_flip": raw[:-1] + bytes([raw[-1] ^ 1])}
+        for kind, m in muts.items():
+            out.append({"source": it["source"], "group": it["group"], "hex": m.hex(), "kind": kind,
+                        **_decode_entry(m, g2)})
+    dump("reference_legacy_encodings.json", {"note": "decode-only; no verdict semantics (SURVEY.md 8(c)4)",
+                                             "cases": out})
+
+
 def recover_cases(name, seed, t, n):
     """Threshold recovery (kyber tbls.Recover (R), restated in
     oracle/drand_ref.recover) over a catalog of partial sets."""
@@ -235,6 +294,7 @@ if __name__ == "__main__":
     chain("chain_on_g1_s1.json", D.SCHEME_UNCHAINED_G1, 1, 12)
     chain("chain_g1_rfc9380_s2.json", D.SCHEME_G1_RFC9380, 2, 8)
     group_keys()
+    legacy_encodings()
     if "--recover" in sys.argv or not os.path.exists(os.path.join(HERE, "recover_t17_n32.json")):
         recover_cases("recover_t3_n8.json", 3, 3, 8)
         recover_cases("recover_t17_n32.json", 5, 17, 32)

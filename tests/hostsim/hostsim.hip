@@ -979,29 +979,3 @@ extern "C" void hs_eng_cof_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {
   g2_compress(out96, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h), inf);
 }
 
-// engine.cuh eng_kb_dec_parts + eng_kb_dec_finish (the split used by
-// k_kb_chain_pre_thr / k_kb_dec_thr) == eng_kb_decompress on n random
-// inputs; returns the number of disagreements.
-extern "C" int hs_kb_dec_split_check(int n, uint64_t seed) {
-  uint64_t s = seed | 1;
-  auto rnd = [&]() {
-    fp x;
-    for (int i = 0; i < FP_LIMBS; ++i) {
-      s ^= s << 13, s ^= s >> 7, s ^= s << 17;
-      x.l[i] = (uint32_t)s & FP_MASK;
-    }
-    x.l[FP_LIMBS - 1] &= 0x1FFFFu;
-    return fp_reduce(x);
-  };
-  int bad = 0;
-  for (int t = 0; t < n; ++t) {
-    const fp2 f1{rnd(), rnd()}, f2{rnd(), rnd()}, f4{rnd(), rnd()}, f5{rnd(), rnd()};
-    const fp ninv = rnd();
-    fp2 a0, a3, b0, b3, nn, vv;
-    eng_kb_decompress(f1, f2, f4, f5, ninv, a0, a3);
-    eng_kb_dec_parts(f1, f2, f4, f5, nn, vv);
-    eng_kb_dec_finish(f1, nn, vv, ninv, b0, b3);
-    if (!fp2_eq(a0, b0) || !fp2_eq(a3, b3)) ++bad;
-  }
-  return bad;
-}

@@ -90,7 +90,8 @@ def test_recover_golden(cref):
 
 def test_cpu_baseline_reports_host_view():
     """bench.py's cpu_baseline leg on a golden chain: every affinity core as
-    threads, the host / affinity / quota core counts, the
+    threads, `cores` = the measured parallelism (VERDICT r05
+    #8), the host / affinity / quota core counts, the
     single-core figure and the all-host-cores projection; verdicts equal the
     fixture's."""
     import numpy as np
@@ -111,5 +112,7 @@ def test_cpu_baseline_reports_host_view():
                np.full(n, 96, dtype=np.uint32), prev, plen, bytes.fromhex(g["genesis"]))
     out = cb.run(ch, 0.2, 2, np.ones(n, dtype=bool))
     assert out["kind"] == "port" and out["sample_verdict_mismatches"] == 0
-    assert out["cores"] == 2 and out["host_cores"] >= 1 and out["affinity_cores"] >= 1
+    assert out["threads"] == 2 and out["host_cores"] >= 1 and out["affinity_cores"] >= 1
+    # cores = the measured parallelism (CPU seconds / wall), not the thread count
+    assert out["cores"] == round(out["effective_parallelism"], 2) and 0 < out["cores"] <= 2.2
     assert out["projected_all_host_cores_value"] == pytest.approx(out["single_core_value"] * out["host_cores"])

@@ -16,7 +16,7 @@ Marked gpu."""
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import load_golden, open_ctx
 from oracle import bls12381 as B
 
 pytestmark = pytest.mark.gpu
@@ -92,6 +92,50 @@ def test_group_toml_keys_decode_on_gpu(gpu_ctx):
     bad.append(bytes([0x80]) + x.to_bytes(48, "big")[1:])  # not on the curve
     rc, _ = decode_g1_points(bad)
     assert rc[1] == 4 and all(r not in (0, 4) for i, r in enumerate(rc) if i != 1)
+
+
+def test_reference_legacy_encodings_decode_on_gpu(gpu_ctx):
+    """The reference's decode-only encodings for the G1-signature layout
+    (SURVEY.md 8(c)4): test/test-integration/test.json's 48-byte G1 Signature
+    and Previous and 96-byte G2 Public, and demo/docker/data's five G1 node
+    keys, each as stored and mutated.  G1 encodings go through the on-G1
+    schemes' signature decoder (k_decode_g1_sigs) and the G2-signature
+    schemes' key decoder; G2 encodings through the on-G1 schemes' key decoder
+    and the G2 signature decoder (k_decode_g2_sigs_sub).  Reasons and
+    coordinates equal the oracle's (tests/golden/reference_legacy_encodings.json).
+    Decode only: test.json's message and hash predate RFC 9380 (its signature
+    verifies under none of SHA-256(prev||round), SHA-256(round) with either
+    RFC 9380 DST), so no verdict is asserted."""
+    from drand_amd import _lib
+    from drand_amd.chain import decode_pubkey, decode_signatures
+    cases = load_golden("reference_legacy_encodings.json")["cases"]
+    for grp, sig_schemes, key_schemes in (
+            ("g1", ("bls-unchained-on-g1", "bls-unchained-g1-rfc9380"), ("pedersen-bls-chained",)),
+            ("g2", ("pedersen-bls-chained", "pedersen-bls-unchained"), ("bls-unchained-on-g1",))):
+        cs = [c for c in cases if c["group"] == grp]
+        raw = [bytes.fromhex(c["hex"]) for c in cs]
+
+        def expect(c):
+            if not c["decodes"]:
+                return None
+            v = [int(c["xy"][96 * j:96 * j + 96], 16) for j in range(len(c["xy"]) // 96)]
+            return tuple(v) if grp == "g1" else ((v[0], v[1]), (v[2], v[3]))
+
+        for name in sig_schemes:
+            reasons, pts = decode_signatures(_sch(name), raw)
+            assert reasons == [c["reason"] for c in cs], name
+            assert pts == [expect(c) for c in cs], name
+        for name in key_schemes:
+            for c, r in zip(cs, raw):
+                if c["decodes"]:
+                    assert decode_pubkey(_sch(name), r) == expect(c)
+                else:
+                    with pytest.raises(_lib.DrandGPUError):
+                        decode_pubkey(_sch(name), r)
+    # the stored test.json key installs as an on-G1 scheme's key (line table built)
+    pub = next(c for c in cases if c["kind"] == "as_stored" and c["group"] == "g2")
+    pkb = np.frombuffer(bytes.fromhex(pub["hex"]), dtype=np.uint8).copy()
+    _lib.check(gpu_ctx.lib.dgpu_set_pubkey(gpu_ctx.handle, _lib.SCHEME_UNCHAINED_G1, _lib.ptr(pkb), 96))
 
 
 def test_two_chains_two_keys_one_context(gpu_ctx):
@@ -365,6 +409,39 @@ def test_null_stream_is_the_default_stream(mode, gpu_ctx):
     assert np.array_equal(r == 0, expect) and set(np.unique(r)) <= {0, 1, 2, 3, 4}
     # dgpu_synchronize: the host-side wait a caller without HIP (cgo) uses
     _lib.check(gpu_ctx.lib.dgpu_synchronize(gpu_ctx.handle))
+
+
+def test_engine_chunk_retry_after_out_of_memory(gpu_ctx):
+    """The engine chunk halves and retries when its buffers do not fit
+    (eng_pairing_locked): the A/B build's DGPU_TEST_ALLOC_CAP=1 GB
+    fails the 40,000-round chunk's 1.8 GB line buffer until the chunk is
+    20,000 rounds.  The call succeeds with the verdicts of an unconstrained
+    context and leaves no stale error message; a later call on the context
+    still works."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 40000
+    c = make_chain(71, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 71, rate=1e-3)
+    ctx = open_ctx({"DGPU_TEST_ALLOC_CAP": str(1 << 30)})
+    try:
+        got = []
+        for _ in range(2):
+            bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+            reason = np.zeros(n, dtype=np.uint8)
+            pk = np.frombuffer(c.pk, dtype=np.uint8).copy()
+            _lib.check(ctx.lib.dgpu_verify_beacons(ctx.handle, _lib.SCHEME_CHAINED, _lib.ptr(pk), pk.size, n,
+                                                   _lib.ptr(c.rounds), _lib.ptr(c.sigs), c.sigs.shape[1],
+                                                   _lib.ptr(c.sig_len), _lib.ptr(c.prev), c.prev.shape[1],
+                                                   _lib.ptr(c.prev_len), _lib.MODE_PER_ROUND, 0, _lib.ptr(bits),
+                                                   _lib.ptr(reason)), ctx.lib)
+            assert ctx.lib.dgpu_last_error() == b""
+            got.append(reason)
+    finally:
+        ctx.close()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(got[0] == 0, expect) and got[0].tolist() == got[1].tolist()
 
 
 def test_empty_batches_are_no_ops(gpu_ctx):

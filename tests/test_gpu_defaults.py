@@ -16,12 +16,11 @@ Tests elsewhere that pin the defaults: test_gpu_parity.py
 test_small_batches_on_lane_kernels, test_rlc_small_batches_take_per_round_path,
 test_rlc_node_checks_on_either_kernel_family."""
 import contextlib
-import os
 
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import load_golden, open_ctx
 
 pytestmark = pytest.mark.gpu
 
@@ -32,17 +31,7 @@ DEFAULTS = {"DGPU_THR_MIN": "65536", "DGPU_RLC_MIN": "131072", "DGPU_COF_ENGINE_
 @contextlib.contextmanager
 def _default_ctx(extra=None):
     from drand_amd import _lib
-    env = dict(DEFAULTS, **(extra or {}))
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        ctx = _lib.Context(0)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    ctx = open_ctx(dict(DEFAULTS, **(extra or {})))
     try:
         yield ctx
     finally:
@@ -145,18 +134,11 @@ def test_recover_batched_check_table_layouts(rows):
         nr = len(msgs)
         out = np.zeros(nr * 96, dtype=np.uint8)
         ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
-        saved = os.environ.get("DGPU_RECOVER_ROWS")
-        os.environ["DGPU_RECOVER_ROWS"] = rows
-        try:
-            with _default_ctx() as ctx:
-                _lib.check(ctx.lib.dgpu_set_group(ctx.handle, len(g["commits"]), g["n"], _lib.ptr(commits)))
-                _lib.check(ctx.lib.dgpu_recover_batch(ctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
-                                                      _lib.ptr(plen), _lib.ptr(out), _lib.ptr(ok), None))
-        finally:
-            if saved is None:
-                del os.environ["DGPU_RECOVER_ROWS"]
-            else:
-                os.environ["DGPU_RECOVER_ROWS"] = saved
+        # the SoA layout is an A/B variant: only the A/B build reads the knob
+        with _default_ctx({"DGPU_RECOVER_ROWS": rows} if rows == "0" else None) as ctx:
+            _lib.check(ctx.lib.dgpu_set_group(ctx.handle, len(g["commits"]), g["n"], _lib.ptr(commits)))
+            _lib.check(ctx.lib.dgpu_recover_batch(ctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(buf), stride,
+                                                  _lib.ptr(plen), _lib.ptr(out), _lib.ptr(ok), None))
         sigs, _ = unpack_recovered(out, ok, None, partials, m)
         assert [s.hex() if s else None for s in sigs] == [c["recovered"] for c in g["cases"]], name
 

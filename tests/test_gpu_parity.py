@@ -6,7 +6,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import load_golden, open_ctx
 from oracle import bls12381 as B
 from oracle import drand_ref as D
 
@@ -243,16 +243,7 @@ def _verify_with_env(c, env, mode=None):
     import os
     from drand_amd import _lib
     n = len(c.rounds)
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        ctx = _lib.Context(0)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    ctx = open_ctx(env)
     try:
         lib = ctx.lib
         _lib.check(lib.dgpu_set_pubkey(ctx.handle, _lib.SCHEME_CHAINED, c.pk, len(c.pk)))
@@ -272,14 +263,13 @@ def _verify_with_env(c, env, mode=None):
 def test_karabina_fe_equals_granger_scott_and_fallback():
     """The Karabina FE (default) against the Granger-Scott kernel (DGPU_FE=gs)
     and against the Karabina path with every 7th item of each chunk forced
-    onto the fallback list (DGPU_KB_TEST_FLAG=7: flagged as if f1 = 0, its FE
-    re-run on prog_fe by k_eng_fe_fb) -- the fallback otherwise practically
-    never runs -- with the 8-lane compressed chain (DGPU_KB_CHAIN=lanes)
-    in place of the per-thread one, and with the decompression split at the
-    inversion (DGPU_KB_DEC=split; fallback forced and not), and with the norms
-    written by the chain or read from the planes (DGPU_KB_NORM, fallback
-    forced).  20,011 rounds (a ragged last block), 1%
-    corrupted: identical reasons, equal to the construction."""
+    onto the fallback list (DGPU_KB_TEST_FLAG=7, a test hook of the A/B build:
+    flagged as if f1 = 0, its FE re-run on prog_fe by k_eng_fe_fb), with the
+    8-lane compressed chain (DGPU_KB_CHAIN=lanes) in place of the per-thread
+    one, and with the norms read from the planes instead of written by the
+    chain (DGPU_KB_NORM=planes, A/B build, fallback forced).  20,011 rounds (a
+    ragged last block), 1% corrupted: identical reasons, equal to the
+    construction."""
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
     n = 20011
@@ -289,13 +279,37 @@ def test_karabina_fe_equals_granger_scott_and_fallback():
     gs = _verify_with_env(c, {"DGPU_FE": "gs"})
     fb = _verify_with_env(c, {"DGPU_KB_TEST_FLAG": "7"})
     lanes = _verify_with_env(c, {"DGPU_KB_CHAIN": "lanes"})
-    split = _verify_with_env(c, {"DGPU_KB_DEC": "split"})
-    split_fb = _verify_with_env(c, {"DGPU_KB_DEC": "split", "DGPU_KB_TEST_FLAG": "7"})
-    # the six norms from the chain's snaps (DGPU_KB_NORM=chain) or from the planes
-    norm_chain = _verify_with_env(c, {"DGPU_KB_NORM": "chain", "DGPU_KB_TEST_FLAG": "7"})
     norm_planes = _verify_with_env(c, {"DGPU_KB_NORM": "planes", "DGPU_KB_TEST_FLAG": "7"})
-    assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist() == split.tolist() == split_fb.tolist()
-    assert norm_chain.tolist() == norm_planes.tolist() == kb.tolist()
+    assert kb.tolist() == gs.tolist() == fb.tolist() == lanes.tolist() == norm_planes.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(kb == 0, expect)
+
+
+def test_karabina_fallback_on_natural_input():
+    """The fallback without a test hook: under the key sk = 1 (pk = g1) a valid
+    signature is H itself, so the two Miller loops are f(g1, H) and f(-g1, H)
+    = conj f(g1, H) up to Fp factors; their product lies in Fp6 and the easy
+    part maps it to m = 1, whose compressed form has f1 = 0: every valid round
+    is flagged by the norms kernel and decided by k_eng_fe_fb, while
+    corrupted rounds (m != 1) take the Karabina path in the same chunks.  The
+    shipped library's reasons equal the construction and the Granger-Scott
+    kernel's (DGPU_FE=gs), per chunk size (one chunk, and 4Ki-round chunks)."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    from oracle import bls12381 as B
+    from oracle import drand_ref as D
+    n = 9001
+    c = make_chain(25, n, _lib.SCHEME_CHAINED, seg_len=64, sk=1)
+    assert bytes(c.pk) == B.g1_compress(B.G1_GEN)
+    # the oracle agrees that such a round verifies (pk = g1, sig = H(msg))
+    assert D.verify_beacon(D.SCHEME_CHAINED, B.g1_decompress(bytes(c.pk)), int(c.rounds[0]),
+                           bytes(c.prev[0, :c.prev_len[0]]), bytes(c.sigs[0]))
+    bad = corrupt(c, 25, rate=2e-2)
+    kb = _verify_with_env(c, {})
+    kb4 = _verify_with_env(c, {"DGPU_ENG_CHUNK": "4096"})
+    gs = _verify_with_env(c, {"DGPU_FE": "gs"})
+    assert kb.tolist() == kb4.tolist() == gs.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(kb == 0, expect)

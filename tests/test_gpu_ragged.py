@@ -18,13 +18,12 @@ corrupted ones alike) and dgpu_verify_recovered over their digests, on
 contexts with the Karabina fallback forced on every 3rd item and off.
 Expected reasons come from the fixtures (tests/golden/make_golden.py)."""
 import hashlib
-import os
 import struct
 
 import numpy as np
 import pytest
 
-from conftest import load_golden
+from conftest import load_golden, open_ctx
 
 pytestmark = pytest.mark.gpu
 
@@ -48,23 +47,9 @@ def _digest(chained, prev, rnd):
     return h.digest()
 
 
-def _open(env):
-    from drand_amd import _lib
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return _lib.Context(0)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
-
-
 @pytest.fixture(scope="module", params=["default", "fallback3"])
 def ctx(request):
-    c = _open({} if request.param == "default" else {"DGPU_KB_TEST_FLAG": "3"})
+    c = open_ctx({} if request.param == "default" else {"DGPU_KB_TEST_FLAG": "3"})
     yield c
     c.close()
 

@@ -9,10 +9,11 @@ holds one entry (buckets cut across many ranges: the fix-up joins the pieces)
 and one where ranges hold many entries.  A corrupted batch on each: RLC
 reasons equal per-round reasons.  Marked gpu."""
 import contextlib
-import os
 
 import numpy as np
 import pytest
+
+from conftest import open_ctx
 
 pytestmark = pytest.mark.gpu
 
@@ -22,18 +23,8 @@ TREE_STAGES = {"rlc_plain_tree", "rlc_leaves_tree", "rlc_confirm"}
 
 @contextlib.contextmanager
 def _ctx(seg):
-    from drand_amd import _lib
-    env = {"DGPU_MSM_SEG": seg, "DGPU_RLC_MIN": "0"}
-    saved = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        ctx = _lib.Context(0)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    # the one-thread-per-bucket sums are an A/B variant (the A/B build reads DGPU_MSM_SEG)
+    ctx = open_ctx({"DGPU_MSM_SEG": seg, "DGPU_RLC_MIN": "0"} if seg == "0" else {"DGPU_RLC_MIN": "0"})
     try:
         yield ctx
     finally:
@@ -67,6 +58,12 @@ def test_clean_root_passes_and_corrupted_matches_per_round(seg, code_name, n):
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
     code = getattr(_lib, code_name)
+    if n < 10000:
+        # "every list range holds one entry": the MSM_MW = 8 list entries per round
+        # (4 MSMs x 2 windows) against the load-balanced kernel's
+        # n_cu x 4 SIMDs x 2 waves x 64 threads (capi.hip rlc_root_msm_t)
+        import torch
+        assert 8 * n <= torch.cuda.get_device_properties(0).multi_processor_count * 512
     c = make_chain(61, n, code, seg_len=64)
     with _ctx(seg) as ctx:
         clean, stages = _reasons(ctx, code, c, _lib.MODE_RLC, profile=True)

@@ -47,14 +47,6 @@ def test_fp_inv_divsteps_matches_fermat(hostsim):
     assert hostsim.hs_fp_inv_check(20000, 12345) == 0
 
 
-def test_kb_decompress_split_matches(hostsim):
-    # the decompression split at the inversion (parts at the chain's snaps,
-    # finish after the per-thread inversion) == the one-piece formula
-    hostsim.hs_kb_dec_split_check.restype = ctypes.c_int
-    hostsim.hs_kb_dec_split_check.argtypes = [ctypes.c_int, ctypes.c_uint64]
-    assert hostsim.hs_kb_dec_split_check(500, 99) == 0
-
-
 def test_fp2_ops_and_sqrt(hostsim):
     rnd = random.Random(2)
     for t in range(12):

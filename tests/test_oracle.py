@@ -93,6 +93,27 @@ def test_group_toml_keys_decode():
         assert B.g1_compress(pt).hex() == k["pk"]
 
 
+def test_reference_legacy_encodings_decode():
+    """The reference's decode-only G1-layout encodings (test/test-integration/
+    test.json, demo/docker/data keys; tests/golden/make_golden.py
+    legacy_encodings): stored forms decode and recompress to the same bytes,
+    mutated forms keep their class."""
+    g = load_golden("reference_legacy_encodings.json")
+    srcs = {c["source"] for c in g["cases"]}
+    assert len(srcs) >= 4 and any("test.json:Public" in s for s in srcs)
+    for c in g["cases"]:
+        raw = bytes.fromhex(c["hex"])
+        g2 = c["group"] == "g2"
+        if c["kind"] == "as_stored":
+            assert c["decodes"] and c["recompressed"] == c["hex"]
+        if c["decodes"]:
+            pt = B.g2_decompress(raw) if g2 else B.g1_decompress(raw)
+            assert (B.g2_compress(pt) if g2 else B.g1_compress(pt)).hex() == c["recompressed"]
+        else:
+            with pytest.raises(B.DecodeError):
+                B.g2_decompress(raw) if g2 else B.g1_decompress(raw)
+
+
 @pytest.mark.parametrize("name", ["chain_chained_s1.json", "chain_unchained_s1.json"])
 def test_golden_chain_verifies(name):
     g = load_golden(name)

@@ -6,6 +6,9 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -121,6 +124,10 @@ constexpr size_t ENG_BYTES_PER_ROUND =
 constexpr size_t LANE_MIN = 262144;
 // decoded public keys cached per context (chain/verify.go:38 passes the key per call)
 constexpr int KEY_SLOTS = 8;
+// host-record staging (verify_status_host_locked): pinned ring slot size and
+// the host threads that fill the slots
+constexpr size_t STAGE_SLOT_BYTES = 16u << 20;
+constexpr int STAGE_COPY_THREADS = 8;
 
 // Per-round G2 path scratch of one "lane" (a stream working on a contiguous
 // slice of the batch).  Two lanes overlap one slice's register-bound hash /
@@ -241,6 +248,15 @@ struct dgpu_ctx {
   bool msm_seg = true;           // load-balanced bucket sums (k_msm_bucket_seg); DGPU_MSM_SEG=0: one thread per bucket (A/B)
   int n_cu = 256;                // compute units (the load-balanced sums launch one wave per SIMD slot)
   bool recover_rows = true;      // the MSM gathers its window tables as rows (DGPU_RECOVER_ROWS=0: SoA planes, A/B)
+  // host-record staging: the pinned ring's two slots, their DMA events, the copy stream
+  void* ring[2] = {nullptr, nullptr};
+  hipEvent_t ring_ev[2] = {nullptr, nullptr};
+  bool ring_busy[2] = {false, false};
+  int ring_next = 0;
+  hipStream_t stream_copy = nullptr;
+  float last_stage_ms = 0.f;      // the last host-record call's staging span (dgpu_staging_stats)
+  size_t last_stage_bytes = 0;
+  bool stage_pageable = false;   // A/B build, DGPU_STAGE=pageable: the round-5 whole-batch pageable copy
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
   // optional per-stage HIP-event timing of the last verify call (event pool;
@@ -1203,9 +1219,27 @@ int check_args(const dgpu_ctx* c, const key_entry* key, const verify_args& a) {
   return DGPU_OK;
 }
 
+// Rounds per slice of the per-round G2 path's lanes (verify_status_locked),
+// which host-record staging follows; the whole batch for every other pipeline.
+size_t lane_slice_len(const dgpu_ctx* c, const verify_args& a) {
+  const size_t n = a.n;
+  if ((a.mode == DGPU_MODE_RLC && n >= c->rlc_min) || sig_on_g1(a.scheme)) return std::max<size_t>(n, 1);
+  const bool two = c->lanes > 1 && !c->profile && n >= LANE_MIN;
+  const size_t slices = two ? std::max<size_t>(2, c->lane_slices) : 1;
+  return two ? ((n / slices + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK
+             : std::max<size_t>(n, 1);
+}
+
+struct host_stager;
+int stager_wait(host_stager* stg, size_t k, hipStream_t s);
+int stager_wait_all(host_stager* stg, hipStream_t s);
+
 // Everything up to the per-item status (ST_*): G1 or G2 signatures, per-round
 // or RLC.  Asynchronous on s (RLC descent synchronizes between its levels).
-int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s) {
+// stg (host records, verify_status_host_locked): each slice's kernels wait
+// for that slice's staging.
+int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, hipStream_t s,
+                         host_stager* stg = nullptr) {
   const size_t n = a.n;
   int rc;
   if ((rc = c->status.ensure(n))) return rc;
@@ -1216,7 +1250,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   if (a.mode == DGPU_MODE_RLC && n >= c->rlc_min) {
     // root first, by bucket MSM; the tree of leaves only when it fails
     const int jw = rlc_geom_of(sig_on_g1(a.scheme)).jw;
-    if ((rc = rlc_points_locked(c, a, s))) return rc;
+    if ((rc = stager_wait_all(stg, s)) || (rc = rlc_points_locked(c, a, s))) return rc;
     if ((rc = c->rlc_root.ensure(2 * jw * 4))) return rc;
     uint32_t* root = (uint32_t*)c->rlc_root.p;
     if ((rc = rlc_root_msm_locked(c, a, s, root))) return rc;
@@ -1232,7 +1266,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
     }
     return rlc_resolve_locked(c, key, a, s, root, true);
   }
-  if (sig_on_g1(a.scheme)) return verify_g1_locked(c, key, a, st, s);
+  if (sig_on_g1(a.scheme)) return (rc = stager_wait_all(stg, s)) ? rc : verify_g1_locked(c, key, a, st, s);
   const uint32_t* consts = (const uint32_t*)key->consts.p;
   const lane_bufs L0{&c->h_pts, &c->sig_pts, &c->h_z,     &c->h_pre, &c->h_tmp,
                      &c->eng_lines, &c->eng_f, &c->eng_n1, &c->eng_kb};
@@ -1243,13 +1277,14 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   // are done, so its register-bound hash runs beside lane 0's LDS-bound
   // engine.  Profiled passes stay on one stream (clean per-kernel times).
   const bool two = c->lanes > 1 && !c->profile && n >= LANE_MIN;
-  const size_t slices = two ? std::max<size_t>(2, c->lane_slices) : 1;
-  const size_t n0 = two ? ((n / slices + ENG_ROUNDS_PER_BLOCK - 1) / ENG_ROUNDS_PER_BLOCK) * ENG_ROUNDS_PER_BLOCK : n;
+  const size_t n0 = two ? lane_slice_len(c, a) : n;
   // one lane: the decode overlaps the hash on the second stream (small calls:
   // the decode's ~0.9 ms leaves the critical path; DGPU_DEC_OVERLAP=0 off)
   // (DGPU_LANES=1 keeps the whole call on one stream: no decode beside the hash either)
   const hipStream_t s_dec = (!two && c->lanes > 1 && c->dec_overlap && !c->profile) ? c->stream2 : nullptr;
-  if ((rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec, consts))) return rc;
+  if ((rc = stager_wait(stg, 0, s)) ||
+      (rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec, consts)))
+    return rc;
   const bool sub = !c->decode_subgroup;
   if (!two)
     return eng_pairing_locked(c, consts, n, (const uint32_t*)c->h_pts.p, (const uint32_t*)c->sig_pts.p, st, s, 0,
@@ -1269,7 +1304,7 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   for (size_t off = n0; off < n; off += n0, ++k) {
     const size_t nk = std::min(n0, n - off);
     const int ln = (int)(k & 1);
-    if ((rc = g2_lane_hash_locked(c, *LL[ln], nk, src_slice(a.m, off), a.sigs + off * a.sig_stride, a.sig_stride,
+    if ((rc = stager_wait(stg, k, ss[ln])) || (rc = g2_lane_hash_locked(c, *LL[ln], nk, src_slice(a.m, off), a.sigs + off * a.sig_stride, a.sig_stride,
                                   a.sig_len + off, st + off, ss[ln])))
       return rc;
     if ((rc = eng_pairing_locked(c, consts, nk, (const uint32_t*)LL[ln]->h_pts->p,
@@ -1336,8 +1371,316 @@ int stage_inputs_locked(dgpu_ctx* c, verify_args& a, hipStream_t s) {
   return DGPU_OK;
 }
 
+// ---------------------------------------------------------------- host-record staging
+// dgpu_verify_beacons / dgpu_verify_recovered / dgpu_verify_multi take host
+// records (the Go caller's slices).  They move through a
+// library-owned pinned ring -- two slots per context, filled by a process-wide
+// pool of host threads and DMA'd to the device on the context's copy stream,
+// a slot reused once its DMA has finished -- slice by slice in the order the
+// per-round pipeline consumes them: the hash of slice k starts as soon as
+// slice k is on the device, while slice k + 1 is still being copied
+// (the lanes of verify_status_locked are the slices).  Pageable
+// hipMemcpyAsync copied the whole batch before the first kernel (VERDICT r05
+// item 4).
+
+// Host memcpy on a few pooled threads (pageable -> pinned runs at host
+// memory bandwidth only when several cores copy).
+class copy_pool {
+ public:
+  explicit copy_pool(int threads) {
+    for (int i = 0; i < threads; ++i) th_.emplace_back([this] { work(); });
+  }
+  ~copy_pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // dst <- src (bytes), split across the pool; returns when every part is done
+  void copy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t PART = 1 << 20;
+    const size_t parts = std::min<size_t>(th_.size(), (bytes + PART - 1) / PART);
+    if (parts <= 1) {
+      memcpy(dst, src, bytes);
+      return;
+    }
+    batch b;
+    b.left = parts;
+    const size_t per = (bytes / parts + 63) & ~(size_t)63;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t p = 0; p < parts; ++p) {
+        const size_t off = std::min(bytes, p * per), len = std::min(bytes - off, per);
+        q_.push_back(task{(uint8_t*)dst + off, (const uint8_t*)src + off, len, &b});
+      }
+    }
+    cv_.notify_all();
+    std::unique_lock<std::mutex> lk(b.mu);
+    b.cv.wait(lk, [&] { return b.left == 0; });
+  }
+
+ private:
+  struct batch {
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t left = 0;
+  };
+  struct task {
+    uint8_t* d;
+    const uint8_t* s;
+    size_t n;
+    batch* b;
+  };
+  void work() {
+    for (;;) {
+      task t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (stop_ && q_.empty()) return;
+        t = q_.front();
+        q_.pop_front();
+      }
+      memcpy(t.d, t.s, t.n);
+      std::lock_guard<std::mutex> lk(t.b->mu);
+      if (--t.b->left == 0) t.b->cv.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<task> q_;
+  bool stop_ = false;
+};
+
+copy_pool& host_copy_pool() {
+  static copy_pool pool(STAGE_COPY_THREADS);
+  return pool;
+}
+
+// The pinned ring: bytes at src (host) -> dst (device) through the slots, on
+// the copy stream, in SLOT-sized pieces (asynchronous; the caller's buffer may
+// be reused once this returns -- every piece has been copied into a slot).
+int ring_copy_locked(dgpu_ctx* c, void* dst, const void* src, size_t bytes) {
+  for (size_t off = 0; off < bytes; off += STAGE_SLOT_BYTES) {
+    const size_t len = std::min(STAGE_SLOT_BYTES, bytes - off);
+    const int k = c->ring_next;
+    c->ring_next ^= 1;
+    if (c->ring_busy[k]) HIP_TRY(hipEventSynchronize(c->ring_ev[k]));  // its previous DMA has read the slot
+    host_copy_pool().copy(c->ring[k], (const uint8_t*)src + off, len);
+    HIP_TRY(hipMemcpyAsync((uint8_t*)dst + off, c->ring[k], len, hipMemcpyHostToDevice, c->stream_copy));
+    HIP_TRY(hipEventRecord(c->ring_ev[k], c->stream_copy));
+    c->ring_busy[k] = true;
+  }
+  return DGPU_OK;
+}
+
+int ring_ensure_locked(dgpu_ctx* c) {
+  for (int k = 0; k < 2; ++k) {
+    if (c->ring[k]) continue;
+    HIP_TRY(hipHostMalloc(&c->ring[k], STAGE_SLOT_BYTES, hipHostMallocDefault));
+  }
+  if (!c->stream_copy) HIP_TRY(hipStreamCreateWithFlags(&c->stream_copy, hipStreamNonBlocking));
+  for (int k = 0; k < 2; ++k)
+    if (!c->ring_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->ring_ev[k], hipEventDisableTiming));
+  return DGPU_OK;
+}
+
+// One call's staging: the device buffers for all n records are allocated up
+// front (a's pointers rewritten to them); a host thread fills slice after
+// slice through the ring and records an event per slice on the copy stream;
+// wait(k, s) makes stream s wait for slice k (the host first waits until the
+// thread has enqueued it).  The destructor joins the thread: nothing of the
+// call's host buffers is read after the entry point returns.
+struct host_stager {
+  dgpu_ctx* c;
+  verify_args host;               // the caller's pointers
+  std::vector<size_t> lo;         // slice k = [lo[k], lo[k + 1])
+  std::vector<hipEvent_t> ev;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t staged = 0;
+  int rc = DGPU_OK;
+  std::string err;
+  std::atomic<bool> cancel{false};
+  hipEvent_t t0 = nullptr, t1 = nullptr;  // copy-stream span of the staging (dgpu_staging_stats)
+  size_t bytes = 0;
+
+  host_stager(dgpu_ctx* c_, const verify_args& h) : c(c_), host(h) {}
+  ~host_stager() {
+    const bool ok = th.joinable();
+    cancel = true;
+    if (ok) th.join();
+    // the staging's span on the copy stream, first piece to last DMA: the
+    // host memcpy into the ring paces the DMAs, so this is the staging time
+    float ms = 0.f;
+    if (ok && rc == DGPU_OK && hipEventSynchronize(t1) == hipSuccess && hipEventElapsedTime(&ms, t0, t1) == hipSuccess) {
+      c->last_stage_ms = ms;
+      c->last_stage_bytes = bytes;
+    }
+    for (hipEvent_t e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (t0) (void)hipEventDestroy(t0);
+    if (t1) (void)hipEventDestroy(t1);
+  }
+  int make_events(size_t slices) {
+    ev.assign(slices, nullptr);
+    for (hipEvent_t& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventCreate(&t0));
+    HIP_TRY(hipEventCreate(&t1));
+    return DGPU_OK;
+  }
+  // items [lo[k], lo[k + 1]) of every record array of `host` into `dev`
+  int stage_slice(const verify_args& dev, size_t a, size_t b) {
+    const msg_src& m = host.m;
+    const size_t n = b - a;
+    bytes += n * (host.sig_stride + 4 + (m.msgs ? m.msg_stride + 4 : 8 + (m.chained ? m.prev_stride + 4 : 0)));
+    int r;
+    if ((r = ring_copy_locked(c, (uint8_t*)dev.sigs + a * host.sig_stride, host.sigs + a * host.sig_stride,
+                              n * host.sig_stride)) ||
+        (r = ring_copy_locked(c, (uint32_t*)dev.sig_len + a, host.sig_len + a, n * 4)))
+      return r;
+    if (m.msgs) {
+      if ((r = ring_copy_locked(c, (uint8_t*)dev.m.msgs + a * m.msg_stride, m.msgs + a * m.msg_stride,
+                                n * m.msg_stride)) ||
+          (r = ring_copy_locked(c, (uint32_t*)dev.m.msg_len + a, m.msg_len + a, n * 4)))
+        return r;
+      return DGPU_OK;
+    }
+    if ((r = ring_copy_locked(c, (uint64_t*)dev.m.rounds + a, m.rounds + a, n * 8))) return r;
+    if (m.chained && ((r = ring_copy_locked(c, (uint8_t*)dev.m.prev + a * m.prev_stride, m.prev + a * m.prev_stride,
+                                            n * m.prev_stride)) ||
+                      (r = ring_copy_locked(c, (uint32_t*)dev.m.prev_len + a, m.prev_len + a, n * 4))))
+      return r;
+    return DGPU_OK;
+  }
+  void start(const verify_args& dev) {
+    th = std::thread([this, dev] {
+      (void)hipSetDevice(c->device);
+      (void)hipEventRecord(t0, c->stream_copy);
+      for (size_t k = 0; k + 1 < lo.size(); ++k) {
+        int r = cancel ? DGPU_EINVAL : stage_slice(dev, lo[k], lo[k + 1]);
+        if (!r && hipEventRecord(ev[k], c->stream_copy) != hipSuccess) r = set_err(DGPU_EDEVICE, "hipEventRecord");
+        if (!r && k + 2 == lo.size() && hipEventRecord(t1, c->stream_copy) != hipSuccess)
+          r = set_err(DGPU_EDEVICE, "hipEventRecord");
+        std::lock_guard<std::mutex> lk(mu);
+        if (r) {
+          rc = r;
+          err = cancel ? std::string("staging cancelled") : g_last_error;
+        } else {
+          staged = k + 1;
+        }
+        cv.notify_all();
+        if (r) return;
+      }
+    });
+  }
+  int wait(size_t k, hipStream_t s) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return staged > k || rc != DGPU_OK; });
+    if (staged <= k) return set_err(rc, "%s", err.c_str());
+    HIP_TRY(hipStreamWaitEvent(s, ev[k], 0));
+    return DGPU_OK;
+  }
+  int wait_all(hipStream_t s) { return lo.size() > 1 ? wait(lo.size() - 2, s) : DGPU_OK; }
+};
+
+int stager_wait(host_stager* stg, size_t k, hipStream_t s) { return stg ? stg->wait(k, s) : DGPU_OK; }
+int stager_wait_all(host_stager* stg, hipStream_t s) { return stg ? stg->wait_all(s) : DGPU_OK; }
+
+// Checks of the host records and the device buffers of a staged call; a's
+// pointers become the device copies' (their contents arrive slice by slice).
+int stage_prepare_locked(dgpu_ctx* c, verify_args& a) {
+  const size_t n = a.n;
+  int rc;
+  if ((rc = ring_ensure_locked(c))) return rc;
+  if ((rc = c->in_sigs.ensure(n * a.sig_stride)) || (rc = c->in_sig_len.ensure(n * 4))) return rc;
+  a.sigs = (const uint8_t*)c->in_sigs.p;
+  a.sig_len = (const uint32_t*)c->in_sig_len.p;
+  msg_src& m = a.m;
+  if (m.msgs) {
+    for (size_t i = 0; i < n; ++i)
+      if (m.msg_len[i] > m.msg_stride) return set_err(DGPU_EINVAL, "msg_len[%zu]=%u > msg_stride", i, m.msg_len[i]);
+    if ((rc = c->in_msgs.ensure(n * m.msg_stride + 1)) || (rc = c->in_msg_len.ensure(n * 4))) return rc;
+    m.msgs = (const uint8_t*)c->in_msgs.p;
+    m.msg_len = (const uint32_t*)c->in_msg_len.p;
+    return DGPU_OK;
+  }
+  if ((rc = c->in_rounds.ensure(n * 8))) return rc;
+  m.rounds = (const uint64_t*)c->in_rounds.p;
+  if (m.chained) {
+    for (size_t i = 0; i < n; ++i)
+      if (m.prev_len[i] > m.prev_stride) return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, m.prev_len[i]);
+    if ((rc = c->in_prev.ensure(n * m.prev_stride + 1)) || (rc = c->in_prev_len.ensure(n * 4))) return rc;
+    m.prev = (const uint8_t*)c->in_prev.p;
+    m.prev_len = (const uint32_t*)c->in_prev_len.p;
+  }
+  return DGPU_OK;
+}
+
+// verify_status_locked over host records, overlapping their staging with the
+// verification: the slices are the per-round G2 path's lane slices
+// (lane_slice_len), one slice for every other pipeline.
+int verify_status_host_locked(dgpu_ctx* c, const key_entry* key, verify_args& a, hipStream_t s) {
+  host_stager stg(c, a);
+  int rc;
+  if ((rc = stage_prepare_locked(c, a))) return rc;
+  // the copy stream (device buffers, ring slots) after the previous call's work
+  HIP_TRY(hipStreamWaitEvent(c->stream_copy, c->done, 0));
+  const size_t n0 = lane_slice_len(c, a);
+  for (size_t off = 0; off < a.n; off += n0) stg.lo.push_back(off);
+  stg.lo.push_back(a.n);
+  if ((rc = stg.make_events(stg.lo.size() - 1))) return rc;
+  stg.start(a);
+  rc = verify_status_locked(c, key, a, s, &stg);
+  if (!rc) rc = stg.wait_all(s);  // every slice consumed (no-op when the pipeline waited for each)
+  return rc;
+}
+
+// Every record of a host call on the device before anything else runs on s
+// (the RLC root's points need the whole shard): one slice through the ring.
+int stage_all_host_locked(dgpu_ctx* c, verify_args& a, hipStream_t s) {
+  host_stager stg(c, a);
+  int rc;
+  if ((rc = stage_prepare_locked(c, a))) return rc;
+  HIP_TRY(hipStreamWaitEvent(c->stream_copy, c->done, 0));
+  stg.lo = {0, a.n};
+  if ((rc = stg.make_events(1))) return rc;
+  stg.start(a);
+  return stg.wait_all(s);
+}
+
 // Host-buffer verify: stage, verify, copy the verdicts back (synchronous).
+int verify_host_pageable_locked(dgpu_ctx* c, const key_entry* key, verify_args a, uint8_t* verdict_bits,
+                                uint8_t* reason);
 int verify_host_locked(dgpu_ctx* c, const key_entry* key, verify_args a, uint8_t* verdict_bits, uint8_t* reason) {
+  if (c->stage_pageable) return verify_host_pageable_locked(c, key, a, verdict_bits, reason);
+  int rc = check_args(c, key, a);
+  if (rc || a.n == 0) return rc;
+  if (!verdict_bits) return set_err(DGPU_EINVAL, "null verdict buffer");
+  hipStream_t s = c->stream;
+  stream_order ord(c, s);
+  if ((rc = c->out_bits.ensure((a.n + 7) / 8)) || (rc = c->out_reason.ensure(a.n))) return rc;
+  if ((rc = verify_status_host_locked(c, key, a, s))) return rc;
+  const uint8_t* st = (const uint8_t*)c->status.p;
+  mark(c, s, "pack_verdicts");
+  hipLaunchKernelGGL(k_pack_verdicts, dim3(grid_for((a.n + 7) / 8, 256)), dim3(256), 0, s, a.n, st,
+                     (uint8_t*)c->out_bits.p);
+  HIP_TRY(hipGetLastError());
+  mark(c, s);
+  HIP_TRY(hipMemcpyAsync(verdict_bits, c->out_bits.p, (a.n + 7) / 8, hipMemcpyDeviceToHost, s));
+  if (reason) HIP_TRY(hipMemcpyAsync(reason, st, a.n, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return DGPU_OK;
+}
+
+// The pre-ring host path (whole batch staged by pageable hipMemcpyAsync, then
+// verified): kept for the A/B build's DGPU_STAGE=pageable comparison.
+int verify_host_pageable_locked(dgpu_ctx* c, const key_entry* key, verify_args a, uint8_t* verdict_bits,
+                                uint8_t* reason) {
   int rc = check_args(c, key, a);
   if (rc || a.n == 0) return rc;
   if (!verdict_bits) return set_err(DGPU_EINVAL, "null verdict buffer");
@@ -1451,6 +1794,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
   const char* ktf = getenv("DGPU_KB_TEST_FLAG");
   if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
+  const char* stv = getenv("DGPU_STAGE");
+  if (stv && !strcmp(stv, "pageable")) c->stage_pageable = true;
   const char* tac = getenv("DGPU_TEST_ALLOC_CAP");
   if (tac && atol(tac) >= 0) g_test_alloc_cap = (size_t)atol(tac);
 #endif
@@ -1486,6 +1831,14 @@ void dgpu_close(dgpu_ctx* c) {
   for (hipEvent_t e : c->cof_ev)
     if (e) hipEventDestroy(e);
   if (c->done) hipEventDestroy(c->done);
+  if (c->stream_copy) {
+    hipStreamSynchronize(c->stream_copy);
+    hipStreamDestroy(c->stream_copy);
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (c->ring_ev[k]) hipEventDestroy(c->ring_ev[k]);
+    if (c->ring[k]) hipHostFree(c->ring[k]);
+  }
   for (key_entry& k : c->keys) {
     k.consts.release();
     k.table.release();
@@ -1683,6 +2036,14 @@ int dgpu_synchronize(dgpu_ctx* c) {
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipEventSynchronize(c->done));
+  return DGPU_OK;
+}
+
+int dgpu_staging_stats(dgpu_ctx* c, double* ms, uint64_t* bytes) {
+  if (!c || !ms || !bytes) return set_err(DGPU_EINVAL, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *ms = c->last_stage_ms;
+  *bytes = c->last_stage_bytes;
   return DGPU_OK;
 }
 

@@ -265,23 +265,28 @@ int dgpu_verify_multi(dgpu_multi* m, int scheme, const uint8_t* pk, size_t pk_le
   const bool rlc = mode == DGPU_MODE_RLC;
   const bool g1 = sig_on_g1(scheme);
   const int jw = g1 ? G1J_WORDS : G2J_WORDS;  // root: P, S (stride-1 Jacobian of the signature group)
-  // phase 1: stage the shard, then per-round verification (or the RLC trees)
+  // phase 1: stage the shard (the records of the device's shard through its
+  // context's pinned ring, overlapped with the verification) and verify it
+  // per round (or compute its RLC root)
   rc = for_each_device(m, [&](int k) -> int {
     dgpu_ctx* c = m->ctx[k];
     verify_args& a = args[k];
     if (a.n == 0) return DGPU_OK;
     hipStream_t s = c->stream;
     int r;
-    if ((r = stage_inputs_locked(c, a, s))) return r;
     if ((r = c->status.ensure(a.n))) return r;
     c->n_ev = 0;
     c->ev_overflow = false;
     if (rlc) {  // the shard's points and its root by bucket MSM (the leaves wait for a failing root)
       c->rlc_pending = false;  // overwrites the points a pending per-rank root (dgpu_rlc_root_device) kept
-      if ((r = rlc_points_locked(c, a, s)) || (r = c->msm_root.ensure(2 * (size_t)jw * 4))) return r;
+      if ((r = stage_all_host_locked(c, a, s)) || (r = rlc_points_locked(c, a, s)) ||
+          (r = c->msm_root.ensure(2 * (size_t)jw * 4)))
+        return r;
       return rlc_root_msm_locked(c, a, s, (uint32_t*)c->msm_root.p);
     }
-    if ((r = verify_status_locked(c, keys[k], a, s))) return r;
+    // the shard's records through the context's pinned ring, slice by slice
+    // beside the verification (verify_status_host_locked)
+    if ((r = verify_status_host_locked(c, keys[k], a, s))) return r;
     return pack_shard_locked(c, a.n, (uint8_t*)m->buf[k].bits.p, (uint8_t*)m->buf[k].reasons.p, s);
   });
   if (rc) return rc;

@@ -245,6 +245,14 @@ int dgpu_verify_batch_device(dgpu_ctx *ctx, int scheme, size_t n, const uint64_t
  * device (its results are then valid on the host and on any stream). */
 int dgpu_synchronize(dgpu_ctx *ctx);
 int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
+/* Host-record staging of the last call on the context that took host records
+ * (dgpu_verify_beacons, dgpu_verify_batch, dgpu_verify_recovered, a shard of
+ * dgpu_verify_multi): the records go through a library-owned pinned ring
+ * (two 16 MiB slots per context, filled by host threads, DMA'd on the
+ * context's copy stream) slice by slice, each slice's kernels starting when
+ * its records have arrived.  ms = the staging's span on the copy stream,
+ * first piece to last DMA (device timeline); bytes = record bytes staged. */
+int dgpu_staging_stats(dgpu_ctx *ctx, double *ms, uint64_t *bytes);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
 
 /* Batch DigestMessage (chain/verify.go:24-32): out32 = n x 32 bytes. */

@@ -444,6 +444,61 @@ def test_engine_chunk_retry_after_out_of_memory(gpu_ctx):
     assert np.array_equal(got[0] == 0, expect) and got[0].tolist() == got[1].tolist()
 
 
+@pytest.mark.parametrize("n,scheme", [(300001, "SCHEME_CHAINED"), (70001, "SCHEME_UNCHAINED"),
+                                      (50001, "SCHEME_UNCHAINED_G1")])
+def test_host_records_staged_through_the_ring(n, scheme, gpu_ctx):
+    """Host records reach the device through the pinned ring (two 16 MiB
+    slots, so every array here takes several pieces), in two slices beside
+    the two lanes for the large chained batch and in one slice otherwise:
+    dgpu_staging_stats reports exactly the record bytes, the verdicts equal
+    the device-resident entry point's on the same records (and the
+    construction), and the caller's buffers are free to reuse after the
+    call (they are overwritten and verified again)."""
+    import torch
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    code = getattr(_lib, scheme)
+    c = make_chain(73, n, code, seg_len=64)
+    bad = corrupt(c, 73, rate=1e-3)
+    pk = np.frombuffer(c.pk, dtype=np.uint8).copy()
+    lib, h = gpu_ctx.lib, gpu_ctx.handle
+
+    def host_call():
+        bits = np.zeros((n + 7) // 8, dtype=np.uint8)
+        reason = np.zeros(n, dtype=np.uint8)
+        _lib.check(lib.dgpu_verify_beacons(h, code, _lib.ptr(pk), pk.size, n, _lib.ptr(c.rounds), _lib.ptr(c.sigs),
+                                           c.sigs.shape[1], _lib.ptr(c.sig_len), _lib.ptr(c.prev), c.prev.shape[1],
+                                           _lib.ptr(c.prev_len), _lib.MODE_PER_ROUND, 0, _lib.ptr(bits),
+                                           _lib.ptr(reason)))
+        return reason
+
+    got = host_call()
+    ms, nbytes = _lib.staging_stats(gpu_ctx)
+    per = c.sigs.shape[1] + 4 + 8 + ((c.prev.shape[1] + 4) if code == _lib.SCHEME_CHAINED else 0)
+    assert nbytes == n * per and ms > 0
+    dev = {k: torch.from_numpy(np.ascontiguousarray(getattr(c, k))).cuda()
+           for k in ("rounds", "sigs", "sig_len", "prev", "prev_len")}
+    dbits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device="cuda")
+    dreason = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.dgpu_verify_beacons_device(h, code, _lib.ptr(pk), pk.size, n, _lib.ptr(dev["rounds"]),
+                                              _lib.ptr(dev["sigs"]), c.sigs.shape[1], _lib.ptr(dev["sig_len"]),
+                                              _lib.ptr(dev["prev"]), c.prev.shape[1], _lib.ptr(dev["prev_len"]),
+                                              _lib.MODE_PER_ROUND, 0, _lib.ptr(dbits), _lib.ptr(dreason), None))
+    torch.cuda.synchronize()
+    assert dreason.cpu().numpy().tolist() == got.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(got == 0, expect)
+    # the records swapped in place (every signature moves to the next round): all fail now
+    keep = c.sigs.copy()
+    c.sigs[:] = np.roll(keep, 1, axis=0)
+    try:
+        again = host_call()
+    finally:
+        c.sigs[:] = keep
+    assert (again != 0).sum() >= n - 2
+
+
 def test_empty_batches_are_no_ops(gpu_ctx):
     """n = 0 on the batch entry points (CheckPastBeacons over an empty range,
     an empty tryNode window): DGPU_OK, nothing written, NULL record arrays

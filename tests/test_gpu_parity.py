@@ -337,10 +337,13 @@ def test_thread_lines_equal_engine_lines():
 
 def test_two_lane_per_round_large_chain():
     """A batch spanning two engine chunks runs on two lanes (streams, half the
-    batch each, capi.hip verify_device_locked): 2*131072 + 1001 rounds (odd
-    split), 0.1% corrupted -- reasons equal the one-lane context's
-    (DGPU_LANES=1, 64Ki-round engine chunks: five chunks) and the
-    construction."""
+    batch each, capi.hip verify_status_locked), its host records staged slice
+    by slice through the pinned ring beside the verification
+    (verify_status_host_locked): 2*131072 + 1001 rounds (odd split), 0.1%
+    corrupted -- reasons equal the one-lane context's (DGPU_LANES=1,
+    64Ki-round engine chunks: five chunks), five slices alternating between
+    the lanes (A/B build), the round-5 whole-batch pageable staging (A/B
+    build, DGPU_STAGE=pageable) and the construction."""
     from drand_amd import _lib
     from drand_amd.synth import corrupt, make_chain
     n = 2 * 131072 + 1001
@@ -350,7 +353,8 @@ def test_two_lane_per_round_large_chain():
     two = _verify_with_env(c, {"DGPU_LANES": "2"})
     one = _verify_with_env(c, {"DGPU_LANES": "1", "DGPU_ENG_CHUNK": "65536"})
     five = _verify_with_env(c, {"DGPU_LANES": "2", "DGPU_LANE_SLICES": "5"})  # slices alternating between lanes
-    assert two.tolist() == one.tolist() == five.tolist()
+    page = _verify_with_env(c, {"DGPU_STAGE": "pageable"})
+    assert two.tolist() == one.tolist() == five.tolist() == page.tolist()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(two == 0, expect)

@@ -256,6 +256,8 @@ struct dgpu_ctx {
   hipStream_t stream_copy = nullptr;
   float last_stage_ms = 0.f;      // the last host-record call's staging span (dgpu_staging_stats)
   size_t last_stage_bytes = 0;
+  int eng_xw = 0;                // 16-group 192-thread engine blocks (no idle lanes): bit 0 the Miller loop
+                                 // (k_eng_miller_xw), bit 1 the FE segments (k_eng_fe_seg_xw); A/B: DGPU_ENG_XW
   bool stage_pageable = false;   // A/B build, DGPU_STAGE=pageable: the round-5 whole-batch pageable copy
   // staging for host-pointer entry points
   DevBuf in_rounds, in_sigs, in_sig_len, in_prev, in_prev_len, in_msgs, in_msg_len, out_bits, out_reason, misc;
@@ -933,9 +935,17 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
       HIP_TRY(hipGetLastError());
     }
     mark(c, s, "eng_fe");
-    hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, ENG_PROG_FEK_OFF[seg],
-                       ENG_PROG_FEK_OFF[seg + 1] - ENG_PROG_FEK_OFF[seg], seg == 0, seg == nseg - 1, cnt, r0, consts,
-                       (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
+    const int so = ENG_PROG_FEK_OFF[seg], sl = ENG_PROG_FEK_OFF[seg + 1] - ENG_PROG_FEK_OFF[seg];
+    if ((c->eng_xw & 2) && seg > 0 && seg < nseg - 1)
+      hipLaunchKernelGGL(k_eng_fe_seg_xw<ENG_FEK_MID_SLOTS>, dim3(grid_for(cnt, ENG_XW_ITEMS)), dim3(ENG_XW_BLOCK), 0, s,
+                         so, sl, false, false, cnt, r0, consts, (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
+    else if (c->eng_xw & 2)
+      hipLaunchKernelGGL(k_eng_fe_seg_xw<ENG_SLOTS_FE>, dim3(grid_for(cnt, ENG_XW_ITEMS)), dim3(ENG_XW_BLOCK), 0, s,
+                         so, sl, seg == 0, seg == nseg - 1, cnt, r0, consts, (const uint32_t*)f, n1inv, xbuf, flags, fb,
+                         st);
+    else
+      hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, so, sl, seg == 0, seg == nseg - 1, cnt, r0,
+                         consts, (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
     HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_eng_fe_fb, dim3(ENG_FB_GRID), dim3(ENG_BLOCK), 0, s, cnt, r0, consts, f, n1inv, st,
@@ -1021,7 +1031,11 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
       }
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_miller");
-      hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
+      if (c->eng_xw & 1)
+        hipLaunchKernelGGL(k_eng_miller_xw, dim3(grid_for(cnt, ENG_XW_ITEMS)), dim3(ENG_XW_BLOCK), 0, s, cnt, consts,
+                           lines, f, n1);
+      else
+        hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
       HIP_TRY(hipGetLastError());
     }
     const size_t inv_threads = std::max<size_t>(1, (cnt + 63) / 64);
@@ -1794,6 +1808,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
   const char* ktf = getenv("DGPU_KB_TEST_FLAG");
   if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
+  const char* xwv = getenv("DGPU_ENG_XW");
+  if (xwv) c->eng_xw = atoi(xwv) & 3;
   const char* stv = getenv("DGPU_STAGE");
   if (stv && !strcmp(stv, "pageable")) c->stage_pageable = true;
   const char* tac = getenv("DGPU_TEST_ALLOC_CAP");

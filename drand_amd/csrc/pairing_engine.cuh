@@ -115,7 +115,8 @@ constexpr bool ENG_COMPILED = true;
 constexpr bool ENG_COMPILED = false;
 #endif
 // KB: LD12 / ST12 address the Karabina FE planes (io.xbuf), else fbuf.
-template <bool FIXED = false, bool CYC = false, int FAM = -1, bool KB = false>
+// XW: the group's lanes may span waves (eng_sync barriers; k_eng_miller_xw).
+template <bool FIXED = false, bool CYC = false, int FAM = -1, bool KB = false, bool XW = false>
 __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t* g, const uint32_t* c,
                                          const eng_lane& L, const eng_io& io) {
   int step = 0;
@@ -137,10 +138,10 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
         continue;
       }
       bool done = false;
-      if constexpr (ENG_COMPILED && FAM == 0) done = eng_run_c0((int)a, g, c, L.k, sink);
-      if constexpr (ENG_COMPILED && FAM == 1) done = eng_run_c1((int)a, g, c, L.k, sink);
-      if constexpr (ENG_COMPILED && FAM == 2) done = eng_run_c2((int)a, g, c, L.k, sink);
-      if (!done) eng_run((int)a, g, c, L.k, sink);
+      if constexpr (ENG_COMPILED && FAM == 0) done = eng_run_c0<XW>((int)a, g, c, L.k, sink);
+      if constexpr (ENG_COMPILED && FAM == 1) done = eng_run_c1<XW>((int)a, g, c, L.k, sink);
+      if constexpr (ENG_COMPILED && FAM == 2) done = eng_run_c2<XW>((int)a, g, c, L.k, sink);
+      if (!done) eng_run<XW>((int)a, g, c, L.k, sink);
     } else if (opc == ENG_OPC_STEP) {
       ++step;
     } else if (opc == ENG_OPC_LDLINE) {
@@ -152,15 +153,19 @@ __device__ __forceinline__ void eng_exec(const uint32_t* prog, int len, uint32_t
         eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.lines, eng_blk_off(L.blk, ENG_LINE_STEPS, step, L.g, L.k)));
       }
       ++step;
+      // consecutive LDLINEs (l1, l2 of a step) share one barrier
+      if (!(pc + 1 < len && (prog[pc + 1] >> 24) == ENG_OPC_LDLINE)) eng_sync<XW>();
     } else if (opc == ENG_OPC_LD12) {
       const int pl = (int)b / 12;
       if constexpr (KB) eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.xbuf, eng_blk_off(L.blk, ENG_KB_PLANES, pl, L.g, L.k)));
       else eng_st(g + (a + L.k) * ENG_SLOT_WORDS, ld_blk(io.fbuf, eng_blk_off(L.blk, 2, (int)b / 12, L.g, L.k)));
+      eng_sync<XW>();
     } else if (opc == ENG_OPC_ST12) {
       if (L.valid) {
         if constexpr (KB) st_blk(io.xbuf, eng_blk_off(L.blk, ENG_KB_PLANES, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
         else st_blk(io.fbuf, eng_blk_off(L.blk, 2, (int)b / 12, L.g, L.k), eng_ld(g + (a + L.k) * ENG_SLOT_WORDS));
       }
+      eng_sync<XW>();
     }
     asm volatile("" ::: "memory");
   }
@@ -323,6 +328,45 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_miller(size_t cnt, const u
   if (L.valid) st_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
 }
 
+// ---------------------------------------------------------------- k_eng_miller_xw
+// k_eng_miller without idle lanes: a 192-thread block (three waves) holds 16
+// groups of 12 lanes, so every lane carries an item (a 64-lane wave holds
+// five groups and four idle lanes).  Groups 5 and 10 span two waves, so the
+// sub-ops are ordered by barriers (engine.cuh eng_sync).  The DPP partner of
+// lane k (k ^ 1) stays in its wave: groups start at even lanes and the wave
+// boundaries (64, 128) fall on even k.  Item i = 16 blockIdx.x + group; the
+// HBM buffers keep the 5-round blocked layout (block i / 5, group i % 5).
+constexpr int ENG_XW_ITEMS = 16;
+constexpr int ENG_XW_BLOCK = ENG_XW_ITEMS * 12;  // three waves
+static_assert(ENG_XW_BLOCK == 192, "16 groups of 12 lanes");
+
+__device__ __forceinline__ eng_lane eng_lane_xw(size_t cnt, int& grp) {
+  grp = (int)threadIdx.x / 12;
+  eng_lane L;
+  L.k = (int)threadIdx.x - 12 * grp;
+  const size_t gi = (size_t)blockIdx.x * ENG_XW_ITEMS + grp;
+  L.valid = gi < cnt;
+  L.i = L.valid ? gi : cnt - 1;
+  L.blk = L.i / ENG_ROUNDS_PER_BLOCK;
+  L.g = (int)(L.i - L.blk * ENG_ROUNDS_PER_BLOCK);
+  return L;
+}
+
+__global__ void __launch_bounds__(ENG_XW_BLOCK, 3) k_eng_miller_xw(size_t cnt, const uint32_t* __restrict__ consts,
+                                                                uint32_t* __restrict__ lines,
+                                                                uint32_t* __restrict__ fbuf, uint32_t* __restrict__ n1) {
+  __shared__ uint32_t lds[(ENG_NCONST + ENG_XW_ITEMS * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS];
+  uint32_t* c = lds;
+  eng_load_consts(c, consts);
+  int grp;
+  const eng_lane L = eng_lane_xw(cnt, grp);
+  uint32_t* g = lds + (ENG_NCONST + grp * ENG_SLOTS_MILLER) * ENG_SLOT_WORDS;
+  eng_st(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS, L.k == 0 ? fp_one() : fp_zero());
+  eng_sync<true>();
+  eng_exec<false, false, 1, false, true>(ENG_PROG_MILLER, ENG_PROG_MILLER_LEN, g, c, L, eng_io{lines, fbuf, n1, cnt});
+  if (L.valid) st_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k), eng_ld(g + (ENG_M_F + L.k) * ENG_SLOT_WORDS));
+}
+
 // ---------------------------------------------------------------- k_eng_inv
 // Thread t inverts the N1 of rounds t, t + T, t + 2T, ... (T = threads in the
 // grid) by Montgomery's trick; prefix products go to `pre` (same layout).
@@ -453,6 +497,54 @@ __global__ void __launch_bounds__(ENG_BLOCK, 3) k_eng_fe_seg(int off, int len, b
     const bool flagged = L.valid && flags[L.i];
     if (L.valid && L.k == 0 && !all && !flagged && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_PAIRING;
     if (__ballot(flagged) != 0 && threadIdx.x == 0) fb[1 + atomicAdd(fb, 1u)] = blockIdx.x;
+  }
+}
+
+// k_eng_fe_seg on 16-group 192-thread blocks (no idle lanes; see
+// k_eng_miller_xw).  SLOTS: the group's LDS slots the segment needs (34 for
+// the segments between the chains, 46 for the easy part and the last one;
+// tools/gen_engine.py prog_fe_kb), so the in-between segments fit four blocks
+// per CU.  The verdict vote of a group spanning waves goes through LDS; the
+// fallback list names 5-round blocks (k_eng_fe_fb's unit), each once: by the
+// first flagged item of the block.
+template <int SLOTS>
+__global__ void __launch_bounds__(ENG_XW_BLOCK, 3) k_eng_fe_seg_xw(int off, int len, bool first, bool last, size_t cnt,
+                                                                size_t r0, const uint32_t* __restrict__ consts,
+                                                                const uint32_t* __restrict__ fbuf,
+                                                                const uint32_t* __restrict__ n1inv,
+                                                                uint32_t* __restrict__ xbuf, uint8_t* __restrict__ flags,
+                                                                uint32_t* __restrict__ fb, uint8_t* __restrict__ status) {
+  static_assert(SLOTS <= ENG_SLOTS_FE, "segment slots");
+  __shared__ uint32_t lds[(ENG_NCONST + ENG_XW_ITEMS * SLOTS) * ENG_SLOT_WORDS];
+  __shared__ uint32_t vote[ENG_XW_ITEMS];
+  uint32_t* c = lds;
+  if (threadIdx.x < ENG_XW_ITEMS) vote[threadIdx.x] = 0;
+  eng_load_consts(c, consts);
+  int grp;
+  const eng_lane L = eng_lane_xw(cnt, grp);
+  uint32_t* g = lds + (ENG_NCONST + grp * SLOTS) * ENG_SLOT_WORDS;
+  if (first) {
+    eng_st(g + (ENG_E_F + L.k) * ENG_SLOT_WORDS, ld_blk(fbuf, eng_blk_off(L.blk, 2, 0, L.g, L.k)));
+    if (L.k == 0) eng_st(g + ENG_E_N1I * ENG_SLOT_WORDS, ld_soa(n1inv, cnt, L.i));
+    if (L.valid && L.k == 0) flags[L.i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) fb[0] = 0;
+  }
+  eng_sync<true>();
+  eng_io io{nullptr, nullptr, nullptr, cnt};
+  io.xbuf = xbuf;
+  eng_exec<false, false, 2, true, true>(ENG_PROG_FEK + off, len, g, c, L, io);
+  if (last) {
+    const fp v = eng_ld(g + (ENG_E_R + L.k) * ENG_SLOT_WORDS);
+    if (eng_eq_canon(v, L.k == 0 ? fp_one() : fp_zero())) atomicOr(&vote[grp], 1u << L.k);
+    eng_sync<true>();
+    const bool all = vote[grp] == 0xFFFu;
+    const bool flagged = L.valid && flags[L.i];
+    if (L.valid && L.k == 0 && !all && !flagged && status[r0 + L.i] == ST_OK) status[r0 + L.i] = ST_PAIRING;
+    if (flagged && L.k == 0) {
+      bool first_in_blk = true;
+      for (int q = 1; q <= L.g; ++q) first_in_blk = first_in_blk && !flags[L.i - q];
+      if (first_in_blk) fb[1 + atomicAdd(fb, 1u)] = (uint32_t)L.blk;
+    }
   }
 }
 

@@ -489,14 +489,22 @@ def test_host_records_staged_through_the_ring(n, scheme, gpu_ctx):
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False
     assert np.array_equal(got == 0, expect)
-    # the records swapped in place (every signature moves to the next round): all fail now
+    # the caller reuses its buffers: every signature moved to the next round
+    # (only an "other round's signature" corruption can turn valid again)
     keep = c.sigs.copy()
     c.sigs[:] = np.roll(keep, 1, axis=0)
     try:
         again = host_call()
+        dev["sigs"].copy_(torch.from_numpy(c.sigs))
+        _lib.check(lib.dgpu_verify_beacons_device(h, code, _lib.ptr(pk), pk.size, n, _lib.ptr(dev["rounds"]),
+                                                  _lib.ptr(dev["sigs"]), c.sigs.shape[1], _lib.ptr(dev["sig_len"]),
+                                                  _lib.ptr(dev["prev"]), c.prev.shape[1], _lib.ptr(dev["prev_len"]),
+                                                  _lib.MODE_PER_ROUND, 0, _lib.ptr(dbits), _lib.ptr(dreason), None))
+        torch.cuda.synchronize()
     finally:
         c.sigs[:] = keep
-    assert (again != 0).sum() >= n - 2
+    assert dreason.cpu().numpy().tolist() == again.tolist()
+    assert (again != 0).sum() >= n - len(bad)
 
 
 def test_empty_batches_are_no_ops(gpu_ctx):

@@ -335,6 +335,31 @@ def test_thread_lines_equal_engine_lines():
     assert np.array_equal(thr == 0, expect)
 
 
+def test_engine_without_idle_lanes_equals_default():
+    """The Miller loop and the Karabina FE segments on 16-group 192-thread
+    blocks (k_eng_miller_xw, k_eng_fe_seg_xw: groups 5 and 10 span two waves,
+    sub-ops ordered by barriers, the verdict vote through LDS) against the
+    five-group wave kernels: 20,011 rounds (a ragged last block of 11 items,
+    and a chunk count that is not a multiple of 16), 1% corrupted, on two
+    engine chunk sizes, and with the Karabina fallback forced on every 7th
+    item (its list names 5-round blocks once each) -- identical reasons,
+    equal to the construction."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 20011
+    c = make_chain(27, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 27, rate=1e-2)
+    ref = _verify_with_env(c, {"DGPU_ENG_XW": "0"})
+    miller = _verify_with_env(c, {"DGPU_ENG_XW": "1"})
+    xw = _verify_with_env(c, {"DGPU_ENG_XW": "3"})
+    xw_small = _verify_with_env(c, {"DGPU_ENG_XW": "3", "DGPU_ENG_CHUNK": "4099"})
+    xw_fb = _verify_with_env(c, {"DGPU_ENG_XW": "3", "DGPU_KB_TEST_FLAG": "7"})
+    assert xw.tolist() == ref.tolist() == miller.tolist() == xw_small.tolist() == xw_fb.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(xw == 0, expect)
+
+
 def test_two_lane_per_round_large_chain():
     """A batch spanning two engine chunks runs on two lanes (streams, half the
     batch each, capi.hip verify_status_locked), its host records staged slice

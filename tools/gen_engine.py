@@ -1169,11 +1169,30 @@ def sub_shape(sub):
     return nt, ntmin, xf, np_, kind, lin32, consts, has_dst, has_exp
 
 
+def sub_in_place(op, si):
+    """Sub-op si writes a slot (output or fused-epilogue sum) that some lane
+    of the same sub-op reads.  Within one wave all lanes read before any
+    writes; when a group spans waves (XW kernels, engine.cuh eng_sync) such a
+    sub-op needs a barrier between its reads and its writes."""
+    sub = op.subs[si]
+    reads = set()
+    for r in sub:
+        for a, b, _, _ in r.terms:
+            reads |= {a, b}
+        for sl, _ in r.post:
+            reads.add(sl)
+    writes = {r.dst for r in sub if r.dst is not None}
+    writes |= {f[0] for f in op.fuse.get(si, []) if f is not None}
+    return bool(reads & writes)
+
+
 def emit_compiled(ops, sub_tab, path):
     idx = {op.name: i for i, op in enumerate(ops)}
     out = ["// GENERATED by tools/gen_engine.py -- do not edit.",
            "// Straight-line forms of the hot engine ops (engine.cuh eng_sub_c): each",
            "// sub-op's shape fixed at compile time, the records and sums the interpreter's.",
+           "// XW: the group's lanes span waves (engine.cuh eng_sync: a barrier between an",
+           "// in-place sub-op's reads and its writes, and after every sub-op's writes).",
            "// Included by engine.cuh inside namespace dgpu.",
            "#pragma once", ""]
     s_index = 0
@@ -1183,7 +1202,7 @@ def emit_compiled(ops, sub_tab, path):
         s_index += len(op.subs)
     for name, fam in COMPILED.items():
         op = ops[idx[name]]
-        out.append("template <class Sink>")
+        out.append("template <bool XW, class Sink>")
         out.append(f"__device__ __forceinline__ void eng_op_c_{name}(uint32_t* g, const uint32_t* c, int k, Sink&& sink) {{")
         for si, sub in enumerate(op.subs):
             nt, ntmin, xf, np_, kind, lin32, consts, has_dst, has_exp = sub_shape(sub)
@@ -1194,7 +1213,7 @@ def emit_compiled(ops, sub_tab, path):
             out.append(f"    const fp o = eng_sub_c<{nt}, {ntmin}, 0x{xf:x}u, {np_}, {kind}, {str(lin32).lower()}, "
                        f"{str(consts).lower()}>(g, c, rec);")
             out.append("    const uint32_t h0 = rec[0];")
-            out.append("    asm volatile(\"\" ::: \"memory\");")
+            out.append(f"    eng_sync<XW && {str(sub_in_place(op, si)).lower()}>();")
             if has_dst:
                 out.append("    if ((h0 & 0xFFu) != 0xFFu) eng_st(g + (h0 & 0xFFu) * ENG_SLOT_WORDS, o);")
             if has_exp:
@@ -1202,17 +1221,17 @@ def emit_compiled(ops, sub_tab, path):
             fz = (ntw >> 21) & 0xFF
             if fz:
                 out.append(f"    eng_fuse_epilogue(g, o, ENG_FUSE_TAB[{fz - 1}][k], k);")
-            out.append("    asm volatile(\"\" ::: \"memory\");")
+            out.append("    eng_sync<XW>();")
             out.append("  }")
         out.append("}")
         out.append("")
     for fam in range(3):
-        out.append("template <class Sink>")
+        out.append("template <bool XW, class Sink>")
         out.append(f"__device__ __forceinline__ bool eng_run_c{fam}(int op, uint32_t* g, const uint32_t* c, int k, Sink&& sink) {{")
         out.append("  switch (op) {")
         for name, f in COMPILED.items():
             if f == fam:
-                out.append(f"    case OP_{name}: eng_op_c_{name}(g, c, k, sink); return true;")
+                out.append(f"    case OP_{name}: eng_op_c_{name}<XW>(g, c, k, sink); return true;")
         out.append("    default: return false;")
         out.append("  }")
         out.append("}")
@@ -1388,6 +1407,23 @@ def emit(path):
     for s in segs:
         offs.append(offs[-1] + len(s))
     lines.append(f"constexpr int ENG_PROG_FEK_OFF[{len(offs)}] = {{{', '.join(map(str, offs))}}};")
+    # group slots each segment touches (ops' records and fused-epilogue sums,
+    # LD12 / ST12 planes): the segments between the chains need fewer than the
+    # FE's maximum, so their XW kernel fits more blocks per CU
+    def op_slots(op):
+        m = nslots[op.name]
+        for lanes in op.fuse.values():
+            m = max([m] + [f[0] + 1 for f in lanes if f is not None])
+        return m
+    seg_slots = []
+    for seg in prog_fe_kb():
+        m = 0
+        for ins in seg:
+            m = max(m, op_slots(ops[op_index[ins[1]]]) if ins[0] == "run" else ins[1] + LANES)
+        seg_slots.append(m)
+    assert max(seg_slots) <= nsl["FE"], (seg_slots, nsl["FE"])
+    lines.append(f"constexpr int ENG_FEK_MID_SLOTS = {max(seg_slots[1:-1])};  // segments 1 .. 4 (per segment: "
+                 f"{', '.join(map(str, seg_slots))})")
     allk = [w for s in segs for w in s]
     lines.append(f"ENG_TABLE_QUAL uint32_t ENG_PROG_FEK[{len(allk)}] = {{")
     for i in range(0, len(allk), 12):

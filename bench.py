@@ -660,9 +660,14 @@ def verify_leg(args, world, rank, local, scheme, n_total, steps, warmup, mode="p
         e2e_steps = max(1, min(steps, 2))
         t_host, _ = timed(step_host, e2e_steps, world, dev)
         host_ok = np.unpackbits(h_bits, bitorder="little")[:n].astype(bool)
+        st_ms, st_bytes = _lib.staging_stats(ctx)
         res["end_to_end"] = {"value": n_total * e2e_steps / t_host, "unit": "rounds/s",
                              "ms_per_step": t_host / e2e_steps * 1e3, "steps": e2e_steps,
-                             "api": "dgpu_verify_beacons (pageable host records: H2D, verify, D2H)",
+                             "api": "dgpu_verify_beacons (pageable caller records through the library's pinned ring, "
+                                    "slice by slice beside the verification; verdicts D2H)",
+                             "staging": {"ms": round(st_ms, 2), "bytes": st_bytes,
+                                         "GB_per_s": round(st_bytes / max(st_ms, 1e-6) / 1e6, 2)},
+                             "vs_resident": (n_total * e2e_steps / t_host) / res["value"] if res.get("value") else None,
                              "verdicts_equal_device_path": bool(np.array_equal(host_ok, verdicts[lo:hi]))}
 
     # configs[2] beside the metric: RLC batch verification (one multi-Miller
@@ -723,6 +728,27 @@ def abi_devices(args, ngpu):
     return list(range(ngpu))
 
 
+def multi_staging(mctx, ndev):
+    """Per device of a dgpu_verify_multi handle: the last call's host-record
+    staging through that context's pinned ring (dgpu_staging_stats: span on
+    its copy stream, bytes) -- the concurrent H2D of every shard from one
+    process, which the per-GPU compute has to hide."""
+    from drand_amd import _lib
+
+    class _C:  # a device context of the handle, as _lib.staging_stats takes it
+        pass
+    out = []
+    for k in range(ndev):
+        h = ctypes.c_void_p()
+        _lib.check(mctx.lib.dgpu_multi_context(mctx.handle, k, ctypes.byref(h)))
+        c = _C()
+        c.lib, c.handle = mctx.lib, h
+        ms, nb = _lib.staging_stats(c)
+        out.append({"ms": round(ms, 2), "bytes": nb, "GB_per_s": round(nb / max(ms, 1e-6) / 1e6, 2)})
+    return {"per_device": out, "max_ms": max(d["ms"] for d in out),
+            "note": "span on each context's copy stream, first ring piece to last DMA of its shard"}
+
+
 def main_abi(args):
     """One process drives every GPU through the C ABI as a Go caller of
     crypto/gpu would: dgpu_verify_multi over host records
@@ -780,7 +806,8 @@ def main_abi(args):
                "rounds_total": n_total, "verdict_mismatches": int(((reason == 0) != expect).sum()),
                "chain_gen_s": t_gen, "scheme": args.scheme, "mode": args.mode,
                "workload": "dgpu_verify_multi over host records (per-device H2D staging, verify, RCCL verdict "
-                           "all-gather, D2H)"}
+                           "all-gather, D2H)",
+               "staging": multi_staging(mctx, len(devs))}
     res.update({"n_gpus": len(devs), "devices": devs, "steps": args.steps, "warmup": args.warmup,
                 "driver": "abi (one process, libdrand_gpu.so multi-GPU handle)",
                 "gather": "in-library device copies (DGPU_MULTI_ALLOW_SAME_DEVICE)" if os.environ.get(

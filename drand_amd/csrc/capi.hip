@@ -936,7 +936,8 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
     }
     mark(c, s, "eng_fe");
     const int so = ENG_PROG_FEK_OFF[seg], sl = ENG_PROG_FEK_OFF[seg + 1] - ENG_PROG_FEK_OFF[seg];
-    if ((c->eng_xw & 2) && seg > 0 && seg < nseg - 1)
+#ifdef DG_AB_KNOBS
+    if ((c->eng_xw & 2) && seg > 0 && seg < nseg - 1)  // measured slower too (r06d)
       hipLaunchKernelGGL(k_eng_fe_seg_xw<ENG_FEK_MID_SLOTS>, dim3(grid_for(cnt, ENG_XW_ITEMS)), dim3(ENG_XW_BLOCK), 0, s,
                          so, sl, false, false, cnt, r0, consts, (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
     else if (c->eng_xw & 2)
@@ -944,6 +945,7 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
                          so, sl, seg == 0, seg == nseg - 1, cnt, r0, consts, (const uint32_t*)f, n1inv, xbuf, flags, fb,
                          st);
     else
+#endif
       hipLaunchKernelGGL(k_eng_fe_seg, dim3(blocks), dim3(ENG_BLOCK), 0, s, so, sl, seg == 0, seg == nseg - 1, cnt, r0,
                          consts, (const uint32_t*)f, n1inv, xbuf, flags, fb, st);
     HIP_TRY(hipGetLastError());
@@ -1031,10 +1033,12 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
       }
       HIP_TRY(hipGetLastError());
       mark(c, s, "eng_miller");
-      if (c->eng_xw & 1)
+#ifdef DG_AB_KNOBS
+      if (c->eng_xw & 1)  // no idle lanes, barrier-ordered: measured 8% slower (profiles/r06/r06d_engine_xw_ab.txt)
         hipLaunchKernelGGL(k_eng_miller_xw, dim3(grid_for(cnt, ENG_XW_ITEMS)), dim3(ENG_XW_BLOCK), 0, s, cnt, consts,
                            lines, f, n1);
       else
+#endif
         hipLaunchKernelGGL(k_eng_miller, dim3(blocks), dim3(ENG_BLOCK), 0, s, cnt, consts, lines, f, n1);
       HIP_TRY(hipGetLastError());
     }
@@ -1097,6 +1101,13 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
                             (const uint32_t*)key->table.p);
 }
 
+// host-record staging (verify_status_host_locked): the kernels of a slice
+// wait for its records
+struct host_stager;
+int stager_wait_msg(host_stager* stg, size_t k, hipStream_t s);
+int stager_wait_sig(host_stager* stg, size_t k, hipStream_t s);
+int stager_wait_all(host_stager* stg, hipStream_t s);
+
 // Per-round G2 path, first half of one lane: hash-to-G2 (field, SSWU, finish),
 // batch affine, signature decode of `n` items into the lane's buffers.
 // s_dec (optional): the signature decode runs on that stream, beside the hash
@@ -1107,7 +1118,8 @@ int verify_g1_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a, ui
 // (pairing_engine.cuh k_cof_*) instead of k_h2c_finish.
 int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src& m, const uint8_t* sigs,
                         size_t sig_stride, const uint32_t* sig_len, uint8_t* st, hipStream_t s,
-                        hipStream_t s_dec = nullptr, const uint32_t* consts = nullptr) {
+                        hipStream_t s_dec = nullptr, const uint32_t* consts = nullptr, host_stager* stg = nullptr,
+                        size_t slice = 0) {
   const unsigned B = 256;
   int rc;
   if ((rc = L.h_pts->ensure(n * G2A_WORDS * 4)) || (rc = L.sig_pts->ensure(n * G2A_WORDS * 4)) ||
@@ -1137,6 +1149,7 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   if (s_dec) {  // first in the second stream's queue: it runs beside the whole hash chain
     HIP_TRY(hipEventRecord(c->lane_ev[0], s));
     HIP_TRY(hipStreamWaitEvent(s_dec, c->lane_ev[0], 0));
+    if ((rc = stager_wait_sig(stg, slice, s_dec))) return rc;  // host records: the slice's signatures on the device
     HIP_TRY(decode(s_dec));
     HIP_TRY(hipEventRecord(c->lane_ev[1], s_dec));
   }
@@ -1192,6 +1205,7 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
     join.release();
   } else {
     mark(c, s, "decode_g2");
+    if ((rc = stager_wait_sig(stg, slice, s))) return rc;
     HIP_TRY(decode(s));
   }
   return DGPU_OK;
@@ -1244,9 +1258,6 @@ size_t lane_slice_len(const dgpu_ctx* c, const verify_args& a) {
              : std::max<size_t>(n, 1);
 }
 
-struct host_stager;
-int stager_wait(host_stager* stg, size_t k, hipStream_t s);
-int stager_wait_all(host_stager* stg, hipStream_t s);
 
 // Everything up to the per-item status (ST_*): G1 or G2 signatures, per-round
 // or RLC.  Asynchronous on s (RLC descent synchronizes between its levels).
@@ -1296,8 +1307,8 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   // the decode's ~0.9 ms leaves the critical path; DGPU_DEC_OVERLAP=0 off)
   // (DGPU_LANES=1 keeps the whole call on one stream: no decode beside the hash either)
   const hipStream_t s_dec = (!two && c->lanes > 1 && c->dec_overlap && !c->profile) ? c->stream2 : nullptr;
-  if ((rc = stager_wait(stg, 0, s)) ||
-      (rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec, consts)))
+  if ((rc = stager_wait_msg(stg, 0, s)) ||
+      (rc = g2_lane_hash_locked(c, L0, n0, a.m, a.sigs, a.sig_stride, a.sig_len, st, s, s_dec, consts, stg, 0)))
     return rc;
   const bool sub = !c->decode_subgroup;
   if (!two)
@@ -1318,8 +1329,9 @@ int verify_status_locked(dgpu_ctx* c, const key_entry* key, const verify_args& a
   for (size_t off = n0; off < n; off += n0, ++k) {
     const size_t nk = std::min(n0, n - off);
     const int ln = (int)(k & 1);
-    if ((rc = stager_wait(stg, k, ss[ln])) || (rc = g2_lane_hash_locked(c, *LL[ln], nk, src_slice(a.m, off), a.sigs + off * a.sig_stride, a.sig_stride,
-                                  a.sig_len + off, st + off, ss[ln])))
+    if ((rc = stager_wait_msg(stg, k, ss[ln])) ||
+        (rc = g2_lane_hash_locked(c, *LL[ln], nk, src_slice(a.m, off), a.sigs + off * a.sig_stride, a.sig_stride,
+                                  a.sig_len + off, st + off, ss[ln], nullptr, nullptr, stg, k)))
       return rc;
     if ((rc = eng_pairing_locked(c, consts, nk, (const uint32_t*)LL[ln]->h_pts->p,
                                  (const uint32_t*)LL[ln]->sig_pts->p, st + off, ss[ln], 0, nullptr, nullptr, nullptr,
@@ -1504,19 +1516,26 @@ int ring_ensure_locked(dgpu_ctx* c) {
 
 // One call's staging: the device buffers for all n records are allocated up
 // front (a's pointers rewritten to them); a host thread fills slice after
-// slice through the ring and records an event per slice on the copy stream;
-// wait(k, s) makes stream s wait for slice k (the host first waits until the
-// thread has enqueued it).  The destructor joins the thread: nothing of the
-// call's host buffers is read after the entry point returns.
+// slice through the ring.  A slice's message part (rounds, previous
+// signatures, or raw messages) goes first -- the hash chain's first kernel
+// reads only that -- and its signatures after (the decode runs after the
+// hash), each part ending in an event on the copy stream: the first kernel
+// waits for half the slice's bytes.  The thread also checks each slice's
+// record lengths against their strides (a bad record fails the call with
+// DGPU_EINVAL, as before, without a serial pass over the batch in front of
+// the first kernel).  wait_msg / wait_sig (k, s) make stream s wait for a
+// part (the host first waits until the thread has enqueued it).  The
+// destructor joins the thread: nothing of the call's host buffers is read
+// after the entry point returns.
 struct host_stager {
   dgpu_ctx* c;
   verify_args host;               // the caller's pointers
   std::vector<size_t> lo;         // slice k = [lo[k], lo[k + 1])
-  std::vector<hipEvent_t> ev;
+  std::vector<hipEvent_t> ev_msg, ev_sig;
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;
-  size_t staged = 0;
+  size_t staged_msg = 0, staged = 0;  // parts enqueued (message parts, whole slices)
   int rc = DGPU_OK;
   std::string err;
   std::atomic<bool> cancel{false};
@@ -1535,40 +1554,59 @@ struct host_stager {
       c->last_stage_ms = ms;
       c->last_stage_bytes = bytes;
     }
-    for (hipEvent_t e : ev)
-      if (e) (void)hipEventDestroy(e);
+    for (auto* v : {&ev_msg, &ev_sig})
+      for (hipEvent_t e : *v)
+        if (e) (void)hipEventDestroy(e);
     if (t0) (void)hipEventDestroy(t0);
     if (t1) (void)hipEventDestroy(t1);
   }
   int make_events(size_t slices) {
-    ev.assign(slices, nullptr);
-    for (hipEvent_t& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto* v : {&ev_msg, &ev_sig}) {
+      v->assign(slices, nullptr);
+      for (hipEvent_t& e : *v) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     HIP_TRY(hipEventCreate(&t0));
     HIP_TRY(hipEventCreate(&t1));
     return DGPU_OK;
   }
-  // items [lo[k], lo[k + 1]) of every record array of `host` into `dev`
-  int stage_slice(const verify_args& dev, size_t a, size_t b) {
+  // the message arrays of items [a, b) (checked against their stride), then
+  // its signature arrays; an event after each part
+  int stage_slice(const verify_args& dev, size_t k, size_t a, size_t b) {
     const msg_src& m = host.m;
     const size_t n = b - a;
-    bytes += n * (host.sig_stride + 4 + (m.msgs ? m.msg_stride + 4 : 8 + (m.chained ? m.prev_stride + 4 : 0)));
     int r;
-    if ((r = ring_copy_locked(c, (uint8_t*)dev.sigs + a * host.sig_stride, host.sigs + a * host.sig_stride,
-                              n * host.sig_stride)) ||
-        (r = ring_copy_locked(c, (uint32_t*)dev.sig_len + a, host.sig_len + a, n * 4)))
-      return r;
     if (m.msgs) {
+      for (size_t i = a; i < b; ++i)
+        if (m.msg_len[i] > m.msg_stride) return set_err(DGPU_EINVAL, "msg_len[%zu]=%u > msg_stride", i, m.msg_len[i]);
       if ((r = ring_copy_locked(c, (uint8_t*)dev.m.msgs + a * m.msg_stride, m.msgs + a * m.msg_stride,
                                 n * m.msg_stride)) ||
           (r = ring_copy_locked(c, (uint32_t*)dev.m.msg_len + a, m.msg_len + a, n * 4)))
         return r;
-      return DGPU_OK;
+      bytes += n * (m.msg_stride + 4);
+    } else {
+      if (m.chained)
+        for (size_t i = a; i < b; ++i)
+          if (m.prev_len[i] > m.prev_stride)
+            return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, m.prev_len[i]);
+      if ((r = ring_copy_locked(c, (uint64_t*)dev.m.rounds + a, m.rounds + a, n * 8))) return r;
+      if (m.chained && ((r = ring_copy_locked(c, (uint8_t*)dev.m.prev + a * m.prev_stride, m.prev + a * m.prev_stride,
+                                              n * m.prev_stride)) ||
+                        (r = ring_copy_locked(c, (uint32_t*)dev.m.prev_len + a, m.prev_len + a, n * 4))))
+        return r;
+      bytes += n * (8 + (m.chained ? m.prev_stride + 4 : 0));
     }
-    if ((r = ring_copy_locked(c, (uint64_t*)dev.m.rounds + a, m.rounds + a, n * 8))) return r;
-    if (m.chained && ((r = ring_copy_locked(c, (uint8_t*)dev.m.prev + a * m.prev_stride, m.prev + a * m.prev_stride,
-                                            n * m.prev_stride)) ||
-                      (r = ring_copy_locked(c, (uint32_t*)dev.m.prev_len + a, m.prev_len + a, n * 4))))
+    HIP_TRY(hipEventRecord(ev_msg[k], c->stream_copy));
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      staged_msg = k + 1;
+    }
+    cv.notify_all();
+    if ((r = ring_copy_locked(c, (uint8_t*)dev.sigs + a * host.sig_stride, host.sigs + a * host.sig_stride,
+                              n * host.sig_stride)) ||
+        (r = ring_copy_locked(c, (uint32_t*)dev.sig_len + a, host.sig_len + a, n * 4)))
       return r;
+    bytes += n * (host.sig_stride + 4);
+    HIP_TRY(hipEventRecord(ev_sig[k], c->stream_copy));
     return DGPU_OK;
   }
   void start(const verify_args& dev) {
@@ -1576,14 +1614,13 @@ struct host_stager {
       (void)hipSetDevice(c->device);
       (void)hipEventRecord(t0, c->stream_copy);
       for (size_t k = 0; k + 1 < lo.size(); ++k) {
-        int r = cancel ? DGPU_EINVAL : stage_slice(dev, lo[k], lo[k + 1]);
-        if (!r && hipEventRecord(ev[k], c->stream_copy) != hipSuccess) r = set_err(DGPU_EDEVICE, "hipEventRecord");
+        int r = cancel ? set_err(DGPU_EINVAL, "staging cancelled") : stage_slice(dev, k, lo[k], lo[k + 1]);
         if (!r && k + 2 == lo.size() && hipEventRecord(t1, c->stream_copy) != hipSuccess)
           r = set_err(DGPU_EDEVICE, "hipEventRecord");
         std::lock_guard<std::mutex> lk(mu);
         if (r) {
           rc = r;
-          err = cancel ? std::string("staging cancelled") : g_last_error;
+          err = g_last_error;
         } else {
           staged = k + 1;
         }
@@ -1592,21 +1629,22 @@ struct host_stager {
       }
     });
   }
-  int wait(size_t k, hipStream_t s) {
+  int wait_part(size_t k, hipStream_t s, bool sig) {
     std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return staged > k || rc != DGPU_OK; });
-    if (staged <= k) return set_err(rc, "%s", err.c_str());
-    HIP_TRY(hipStreamWaitEvent(s, ev[k], 0));
+    cv.wait(lk, [&] { return (sig ? staged : staged_msg) > k || rc != DGPU_OK; });
+    if ((sig ? staged : staged_msg) <= k) return set_err(rc, "%s", err.c_str());
+    HIP_TRY(hipStreamWaitEvent(s, (sig ? ev_sig : ev_msg)[k], 0));
     return DGPU_OK;
   }
-  int wait_all(hipStream_t s) { return lo.size() > 1 ? wait(lo.size() - 2, s) : DGPU_OK; }
+  int wait_all(hipStream_t s) { return lo.size() > 1 ? wait_part(lo.size() - 2, s, true) : DGPU_OK; }
 };
 
-int stager_wait(host_stager* stg, size_t k, hipStream_t s) { return stg ? stg->wait(k, s) : DGPU_OK; }
+int stager_wait_msg(host_stager* stg, size_t k, hipStream_t s) { return stg ? stg->wait_part(k, s, false) : DGPU_OK; }
+int stager_wait_sig(host_stager* stg, size_t k, hipStream_t s) { return stg ? stg->wait_part(k, s, true) : DGPU_OK; }
 int stager_wait_all(host_stager* stg, hipStream_t s) { return stg ? stg->wait_all(s) : DGPU_OK; }
 
-// Checks of the host records and the device buffers of a staged call; a's
-// pointers become the device copies' (their contents arrive slice by slice).
+// The device buffers of a staged call; a's pointers become the device
+// copies' (their contents arrive slice by slice).
 int stage_prepare_locked(dgpu_ctx* c, verify_args& a) {
   const size_t n = a.n;
   int rc;
@@ -1616,8 +1654,6 @@ int stage_prepare_locked(dgpu_ctx* c, verify_args& a) {
   a.sig_len = (const uint32_t*)c->in_sig_len.p;
   msg_src& m = a.m;
   if (m.msgs) {
-    for (size_t i = 0; i < n; ++i)
-      if (m.msg_len[i] > m.msg_stride) return set_err(DGPU_EINVAL, "msg_len[%zu]=%u > msg_stride", i, m.msg_len[i]);
     if ((rc = c->in_msgs.ensure(n * m.msg_stride + 1)) || (rc = c->in_msg_len.ensure(n * 4))) return rc;
     m.msgs = (const uint8_t*)c->in_msgs.p;
     m.msg_len = (const uint32_t*)c->in_msg_len.p;
@@ -1626,8 +1662,6 @@ int stage_prepare_locked(dgpu_ctx* c, verify_args& a) {
   if ((rc = c->in_rounds.ensure(n * 8))) return rc;
   m.rounds = (const uint64_t*)c->in_rounds.p;
   if (m.chained) {
-    for (size_t i = 0; i < n; ++i)
-      if (m.prev_len[i] > m.prev_stride) return set_err(DGPU_EINVAL, "prev_len[%zu]=%u > prev_stride", i, m.prev_len[i]);
     if ((rc = c->in_prev.ensure(n * m.prev_stride + 1)) || (rc = c->in_prev_len.ensure(n * 4))) return rc;
     m.prev = (const uint8_t*)c->in_prev.p;
     m.prev_len = (const uint32_t*)c->in_prev_len.p;

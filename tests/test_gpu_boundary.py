@@ -505,6 +505,20 @@ def test_host_records_staged_through_the_ring(n, scheme, gpu_ctx):
         c.sigs[:] = keep
     assert dreason.cpu().numpy().tolist() == again.tolist()
     assert (again != 0).sum() >= n - len(bad)
+    if code == _lib.SCHEME_CHAINED:
+        # a record longer than its stride, in the first and in the last slice:
+        # the staging thread finds it and the call fails with DGPU_EINVAL; the
+        # context serves the next call
+        for i in (2, n - 3):
+            old = int(c.prev_len[i])
+            c.prev_len[i] = c.prev.shape[1] + 1
+            try:
+                with pytest.raises(_lib.DrandGPUError) as e:
+                    host_call()
+                assert e.value.code == _lib.DGPU_EINVAL and f"prev_len[{i}]" in str(e.value)
+            finally:
+                c.prev_len[i] = old
+        assert host_call().tolist() == got.tolist()
 
 
 def test_empty_batches_are_no_ops(gpu_ctx):

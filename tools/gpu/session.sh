@@ -15,6 +15,9 @@
 #   pmc        the SQ/TCC counter passes of tools/pmc.sh over prof_verify -> pmc/
 #   ab         bench each library in $VARIANTS (DRAND_GPU_LIB) with $BENCH_ARGS -> ab/<name>.json
 #   small      the small-batch latency curve (bench.py --small-batch-only) -> small.json
+#   abi8       the 8-GPU host side rehearsed on one GPU: dgpu_verify_multi over 8
+#              loopback contexts of device 0 (10M rounds, 1.25M per shard), with
+#              each shard's staging time through its context's pinned ring -> abi8.json
 export TMPDIR=/tmp
 TAG=${TAG:-session}
 O=gpurun_out/$TAG
@@ -63,6 +66,10 @@ run_step() {
   small)
     timeout -k 10 600 python -u bench.py --small-batch-only > $O/small.json 2> $O/small.err
     rc=$?; cat $O/small.json; return $rc ;;
+  abi8)
+    DGPU_MULTI_ALLOW_SAME_DEVICE=1 DGPU_ENG_CHUNK=131072 timeout -k 10 600 python -u bench.py --driver abi --gpus 8 \
+      --abi-devices 0,0,0,0,0,0,0,0 --steps ${ABI8_STEPS:-2} --warmup 1 > $O/abi8.json 2> $O/abi8.err
+    rc=$?; head -c 600 $O/abi8.json; echo; return $rc ;;
   *) echo "unknown step $1"; return 2 ;;
   esac
 }

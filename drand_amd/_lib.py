@@ -18,7 +18,7 @@ AB_LIB_PATH = os.path.join(_HERE, "libdrand_gpu_ab.so")
 AB_KNOBS = frozenset({"DGPU_DEC_OVERLAP", "DGPU_MSM_SEG", "DGPU_LANE_SLICES", "DGPU_KB_NORM", "DGPU_RLC_DESCENT_STEP",
                       "DGPU_RLC_LOCALIZE", "DGPU_G1_LINES", "DGPU_SUBGROUP", "DGPU_RECOVER", "DGPU_RECOVER_ROWS",
                       "DGPU_KB_INV_CHAIN", "DGPU_KB_TEST_FLAG", "DGPU_TEST_ALLOC_CAP", "DGPU_STAGE",
-                      "DGPU_ENG_XW"})
+                      "DGPU_ENG_XW", "DGPU_TEST_STAGE_ONLY"})
 
 DGPU_OK = 0
 DGPU_EINVAL = -1
@@ -56,7 +56,7 @@ SYMBOLS = [
     ("dgpu_verify_batch_device", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P, _c.c_size_t,
                                             _P, _c.c_int, _c.c_uint64, _P, _P, _P]),
     ("dgpu_set_profiling", _c.c_int, [_P, _c.c_int]),
-    ("dgpu_staging_stats", _c.c_int, [_P, _c.POINTER(_c.c_double), _c.POINTER(_c.c_uint64)]),
+    ("dgpu_staging_stats", _c.c_int, [_P, _c.POINTER(_c.c_double), _c.POINTER(_c.c_double), _c.POINTER(_c.c_uint64)]),
     ("dgpu_synchronize", _c.c_int, [_P]),
     ("dgpu_stage_times", _c.c_int, [_P, _c.POINTER(_c.c_float), _c.c_int, _c.POINTER(_c.c_char_p)]),
     ("dgpu_digest_batch", _c.c_int, [_P, _c.c_int, _c.c_size_t, _P, _P, _c.c_size_t, _P, _P]),
@@ -153,10 +153,11 @@ def stage_times(ctx):
 
 
 def staging_stats(ctx):
-    """dgpu_staging_stats: (ms, bytes) of the context's last host-record staging."""
-    ms, nb = ctypes.c_double(), ctypes.c_uint64()
-    check(ctx.lib.dgpu_staging_stats(ctx.handle, ctypes.byref(ms), ctypes.byref(nb)), ctx.lib)
-    return ms.value, nb.value
+    """dgpu_staging_stats: (device_ms, host_ms, bytes) of the context's last
+    host-record staging."""
+    ms, hms, nb = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+    check(ctx.lib.dgpu_staging_stats(ctx.handle, ctypes.byref(ms), ctypes.byref(hms), ctypes.byref(nb)), ctx.lib)
+    return ms.value, hms.value, nb.value
 
 
 def shard_range(n, ndev, k):

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <cstdarg>
@@ -255,6 +256,8 @@ struct dgpu_ctx {
   int ring_next = 0;
   hipStream_t stream_copy = nullptr;
   float last_stage_ms = 0.f;      // the last host-record call's staging span (dgpu_staging_stats)
+  double last_stage_host_ms = 0.0;
+  bool test_stage_only = false;   // A/B build, DGPU_TEST_STAGE_ONLY=1: host-record calls stage and stop (staging rehearsal)
   size_t last_stage_bytes = 0;
   int eng_xw = 0;                // 16-group 192-thread engine blocks (no idle lanes): bit 0 the Miller loop
                                  // (k_eng_miller_xw), bit 1 the FE segments (k_eng_fe_seg_xw); A/B: DGPU_ENG_XW
@@ -1541,6 +1544,7 @@ struct host_stager {
   std::atomic<bool> cancel{false};
   hipEvent_t t0 = nullptr, t1 = nullptr;  // copy-stream span of the staging (dgpu_staging_stats)
   size_t bytes = 0;
+  double host_ms = 0.0;                    // the thread's wall time, first memcpy to last DMA enqueued
 
   host_stager(dgpu_ctx* c_, const verify_args& h) : c(c_), host(h) {}
   ~host_stager() {
@@ -1552,6 +1556,7 @@ struct host_stager {
     float ms = 0.f;
     if (ok && rc == DGPU_OK && hipEventSynchronize(t1) == hipSuccess && hipEventElapsedTime(&ms, t0, t1) == hipSuccess) {
       c->last_stage_ms = ms;
+      c->last_stage_host_ms = host_ms;
       c->last_stage_bytes = bytes;
     }
     for (auto* v : {&ev_msg, &ev_sig})
@@ -1612,11 +1617,14 @@ struct host_stager {
   void start(const verify_args& dev) {
     th = std::thread([this, dev] {
       (void)hipSetDevice(c->device);
+      const auto w0 = std::chrono::steady_clock::now();
       (void)hipEventRecord(t0, c->stream_copy);
       for (size_t k = 0; k + 1 < lo.size(); ++k) {
         int r = cancel ? set_err(DGPU_EINVAL, "staging cancelled") : stage_slice(dev, k, lo[k], lo[k + 1]);
         if (!r && k + 2 == lo.size() && hipEventRecord(t1, c->stream_copy) != hipSuccess)
           r = set_err(DGPU_EDEVICE, "hipEventRecord");
+        if (k + 2 == lo.size())
+          host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
         std::lock_guard<std::mutex> lk(mu);
         if (r) {
           rc = r;
@@ -1683,6 +1691,9 @@ int verify_status_host_locked(dgpu_ctx* c, const key_entry* key, verify_args& a,
   stg.lo.push_back(a.n);
   if ((rc = stg.make_events(stg.lo.size() - 1))) return rc;
   stg.start(a);
+#ifdef DG_AB_KNOBS
+  if (c->test_stage_only) return stg.wait_all(s);  // staging rehearsal: no verification (statuses undefined)
+#endif
   rc = verify_status_locked(c, key, a, s, &stg);
   if (!rc) rc = stg.wait_all(s);  // every slice consumed (no-op when the pipeline waited for each)
   return rc;
@@ -1846,6 +1857,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (xwv) c->eng_xw = atoi(xwv) & 3;
   const char* stv = getenv("DGPU_STAGE");
   if (stv && !strcmp(stv, "pageable")) c->stage_pageable = true;
+  const char* tso = getenv("DGPU_TEST_STAGE_ONLY");
+  if (tso && !strcmp(tso, "1")) c->test_stage_only = true;
   const char* tac = getenv("DGPU_TEST_ALLOC_CAP");
   if (tac && atol(tac) >= 0) g_test_alloc_cap = (size_t)atol(tac);
 #endif
@@ -2089,10 +2102,11 @@ int dgpu_synchronize(dgpu_ctx* c) {
   return DGPU_OK;
 }
 
-int dgpu_staging_stats(dgpu_ctx* c, double* ms, uint64_t* bytes) {
-  if (!c || !ms || !bytes) return set_err(DGPU_EINVAL, "null argument");
+int dgpu_staging_stats(dgpu_ctx* c, double* device_ms, double* host_ms, uint64_t* bytes) {
+  if (!c || !device_ms || !host_ms || !bytes) return set_err(DGPU_EINVAL, "null argument");
   std::lock_guard<std::mutex> lk(c->mu);
-  *ms = c->last_stage_ms;
+  *device_ms = c->last_stage_ms;
+  *host_ms = c->last_stage_host_ms;
   *bytes = c->last_stage_bytes;
   return DGPU_OK;
 }

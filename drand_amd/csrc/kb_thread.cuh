@@ -40,6 +40,22 @@ DG_FN fp2 kb_t_cross(const fp2& ss, const fp2& xx, const fp2& yy) {  // ss - xx 
   return fp2{fp_norm(fp_sub2_lz(ss.c0, fp_add_lz(xx.c0, yy.c0))), fp_norm(fp_sub2_lz(ss.c1, fp_add_lz(xx.c1, yy.c1)))};
 }
 
+// xi (2 f2 f5) = xi ((f2 + f5)^2 - f2^2 - f5^2) straight from the six product
+// components (each < 1.01p, normalized), without reducing 2 f2 f5 first:
+//   re = s.re + c2.im + c5.im - s.im - (c2.re + c5.re),
+//   im = s.re + s.im - (c2.re + c5.re) - (c2.im + c5.im)
+// with the subtrahends as 8p - x and 32p - (x + y) (fp_sub_lz, fp_sub2_lz):
+// limbs < 3 (2^28) + 2^29 + 0x30000000 < 2^31, and 2 (2^28) + 2 x 0x30000000
+// < 2^31; carried, < 43.1p and < 66.1p.  kb_t_out then triples them (< 2^30.3
+// per limb after the carry) and adds 2 f1: < 133p and < 203p, inside
+// fp_reduce's < 2^392.  Two reductions fewer per compressed squaring than
+// reducing 2 f2 f5 before the twist.
+DG_FN fp2 kb_t_xi_cross(const fp2& s, const fp2& c2, const fp2& c5) {
+  const fp re = fp_sub2_lz(fp_sub_lz(fp_add_lz(fp_add_lz(s.c0, c2.c1), c5.c1), s.c1), fp_add_lz(c2.c0, c5.c0));
+  const fp im = fp_sub2_lz(fp_sub2_lz(fp_add_lz(s.c0, s.c1), fp_add_lz(c2.c0, c5.c0)), fp_add_lz(c2.c1, c5.c1));
+  return fp2{fp_norm(re), fp_norm(im)};
+}
+
 DG_FN void kb_sqr_thr(fp2& f1, fp2& f2, fp2& f4, fp2& f5) {
   // C side: f1' and f4' (they need the old f1, f4, which the B side squares)
   fp2 n1, n4;
@@ -48,9 +64,13 @@ DG_FN void kb_sqr_thr(fp2& f1, fp2& f2, fp2& f4, fp2& f5) {
     const fp2 c25 = fp2_sqr(fp2_carry(fp2_add_lz(f2, f5)));
     const fp2 q = kb_t_qsum(c2, c5);
     n4 = fp2{kb_t_out(q.c0, f4.c0, true), kb_t_out(q.c1, f4.c1, true)};
+#ifdef DG_KB_XI_REDUCED  // A/B: 2 f2 f5 reduced before the twist (rounds 3-5)
     const fp2 x = kb_t_cross(c25, c2, c5);
     const fp2 xr{fp_reduce(x.c0), fp_reduce(x.c1)};
     const fp2 xx{fp_norm(fp_sub_lz(xr.c0, xr.c1)), fp_norm(fp_add_lz(xr.c0, xr.c1))};  // xi (2 f2 f5)
+#else
+    const fp2 xx = kb_t_xi_cross(c25, c2, c5);
+#endif
     n1 = fp2{kb_t_out(xx.c0, f1.c0, false), kb_t_out(xx.c1, f1.c1, false)};
   }
   // B side: f2' and f5'

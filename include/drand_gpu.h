@@ -250,9 +250,11 @@ int dgpu_set_profiling(dgpu_ctx *ctx, int enable);
  * dgpu_verify_multi): the records go through a library-owned pinned ring
  * (two 16 MiB slots per context, filled by host threads, DMA'd on the
  * context's copy stream) slice by slice, each slice's kernels starting when
- * its records have arrived.  ms = the staging's span on the copy stream,
- * first piece to last DMA (device timeline); bytes = record bytes staged. */
-int dgpu_staging_stats(dgpu_ctx *ctx, double *ms, uint64_t *bytes);
+ * its records have arrived.  device_ms = the staging's span on the copy
+ * stream, first piece to last DMA (device timeline); host_ms = the staging
+ * thread's wall time, first memcpy into the ring to the last DMA enqueued;
+ * bytes = record bytes staged. */
+int dgpu_staging_stats(dgpu_ctx *ctx, double *device_ms, double *host_ms, uint64_t *bytes);
 int dgpu_stage_times(dgpu_ctx *ctx, float *ms_out, int max_stages, const char **names_out);
 
 /* Batch DigestMessage (chain/verify.go:24-32): out32 = n x 32 bytes. */

@@ -473,9 +473,9 @@ def test_host_records_staged_through_the_ring(n, scheme, gpu_ctx):
         return reason
 
     got = host_call()
-    ms, nbytes = _lib.staging_stats(gpu_ctx)
+    ms, host_ms, nbytes = _lib.staging_stats(gpu_ctx)
     per = c.sigs.shape[1] + 4 + 8 + ((c.prev.shape[1] + 4) if code == _lib.SCHEME_CHAINED else 0)
-    assert nbytes == n * per and ms > 0
+    assert nbytes == n * per and ms > 0 and host_ms > 0
     dev = {k: torch.from_numpy(np.ascontiguousarray(getattr(c, k))).cuda()
            for k in ("rounds", "sigs", "sig_len", "prev", "prev_len")}
     dbits = torch.zeros((n + 7) // 8, dtype=torch.uint8, device="cuda")

@@ -259,6 +259,7 @@ struct dgpu_ctx {
   double last_stage_host_ms = 0.0;
   bool test_stage_only = false;   // A/B build, DGPU_TEST_STAGE_ONLY=1: host-record calls stage and stop (staging rehearsal)
   size_t last_stage_bytes = 0;
+  bool lines_wave = true;        // k_lines_thr with a pair per wave (G1 point in SGPRs; A/B: DGPU_LINES_WAVE=0)
   int eng_xw = 0;                // 16-group 192-thread engine blocks (no idle lanes): bit 0 the Miller loop
                                  // (k_eng_miller_xw), bit 1 the FE segments (k_eng_fe_seg_xw); A/B: DGPU_ENG_XW
   bool stage_pageable = false;   // A/B build, DGPU_STAGE=pageable: the round-5 whole-batch pageable copy
@@ -1027,9 +1028,13 @@ int eng_pairing_locked(dgpu_ctx* c, const uint32_t* consts, size_t n, const uint
                            fixed_table, lines);
       } else {
         mark(c, s, "eng_lines");
-        if (c->lines_thread && cnt >= c->thr_min)
-          hipLaunchKernelGGL(k_lines_thr, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, n, r0, cnt, h, h_stride, h_idx,
-                             sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
+        if (c->lines_thread && cnt >= c->thr_min && !pk_items && c->lines_wave)  // pair per wave: P in SGPRs
+          hipLaunchKernelGGL(k_lines_thr<true>, dim3(grid_for(2 * ((cnt + 63) / 64 * 64), 256)), dim3(256), 0, s, n, r0,
+                             cnt, h, h_stride, h_idx, sg, pk_items, consts, lines,
+                             sig_subgroup ? st : (uint8_t*)nullptr);
+        else if (c->lines_thread && cnt >= c->thr_min)
+          hipLaunchKernelGGL(k_lines_thr<false>, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, n, r0, cnt, h, h_stride,
+                             h_idx, sg, pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr);
         else
           hipLaunchKernelGGL(k_eng_lines, dim3(blocks), dim3(ENG_BLOCK), 0, s, n, r0, cnt, h, h_stride, h_idx, sg,
                            pk_items, consts, lines, sig_subgroup ? st : (uint8_t*)nullptr, (uint32_t*)nullptr);
@@ -1853,6 +1858,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
   const char* ktf = getenv("DGPU_KB_TEST_FLAG");
   if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
+  const char* lwv = getenv("DGPU_LINES_WAVE");
+  if (lwv && !strcmp(lwv, "0")) c->lines_wave = false;
   const char* xwv = getenv("DGPU_ENG_XW");
   if (xwv) c->eng_xw = atoi(xwv) & 3;
   const char* stv = getenv("DGPU_STAGE");

@@ -169,6 +169,12 @@ namespace dgpu {
 // k_eng_lines (pairing_engine.cuh); consts: the engine constant block (pair
 // points (-x, y) in slots ENG_C_NXP0..ENG_C_YP1).  Each step's 6 exports of
 // the pair are 6 consecutive words per limb plane, written as 3 dwordx2.
+// WAVE (no per-item keys, pk_items == nullptr): a wave holds 64 rounds of one
+// pair (waves alternate between the pairs) instead of 32 rounds of both, so
+// the pair's G1 point -- the key or -g1, the same for every lane -- is
+// wave-uniform and lives in scalar registers (readfirstlane), off the T-step
+// loop's VGPR budget.
+template <bool WAVE>
 __global__ void __launch_bounds__(256, DG_LINES_OCC) k_lines_thr(size_t n, size_t r0, size_t cnt,
                                                                  const uint32_t* __restrict__ h_pts, size_t h_stride,
                                                                  const uint32_t* __restrict__ h_idx,
@@ -178,8 +184,8 @@ __global__ void __launch_bounds__(256, DG_LINES_OCC) k_lines_thr(size_t n, size_
                                                                  uint32_t* __restrict__ lines,
                                                                  uint8_t* __restrict__ status) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t i = t >> 1;
-  const int p = (int)(t & 1);
+  const size_t i = WAVE ? ((t >> 7) << 6) + (t & 63) : t >> 1;
+  const int p = WAVE ? (int)((t >> 6) & 1) : (int)(t & 1);
   if (i >= cnt) return;
   const size_t r = r0 + i;
   const uint32_t* qb = p ? sig_pts : h_pts;
@@ -235,7 +241,14 @@ __global__ void __launch_bounds__(256, DG_LINES_OCC) k_lines_thr(size_t n, size_
 #else
   lt_pt_val P;
 #pragma unroll
-  for (int l = 0; l < FP_LIMBS; ++l) P.nx_.l[l] = pt[l * stride], P.y_.l[l] = pt[ystep + l * stride];
+  for (int l = 0; l < FP_LIMBS; ++l) {
+    if constexpr (WAVE) {  // uniform: scalar registers
+      P.nx_.l[l] = __builtin_amdgcn_readfirstlane(pt[l * stride]);
+      P.y_.l[l] = __builtin_amdgcn_readfirstlane(pt[ystep + l * stride]);
+    } else {
+      P.nx_.l[l] = pt[l * stride], P.y_.l[l] = pt[ystep + l * stride];
+    }
+  }
 #endif
   const g2p T = lt_pair_p(Qs, P, [&](int step, int k, const fp2& v) {
     uint2* b = reinterpret_cast<uint2*>(base + (size_t)step * FP_LIMBS * ENG_WAVE_WORDS) + k;

@@ -259,7 +259,8 @@ struct dgpu_ctx {
   double last_stage_host_ms = 0.0;
   bool test_stage_only = false;   // A/B build, DGPU_TEST_STAGE_ONLY=1: host-record calls stage and stop (staging rehearsal)
   size_t last_stage_bytes = 0;
-  bool lines_wave = true;        // k_lines_thr with a pair per wave (G1 point in SGPRs; A/B: DGPU_LINES_WAVE=0)
+  bool lines_wave = false;       // A/B: DGPU_LINES_WAVE=1, k_lines_thr with a pair per wave (G1 point in SGPRs;
+                                 // spills 280 -> 226 but 1.5% slower, r06f)
   int eng_xw = 0;                // 16-group 192-thread engine blocks (no idle lanes): bit 0 the Miller loop
                                  // (k_eng_miller_xw), bit 1 the FE segments (k_eng_fe_seg_xw); A/B: DGPU_ENG_XW
   bool stage_pageable = false;   // A/B build, DGPU_STAGE=pageable: the round-5 whole-batch pageable copy
@@ -1200,7 +1201,7 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
     if (side) HIP_TRY(hipStreamWaitEvent(s, c->cof_ev[1], 0));
     hipLaunchKernelGGL(k_cof_final, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)w, h, (uint32_t*)L.h_z->p);
   } else {
-    hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, h,
+    hipLaunchKernelGGL(k_h2c_finish, dim3(grid_for(n, B)), dim3(B), 0, s, n, q, h,
                        (uint32_t*)L.h_z->p);
   }
   HIP_TRY(hipGetLastError());
@@ -1859,7 +1860,7 @@ int dgpu_open(int device, dgpu_ctx** out) {
   const char* ktf = getenv("DGPU_KB_TEST_FLAG");
   if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
   const char* lwv = getenv("DGPU_LINES_WAVE");
-  if (lwv && !strcmp(lwv, "0")) c->lines_wave = false;
+  if (lwv) c->lines_wave = !strcmp(lwv, "1");
   const char* xwv = getenv("DGPU_ENG_XW");
   if (xwv) c->eng_xw = atoi(xwv) & 3;
   const char* stv = getenv("DGPU_STAGE");

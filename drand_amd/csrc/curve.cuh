@@ -318,6 +318,99 @@ DG_FN bool g2_on_curve_affine(const g2a& a) {
   return fp2_eq(fp2_sqr(a.y), rhs);
 }
 
+// add-2007-bl for operands that are neither equal, opposite nor the identity:
+// g2_add_body without its exceptional branches (whose out-of-line g2_dbl call
+// is a call site in the caller's loop); `exc` is set when one of those cases
+// arises, and the caller redoes the whole computation on the generic path.
+// The second operand comes through `q` (q.x(), q.y(), q.z()), each coordinate
+// fetched where it is used -- from HBM in the cofactor ladders -- and the
+// products ordered so p's coordinates die early: at most six Fp2 values live.
+// Z3 = 2 Z1 Z2 H (the same value as ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H), 2 Z1Z2
+// lazy into fp2_mul (limbs < 2^29).
+template <class Q>
+DG_FN g2j g2_add_nx_q(const g2j& p, const Q& q, bool& exc) {
+  fp2 u1, s1, z1z2;
+  {
+    const fp2 qz = q.z();
+    exc = exc || fp2_is_zero(qz);
+    const fp2 z2z2 = fp2_sqr(qz);
+    u1 = fp2_mul(p.x, z2z2);
+    s1 = fp2_mul(fp2_mul(p.y, qz), z2z2);
+    z1z2 = fp2_mul(p.z, qz);
+  }
+  fp2 h, rh;
+  {
+    const fp2 z1z1 = fp2_sqr(p.z);
+    h = fp2_sub(fp2_mul(q.x(), z1z1), u1);
+    rh = fp2_sub(fp2_mul(fp2_mul(q.y(), p.z), z1z1), s1);
+  }
+  exc = exc || g2_is_inf(p) || fp2_is_zero(h);
+  g2j r;
+  r.z = fp2_mul(fp2_add_lz(z1z2, z1z2), h);
+  const fp2 rr = fp2_carry(fp2_add_lz(rh, rh));
+  const fp2 i = fp2_sqr(fp2_carry(fp2_add_lz(h, h)));
+  const fp2 j = fp2_mul(h, i);
+  const fp2 v = fp2_mul(u1, i);
+  r.x = fp2_sub32(fp2_sqr(rr), fp2_carry(fp2_add_lz(fp2_add_lz(j, v), v)));
+  const fp2 VX = fp2_carry(fp2{fp_sub_lz(v.c0, r.x.c0), fp_sub_lz(v.c1, r.x.c1)});
+  r.y = fp2_sub(fp2_mul(rr, VX), fp2_mul(fp2_add_lz(s1, s1), j));
+  return r;
+}
+struct g2j_q {  // an in-register second operand
+  const g2j& p;
+  DG_FN fp2 x() const { return p.x; }
+  DG_FN fp2 y() const { return p.y; }
+  DG_FN fp2 z() const { return p.z; }
+};
+DG_FN g2j g2_add_nx(const g2j& p, const g2j& q, bool& exc) { return g2_add_nx_q(p, g2j_q{q}, exc); }
+DG_FN g2j g2_psi_body(const g2j& p) {
+  return g2j{fp2_mul(fp2_conj(p.x), C_PSI_CX), fp2_mul(fp2_conj(p.y), C_PSI_CY), fp2_conj(p.z)};
+}
+DG_FN g2j g2_psi2_body(const g2j& p) {
+  return g2j{fp2_mul_fp(p.x, fp2(C_PSI2_CX).c0), fp2_mul_fp(p.y, fp2(C_PSI2_CY).c0), p.z};
+}
+
+// [|x|] of the point in stash slot k, |x| = 0xd201000000010000 (bits 63, 62,
+// 60, 57, 48, 16): runs of 1, 2, 3, 9 and 32 doublings, each closed by an
+// addition of the point reloaded from the slot, then 16 doublings -- only the
+// accumulator lives across the loops.
+template <class Stash>
+DG_FN g2j g2_mul_absx_stash(Stash& st, int k, bool& exc) {
+  g2j r = st.get(k);
+#pragma unroll 1
+  for (int a = 0; a < 5; ++a) {
+    const int nd = a == 0 ? 1 : a == 1 ? 2 : a == 2 ? 3 : a == 3 ? 9 : 32;
+#pragma unroll 1
+    for (int d = 0; d < nd; ++d) r = g2_dbl_body(r);
+    r = g2_add_nx_q(r, st.at(k), exc);
+  }
+#pragma unroll 1
+  for (int d = 0; d < 16; ++d) r = g2_dbl_body(r);
+  return r;
+}
+
+// h_eff (Q0 + Q1) in the order of g2_clear_cofactor (RFC 9380 G.3) with the
+// cold operands parked in three point slots of `st` (k_h2c_finish: the
+// round's own SoA slots in HBM) so the two [|x|] ladders hold one point each:
+//   slot 0: P = Q0 + Q1 (generic addition);  slot 1: R = psi^2(2P) - psi(P) - P,
+//   then R - [x]P;  slot 2: U = [x]P + psi(P);  result R + [x]U.
+// exc: an exceptional addition arose on the fast path (the caller recomputes
+// with g2_clear_cofactor).
+template <class Stash>
+DG_FN g2j g2_clear_cofactor_stash(const g2j& q0, const g2j& q1, Stash& st, bool& exc) {
+  {
+    const g2j P = g2_add_body(q0, q1);
+    st.put(0, P);
+    const g2j t = g2_add_nx(g2_psi2_body(g2_dbl_body(P)), g2_neg(g2_psi_body(P)), exc);
+    st.put(1, g2_add_nx(t, g2_neg(P), exc));
+  }
+  const g2j nA = g2_mul_absx_stash(st, 0, exc);  // -[x]P
+  st.put(2, g2_add_nx(g2_neg(nA), g2_psi_body(st.get(0)), exc));
+  st.put(1, g2_add_nx(st.get(1), nA, exc));
+  const g2j nB = g2_mul_absx_stash(st, 2, exc);  // -[x]U
+  return g2_add_nx(st.get(1), g2_neg(nB), exc);
+}
+
 // Clear cofactor with the whole computation inlined (k_h2c_finish).
 DG_FN g2j g2_clear_cofactor_inl(const g2j& p) {
   g2j t1 = g2_neg(g2_mul_absx_inl(p));

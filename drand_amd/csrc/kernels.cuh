@@ -147,14 +147,73 @@ __global__ void __launch_bounds__(256, DG_SSWU_OCC) k_h2c_sswu(size_t n, const u
   st_g2j(q_out + which * G2J_WORDS * n, n, i, map_to_curve_sswu_iso3_body(uu));
 }
 
-__global__ void __launch_bounds__(256, DG_FINISH_OCC) k_h2c_finish(size_t n, const uint32_t* __restrict__ q,
+// Point slots of g2_clear_cofactor_stash in the round's own SoA words: 0, 1 =
+// the two SSWU outputs' slots of q (each read once, before it is written),
+// 2 = the output slot (X, Y in h_out, Z in z_out).
+struct h2c_finish_stash {
+  uint32_t* q;
+  uint32_t* h_out;
+  uint32_t* z_out;
+  size_t n, i;
+  __device__ __forceinline__ void put(int k, const g2j& p) {
+    if (k < 2) {
+      st_g2j(q + (size_t)k * G2J_WORDS * n, n, i, p);
+    } else {
+      st_g2a(h_out, n, i, g2a{p.x, p.y});
+      st_fp(z_out, n, i, p.z.c0);
+      st_fp(z_out + FP_WORDS * n, n, i, p.z.c1);
+    }
+  }
+  struct fetch {  // slot k's coordinates, each loaded where g2_add_nx_q uses it
+    const uint32_t* xy;
+    const uint32_t* zp;
+    size_t n, i;
+    __device__ __forceinline__ fp2 x() const { return fp2{ld_fp(xy, n, i), ld_fp(xy + FP_WORDS * n, n, i)}; }
+    __device__ __forceinline__ fp2 y() const {
+      return fp2{ld_fp(xy + 2 * FP_WORDS * n, n, i), ld_fp(xy + 3 * FP_WORDS * n, n, i)};
+    }
+    __device__ __forceinline__ fp2 z() const { return fp2{ld_fp(zp, n, i), ld_fp(zp + FP_WORDS * n, n, i)}; }
+  };
+  // (the bases pass through an empty asm: the slot is re-read at each
+  // addition instead of hoisted out of the ladder and spilled)
+  __device__ __forceinline__ fetch at(int k) const {
+    const uint32_t* qb = q;
+    const uint32_t* hb = h_out;
+    const uint32_t* zb = z_out;
+#ifdef __HIP_DEVICE_COMPILE__
+    __asm__ volatile("" : "+s"(qb), "+s"(hb), "+s"(zb));
+#endif
+    const uint32_t* xy = k < 2 ? qb + (size_t)k * G2J_WORDS * n : hb;
+    return fetch{xy, k < 2 ? xy + 4 * FP_WORDS * n : zb, n, i};
+  }
+  __device__ __forceinline__ g2j get(int k) const {
+    if (k < 2) return ld_g2j(q + (size_t)k * G2J_WORDS * n, n, i);
+    const g2a a = ld_g2a(h_out, n, i);
+    return g2j{a.x, a.y, fp2{ld_fp(z_out, n, i), ld_fp(z_out + FP_WORDS * n, n, i)}};
+  }
+};
+
+// Q0 + Q1 and the cofactor clearing, its cold points parked in HBM (one
+// point live per [|x|] ladder, no call sites in the loops; VERDICT r05 item
+// 3).  An exceptional addition on the fast path (Q0 = +-Q1, a small-order
+// point, ...) redoes the round with the generic g2_clear_cofactor from P,
+// which slot 0 still holds.  Overwrites q.
+__global__ void __launch_bounds__(256, DG_FINISH_OCC) k_h2c_finish(size_t n, uint32_t* __restrict__ q,
                                                      uint32_t* __restrict__ h_out, uint32_t* __restrict__ z_out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const g2j h = g2_clear_cofactor_inl(g2_add_body(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i)));
-  st_g2a(h_out, n, i, g2a{h.x, h.y});
-  st_fp(z_out, n, i, h.z.c0);
-  st_fp(z_out + FP_WORDS * n, n, i, h.z.c1);
+#ifdef DG_FINISH_INL  // A/B: rounds 1-5, the whole ladder in registers (4 KB of scratch per lane)
+  const g2j hh = g2_clear_cofactor_inl(g2_add_body(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i)));
+  st_g2a(h_out, n, i, g2a{hh.x, hh.y});
+  st_fp(z_out, n, i, hh.z.c0);
+  st_fp(z_out + FP_WORDS * n, n, i, hh.z.c1);
+  return;
+#endif
+  h2c_finish_stash st{q, h_out, z_out, n, i};
+  bool exc = false;
+  g2j h = g2_clear_cofactor_stash(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i), st, exc);
+  if (exc) h = g2_clear_cofactor(st.get(0));
+  st.put(2, h);
 }
 
 // RLC mode's pre-cofactor hash point R = Q0 + Q1 (Jacobian, [6 fp][n]) from

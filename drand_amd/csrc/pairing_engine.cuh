@@ -652,7 +652,7 @@ __global__ void __launch_bounds__(256, 2) k_eng_kb_norm(size_t cnt, size_t r0, c
 
 // Decompression, one thread per stored value j of item i (element e = j cnt
 // + i): 1 / N_j = E_j / P (ebuf, pbuf after k_eng_inv), then f0 and f3 of
-// plane X0 + j (engine.cuh eng_kb_decompress).  Flagged items are skipped.
+// plane X0 + j (engine.cuh ENG_KB_DECOMPRESS).  Flagged items are skipped.
 // 2 waves/SIMD (13 spilled VGPRs) measured faster than 1 (r03k: the FE's
 // inversion + decompression stages 47.3 vs 60.9 ms per 2M rounds).
 #ifndef DG_KB_DEC_OCC
@@ -669,7 +669,7 @@ __global__ void __launch_bounds__(256, DG_KB_DEC_OCC) k_eng_kb_dec(size_t cnt, u
   const int pl = ENG_KB_PL_X0 + (int)j;
   const fp ninv = fp_mul(ld_soa(pbuf, cnt, i), ld_soa(ebuf + j * FP_LIMBS * cnt, cnt, i));
   fp2 f0, f3;
-  eng_kb_decompress(kb_ld2(xbuf, i, pl, 2), kb_ld2(xbuf, i, pl, 4), kb_ld2(xbuf, i, pl, 8), kb_ld2(xbuf, i, pl, 10),
+  ENG_KB_DECOMPRESS(kb_ld2(xbuf, i, pl, 2), kb_ld2(xbuf, i, pl, 4), kb_ld2(xbuf, i, pl, 8), kb_ld2(xbuf, i, pl, 10),
                     ninv, f0, f3);
   kb_st2(xbuf, i, pl, 0, f0);
   kb_st2(xbuf, i, pl, 6, f3);

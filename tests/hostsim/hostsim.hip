@@ -21,6 +21,14 @@ unsigned long long dg_count_mul = 0, dg_count_sqr = 0;
 static void fp_to_be(const fp& a, uint8_t* out) { fp_std_to_be48(fp_from_mont(a), out); }
 static fp fp_from_be(const uint8_t* in) { return fp_to_mont(fp_std_from_be48(in)); }
 
+// k_h2c_finish's point slots (kernels.cuh h2c_finish_stash) in host memory
+struct hs_stash {
+  g2j s[3];
+  void put(int k, const g2j& p) { s[k] = p; }
+  g2j get(int k) const { return s[k]; }
+  g2j_q at(int k) const { return g2j_q{s[k]}; }
+};
+
 extern "C" {
 
 // per-stage Fp mul/sqr counts of one per-round verification (DG_COUNT_OPS builds)
@@ -99,7 +107,9 @@ int hs_count_kernels(const uint8_t* prev, uint32_t prev_len, uint64_t round, con
   const g2j q0 = map_to_curve_sswu_iso3_body(u0), q1 = map_to_curve_sswu_iso3_body(u1);
   out[2] = dg_count_mul; out[3] = dg_count_sqr;
   dg_count_mul = dg_count_sqr = 0;
-  const g2j h = g2_clear_cofactor_inl(g2_add_body(q0, q1));
+  hs_stash st;
+  bool exc = false;
+  const g2j h = g2_clear_cofactor_stash(q0, q1, st, exc);
   out[4] = dg_count_mul; out[5] = dg_count_sqr;
   dg_count_mul = dg_count_sqr = 0;
   g2a s;
@@ -367,6 +377,32 @@ void hs_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {
   bool inf = g2_is_inf(h);
   g2a a = inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h);
   g2_compress(out96, a, inf);
+}
+
+// k_h2c_finish's sequence (g2_clear_cofactor_stash, the generic
+// g2_clear_cofactor from slot 0 when it flags an exceptional addition) on
+// Q0, Q1 = SSWU(u0), SSWU(u1) of msg, with Q1 replaced by Q0 (mode 1) or -Q0
+// (mode 2, P = O) -- H compressed to out96 (the generic path's to gen96);
+// returns the exceptional flag.
+int hs_h2c_finish_check(const uint8_t* msg32, int mode, uint8_t* out96, uint8_t* gen96) {
+  uint32_t m[8];
+  msg_words(msg32, m);
+  fp2 u0, u1;
+  hash_to_field_g2(u0, u1, m);
+  const g2j q0 = map_to_curve_sswu_iso3_body(u0);
+  g2j q1 = map_to_curve_sswu_iso3_body(u1);
+  if (mode == 1) q1 = q0;
+  if (mode == 2) q1 = g2_neg(q0);
+  hs_stash st;
+  bool exc = false;
+  g2j h = g2_clear_cofactor_stash(q0, q1, st, exc);
+  if (exc) h = g2_clear_cofactor(st.get(0));
+  const g2j g = g2_clear_cofactor(g2_add(q0, q1));
+  bool inf = g2_is_inf(h);
+  g2_compress(out96, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h), inf);
+  inf = g2_is_inf(g);
+  g2_compress(gen96, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(g), inf);
+  return exc ? 1 : 0;
 }
 
 int hs_decompress_g2(const uint8_t* in96, uint8_t* recompressed) {
@@ -734,7 +770,7 @@ bool host_fe_kb(HostGroup& G, const fp f[12], const fp& n1inv) {
       const fp nrm = eng_kb_norm(fp2{x[2], x[3]});
       if (fp_is_zero(nrm)) return false;
       fp2 f0, f3;
-      eng_kb_decompress(fp2{x[2], x[3]}, fp2{x[4], x[5]}, fp2{x[8], x[9]}, fp2{x[10], x[11]}, fp_inv(nrm), f0, f3);
+      ENG_KB_DECOMPRESS(fp2{x[2], x[3]}, fp2{x[4], x[5]}, fp2{x[8], x[9]}, fp2{x[10], x[11]}, fp_inv(nrm), f0, f3);
       x[0] = f0.c0, x[1] = f0.c1, x[6] = f3.c0, x[7] = f3.c1;
     }
     host_scramble(G, 0x9E3779B9ull * (uint64_t)e + 1);
@@ -979,3 +1015,41 @@ extern "C" void hs_eng_cof_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {
   g2_compress(out96, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h), inf);
 }
 
+// engine.cuh eng_kb_decompress_lz (lazy linear steps, what k_eng_kb_dec runs)
+// == eng_kb_decompress (every step reduced) on n random CI inputs -- values
+// up to the CI bound 2.01p, where the lazy bounds are tightest -- and on the
+// all-maximal-limb input; returns the number of disagreements (outputs
+// compared mod p and checked CI: normalized limbs, < 2.01p).
+extern "C" int hs_kb_dec_lz_check(int n, uint64_t seed) {
+  uint64_t s = seed | 1;
+  auto rnd = [&]() {
+    fp x;
+    for (int i = 0; i < FP_LIMBS; ++i) {
+      s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+      x.l[i] = (uint32_t)s & FP_MASK;
+    }
+    x.l[FP_LIMBS - 1] &= 0x3FFFFFu;  // up to ~2.46p, reduced to CI (< 2.01p)
+    return fp_reduce(x);
+  };
+  auto ci = [](const fp& v) {  // normalized, value < 2.01p (top limb below 2.01 x p's)
+    for (int i = 0; i < FP_LIMBS - 1; ++i)
+      if (v.l[i] > FP_MASK) return false;
+    return v.l[FP_LIMBS - 1] <= (uint32_t)(2.01 * (double)FP_P[FP_LIMBS - 1]);
+  };
+  fp mx;
+  for (int i = 0; i < FP_LIMBS; ++i) mx.l[i] = FP_MASK;
+  mx.l[FP_LIMBS - 1] = 0x3FFFFFu;
+  mx = fp_reduce(mx);
+  int bad = 0;
+  for (int t = 0; t <= n; ++t) {
+    const bool edge = t == n;
+    const fp2 f1 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()}, f2 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()};
+    const fp2 f4 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()}, f5 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()};
+    const fp ninv = edge ? mx : rnd();
+    fp2 a0, a3, b0, b3;
+    eng_kb_decompress(f1, f2, f4, f5, ninv, a0, a3);
+    eng_kb_decompress_lz(f1, f2, f4, f5, ninv, b0, b3);
+    if (!fp2_eq(a0, b0) || !fp2_eq(a3, b3) || !ci(b0.c0) || !ci(b0.c1) || !ci(b3.c0) || !ci(b3.c1)) ++bad;
+  }
+  return bad;
+}

@@ -317,7 +317,8 @@ def test_karabina_fallback_on_natural_input():
 
 def test_thread_lines_equal_engine_lines():
     """The per-thread T-steps (k_lines_thr, default) against the 12-lane
-    engine's lines program (DGPU_LINES=engine): 20,011 rounds (ragged last
+    engine's lines program (DGPU_LINES=engine) and the pair-per-wave variant
+    (A/B build, DGPU_LINES_WAVE=1): 20,011 rounds (ragged last
     block), 1% corrupted -- identical reasons (x-bit flips that stay on the
     curve exercise the fused membership test: REASON_SUBGROUP from both),
     equal to the construction."""
@@ -328,7 +329,8 @@ def test_thread_lines_equal_engine_lines():
     bad = corrupt(c, 23, rate=1e-2)
     thr = _verify_with_env(c, {})
     eng = _verify_with_env(c, {"DGPU_LINES": "engine"})
-    assert thr.tolist() == eng.tolist()
+    wave = _verify_with_env(c, {"DGPU_LINES_WAVE": "1"})  # A/B: a pair per wave, P in SGPRs
+    assert thr.tolist() == eng.tolist() == wave.tolist()
     assert (thr == _lib.REASON_SUBGROUP).any()
     expect = np.ones(n, dtype=bool)
     expect[list(bad.keys())] = False

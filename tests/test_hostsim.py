@@ -99,6 +99,30 @@ def test_hash_to_g2_golden(hostsim):
         assert o.raw.hex() == c["h"]
 
 
+def test_h2c_finish_ladder_matches_generic(hostsim):
+    """k_h2c_finish's sequence (cold points parked in slots, fast additions
+    flagging the exceptional cases, the generic cofactor clearing as the
+    fallback) equals hash_to_g2 on the golden messages and on 32 random ones,
+    and on Q1 = Q0 (P = 2 Q0 via the generic first addition) and Q1 = -Q0
+    (P = O: every later addition is exceptional -> fallback, H = O)."""
+    import random
+    rng = random.Random(5)
+    msgs = [bytes.fromhex(c["msg"]) for c in load_golden("hash_to_g2.json")["cases"]]
+    msgs += [rng.randbytes(32) for _ in range(32)]
+    for msg in msgs:
+        for mode in (0, 1, 2):
+            o, g = buf(96), buf(96)
+            exc = hostsim.hs_h2c_finish_check(msg, mode, o, g)
+            assert o.raw == g.raw
+            assert exc == (1 if mode == 2 else 0)
+            if mode == 0:
+                h = buf(96)
+                hostsim.hs_hash_to_g2(msg, h)
+                assert o.raw == h.raw
+            if mode == 2:
+                assert o.raw[0] & 0x40  # the infinity flag
+
+
 def test_decompress_kat(hostsim):
     k = load_golden("kat_bls12381_compat_v112.json")
     o = buf(96)
@@ -361,6 +385,15 @@ def test_thread_lines_match_oracle_and_engine(hostsim):
             assert hostsim.hs_eng_subgroup(B.g2_compress(q)) == 0
     finally:
         hostsim.hs_eng_set_lines_thread(0)
+
+
+def test_kb_decompress_lazy_matches(hostsim):
+    # the decompression with lazy linear steps (what k_eng_kb_dec runs) ==
+    # the every-step-reduced form, outputs CI, on 2,000 random inputs up to the
+    # CI bound and the all-maximal-limb input
+    hostsim.hs_kb_dec_lz_check.restype = ctypes.c_int
+    hostsim.hs_kb_dec_lz_check.argtypes = [ctypes.c_int, ctypes.c_uint64]
+    assert hostsim.hs_kb_dec_lz_check(2000, 77) == 0
 
 
 def test_thread_kb_chain_matches_lane_chain(hostsim):

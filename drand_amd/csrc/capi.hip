@@ -505,6 +505,32 @@ inline rlc_geom rlc_geom_of(bool g1) { return g1 ? rlc_geom{true, G1A_WORDS, G1J
 // both groups' cofactors have small prime factors, so a small-order component
 // would survive a random 64-bit combination with noticeable probability).
 // Asynchronous on s.
+// The SSWU stage of the G2 hash over 2n field elements u -> Jacobian points
+// in q (k_h2c_sswu's contract): five launches with the two exponentiations
+// on their own high-occupancy kernel (kernels.cuh k_sswu_a); `aux` = six
+// free planes of FP_WORDS x n words (A/B build -DDG_SSWU_FUSED: the one
+// fused kernel, 2 waves per SIMD throughout).
+hipError_t launch_sswu(size_t n, const uint32_t* u, uint32_t* q, const sswu_planes& aux, hipStream_t s) {
+  const unsigned B = 256, g = grid_for(2 * n, B);
+#ifdef DG_SSWU_FUSED
+  (void)aux;
+  hipLaunchKernelGGL(k_h2c_sswu, dim3(g), dim3(B), 0, s, n, u, q);
+  return hipGetLastError();
+#else
+  hipLaunchKernelGGL(k_sswu_a, dim3(g), dim3(B), 0, s, n, u, q, aux);
+  hipLaunchKernelGGL(k_fp_pow_planes<0>, dim3(g), dim3(B), 0, s, n, aux, 0);
+  hipLaunchKernelGGL(k_sswu_b, dim3(g), dim3(B), 0, s, n, u, q, aux);
+  hipLaunchKernelGGL(k_fp_pow_planes<1>, dim3(g), dim3(B), 0, s, n, aux, 2);
+  hipLaunchKernelGGL(k_sswu_c, dim3(g), dim3(B), 0, s, n, u, q, aux);
+  return hipGetLastError();
+#endif
+}
+sswu_planes planes_of(uint32_t* base, size_t n) {  // six consecutive FP planes
+  sswu_planes a;
+  for (int k = 0; k < 6; ++k) a.p[k] = base + (size_t)k * FP_WORDS * n;
+  return a;
+}
+
 size_t rlc_tree_points(size_t n) {
   size_t total = 0;
   for (size_t v = n;; v = (v + 1) / 2) {
@@ -552,8 +578,7 @@ int rlc_points_locked(dgpu_ctx* c, const verify_args& a, hipStream_t s) {
     uint32_t* q = u + 4 * FP_WORDS * n;
     hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, a.m, u);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_sswu(n, u, q, planes_of(rpts, n), s));  // rpts is free until k_h2c_sum
     hipLaunchKernelGGL(k_h2c_sum, dim3(grid_for(n, B)), dim3(B), 0, s, n, (const uint32_t*)q, rpts);
     HIP_TRY(hipGetLastError());
   }
@@ -1165,8 +1190,12 @@ int g2_lane_hash_locked(dgpu_ctx* c, const lane_bufs& L, size_t n, const msg_src
   mark(c, s, "hash_to_g2");
   hipLaunchKernelGGL(k_h2c_field, dim3(grid_for(n, B)), dim3(B), 0, s, n, m, u);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_h2c_sswu, dim3(grid_for(2 * n, B)), dim3(B), 0, s, n, (const uint32_t*)u, q);
-  HIP_TRY(hipGetLastError());
+  {  // the SSWU's planes: h_pts and h_z, free until the cofactor step writes them
+    sswu_planes aux;
+    for (int k = 0; k < 4; ++k) aux.p[k] = h + (size_t)k * FP_WORDS * n;
+    for (int k = 0; k < 2; ++k) aux.p[4 + k] = (uint32_t*)L.h_z->p + (size_t)k * FP_WORDS * n;
+    HIP_TRY(launch_sswu(n, u, q, aux, s));
+  }
   if (cof_engine) {
     const unsigned blocks = cof_blocks;
     uint32_t* w = (uint32_t*)c->cof_tmp.p;

@@ -147,6 +147,73 @@ __global__ void __launch_bounds__(256, DG_SSWU_OCC) k_h2c_sswu(size_t n, const u
   st_g2j(q_out + which * G2J_WORDS * n, n, i, map_to_curve_sswu_iso3_body(uu));
 }
 
+// The SSWU stage in five launches (round 6): the two exponentiations of
+// each item (~85% of its products) run alone in k_fp_pow_planes, whose few
+// VGPRs let 8 waves share a SIMD, where the fused k_h2c_sswu holds 256 VGPRs
+// (2 waves) for its pre- and post-steps.  The out-of-line Fp calls issue
+// ~1.3x faster at 6-8 waves than at 2 (`tools/engbench/powprobe.hip`,
+// profiles/r06/r06h_powprobe.json).  Item j of 2n (which = j / n, i = j % n):
+//   k_sswu_a   u -> N, D, w into the item's q slot (x, y, z words), Norm(w) -> plane 3 which
+//   pow        plane 3 which: alpha -> g = alpha^((p+1)/4)
+//   k_sswu_b   square test (x2 if not), N, w updated in the slot; d -> plane 3 which + 1,
+//              dm4 -> plane 3 which + 2
+//   pow        plane 3 which + 2: dm4 -> t = dm4^((p-3)/4)
+//   k_sswu_c   y, sign, 3-isogeny -> the Jacobian point over the slot (k_h2c_sswu's output)
+// The arithmetic is map_to_curve_sswu_iso3_body's, stage by stage (h2c.cuh).
+struct sswu_planes {
+  uint32_t* p[6];  // [3 which + k]: FP_WORDS x n words each
+};
+__global__ void __launch_bounds__(256, 2) k_sswu_a(size_t n, const uint32_t* __restrict__ u, uint32_t* __restrict__ q,
+                                                sswu_planes aux) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const size_t which = j / n, i = j % n;
+  const uint32_t* ub = u + which * 2 * FP_WORDS * n;
+  fp2 N, D, w;
+  sswu_pre(fp2{ld_fp(ub, n, i), ld_fp(ub + FP_WORDS * n, n, i)}, N, D, w);
+  st_g2j(q + which * G2J_WORDS * n, n, i, g2j{N, D, w});
+  st_fp(aux.p[3 * which], n, i, fp2_norm(w));
+}
+template <int E>
+__global__ void __launch_bounds__(256) k_fp_pow_planes(size_t n, sswu_planes aux, int k) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const size_t which = j / n, i = j % n;
+  uint32_t* pl = aux.p[3 * which + k];
+  const fp a = ld_fp(pl, n, i);
+  st_fp(pl, n, i, E == 0 ? fp_sqrt_cand(a) : DG_POW(a, EXP_P_MINUS_3_DIV_4));
+}
+__global__ void __launch_bounds__(256, 2) k_sswu_b(size_t n, const uint32_t* __restrict__ u, uint32_t* __restrict__ q,
+                                                sswu_planes aux) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const size_t which = j / n, i = j % n;
+  const uint32_t* ub = u + which * 2 * FP_WORDS * n;
+  uint32_t* qs = q + which * G2J_WORDS * n;
+  const g2j s = ld_g2j(qs, n, i);
+  fp2 N = s.x, w = s.z;
+  fp dm4;
+  const fp d = sswu_mid(fp2{ld_fp(ub, n, i), ld_fp(ub + FP_WORDS * n, n, i)}, N, s.y, w,
+                        ld_fp(aux.p[3 * which], n, i), dm4);
+  st_g2j(qs, n, i, g2j{N, s.y, w});
+  st_fp(aux.p[3 * which + 1], n, i, d);
+  st_fp(aux.p[3 * which + 2], n, i, dm4);
+}
+__global__ void __launch_bounds__(256, DG_SSWU_OCC) k_sswu_c(size_t n, const uint32_t* __restrict__ u,
+                                                             uint32_t* __restrict__ q, sswu_planes aux) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const size_t which = j / n, i = j % n;
+  const uint32_t* ub = u + which * 2 * FP_WORDS * n;
+  uint32_t* qs = q + which * G2J_WORDS * n;
+  const g2j s = ld_g2j(qs, n, i);
+  const fp d = ld_fp(aux.p[3 * which + 1], n, i);
+  const fp m2 = fp_sqr(fp2_norm(s.y));  // dm4 = d Norm(D)^4 again, as fp2_sqrt_scaled_pre forms it
+  const fp dm4 = fp_mul(d, fp_sqr(m2));
+  st_g2j(qs, n, i, sswu_post(fp2{ld_fp(ub, n, i), ld_fp(ub + FP_WORDS * n, n, i)}, s.x, s.y, s.z, d, dm4,
+                             ld_fp(aux.p[3 * which + 2], n, i)));
+}
+
 // Point slots of g2_clear_cofactor_stash in the round's own SoA words: 0, 1 =
 // the two SSWU outputs' slots of q (each read once, before it is written),
 // 2 = the output slot (X, Y in h_out, Z in z_out).

@@ -100,16 +100,26 @@ DG_FN bool fp2_is_square(const fp2& a) { return fp_is_square(fp2_norm(a)); }
 // (or (w0 - g) / 2 when that is 0, i.e. w1 = 0) and t = (d m^4)^((p-3)/4):
 // d square -> d t + (w1 t / 2) u, else (w1 t / 2) - d t u.
 // Derivation and model: tools/sswu_model.py (sqrt_scaled).
-DG_NOINL fp2 fp2_sqrt_scaled(const fp2& w, const fp& g, const fp& m) {
+// fp2_sqrt_scaled in two halves around its exponentiation t = dm4^((p-3)/4)
+// (the staged SSWU runs that exponentiation as its own launch): _pre returns
+// d and dm4 = d m^4, _post the root from t.
+DG_FN fp fp2_sqrt_scaled_pre(const fp2& w, const fp& g, const fp& m, fp& dm4) {
   fp d = fp_half(fp_add(w.c0, g));
   d = fp_cmov(d, fp_half(fp_sub(w.c0, g)), fp_is_zero(d));
   const fp m2 = fp_sqr(m);
-  const fp dm4 = fp_mul(d, fp_sqr(m2));
-  const fp t = DG_POW(dm4, EXP_P_MINUS_3_DIV_4);
+  dm4 = fp_mul(d, fp_sqr(m2));
+  return d;
+}
+DG_FN fp2 fp2_sqrt_scaled_post(const fp2& w, const fp& d, const fp& dm4, const fp& t) {
   const bool sq = fp_eq(fp_mul(dm4, fp_sqr(t)), fp_one());
   const fp dt = fp_mul(d, t);
   const fp wt = fp_half(fp_mul(w.c1, t));
   return sq ? fp2{dt, wt} : fp2{wt, fp_neg(dt)};
+}
+DG_NOINL fp2 fp2_sqrt_scaled(const fp2& w, const fp& g, const fp& m) {
+  fp dm4;
+  const fp d = fp2_sqrt_scaled_pre(w, g, m, dm4);
+  return fp2_sqrt_scaled_post(w, d, dm4, DG_POW(dm4, EXP_P_MINUS_3_DIV_4));
 }
 
 // Square root in Fp2 (p = 3 mod 4) by the norm method in two exponentiations

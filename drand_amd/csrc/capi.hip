@@ -259,6 +259,7 @@ struct dgpu_ctx {
   double last_stage_host_ms = 0.0;
   bool test_stage_only = false;   // A/B build, DGPU_TEST_STAGE_ONLY=1: host-record calls stage and stop (staging rehearsal)
   size_t last_stage_bytes = 0;
+  bool kb_pair = false;          // A/B: DGPU_KB_PAIR=1, the Karabina chain on two lanes per round (k_kb_chain_pair)
   bool lines_wave = false;       // A/B: DGPU_LINES_WAVE=1, k_lines_thr with a pair per wave (G1 point in SGPRs;
                                  // spills 280 -> 226 but 1.5% slower, r06f)
   int eng_xw = 0;                // 16-group 192-thread engine blocks (no idle lanes): bit 0 the Miller loop
@@ -506,13 +507,13 @@ inline rlc_geom rlc_geom_of(bool g1) { return g1 ? rlc_geom{true, G1A_WORDS, G1J
 // would survive a random 64-bit combination with noticeable probability).
 // Asynchronous on s.
 // The SSWU stage of the G2 hash over 2n field elements u -> Jacobian points
-// in q (k_h2c_sswu's contract): five launches with the two exponentiations
-// on their own high-occupancy kernel (kernels.cuh k_sswu_a); `aux` = six
-// free planes of FP_WORDS x n words (A/B build -DDG_SSWU_FUSED: the one
-// fused kernel, 2 waves per SIMD throughout).
+// in q: the fused k_h2c_sswu.  A/B build -DDG_SSWU_STAGED: five launches with
+// the two exponentiations on their own 90-VGPR kernel (kernels.cuh k_sswu_a;
+// `aux` = six free planes of FP_WORDS x n words) -- measured slower (r06i:
+// hash 151.0 vs 148.0 ms per 2M, RLC raw hash 62.7 vs 60.0), not shipped.
 hipError_t launch_sswu(size_t n, const uint32_t* u, uint32_t* q, const sswu_planes& aux, hipStream_t s) {
   const unsigned B = 256, g = grid_for(2 * n, B);
-#ifdef DG_SSWU_FUSED
+#ifndef DG_SSWU_STAGED
   (void)aux;
   hipLaunchKernelGGL(k_h2c_sswu, dim3(g), dim3(B), 0, s, n, u, q);
   return hipGetLastError();
@@ -943,7 +944,9 @@ int eng_fe_kb_locked(dgpu_ctx* c, const uint32_t* consts, size_t cnt, size_t cap
       mark(c, s, "eng_fe_chain");
       const bool kb_thread = c->kb_thread && cnt >= c->thr_min;
       const bool norm_pre = kb_thread && c->kb_norm_chain;
-      if (norm_pre)
+      if (norm_pre && c->kb_pair)  // two lanes per round
+        hipLaunchKernelGGL(k_kb_chain_pair<true>, dim3(grid_for(2 * cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
+      else if (norm_pre)
         hipLaunchKernelGGL(k_kb_chain_thr<true>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, ebuf);
       else if (kb_thread)
         hipLaunchKernelGGL(k_kb_chain_thr<false>, dim3(grid_for(cnt, 256)), dim3(256), 0, s, cnt, xbuf, nullptr);
@@ -1888,6 +1891,8 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (kic && atol(kic) >= 1) c->kb_inv_chain = (size_t)atol(kic);
   const char* ktf = getenv("DGPU_KB_TEST_FLAG");
   if (ktf && atol(ktf) >= 1) c->kb_test_flag = (size_t)atol(ktf);
+  const char* kpv = getenv("DGPU_KB_PAIR");
+  if (kpv) c->kb_pair = !strcmp(kpv, "1");
   const char* lwv = getenv("DGPU_LINES_WAVE");
   if (lwv) c->lines_wave = !strcmp(lwv, "1");
   const char* xwv = getenv("DGPU_ENG_XW");

@@ -84,6 +84,32 @@ DG_FN void kb_sqr_thr(fp2& f1, fp2& f2, fp2& f4, fp2& f5) {
   f4 = n4;
 }
 
+// The same squaring split over two lanes (k_kb_chain_pair): the B lane holds
+// (x, y) = (f1, f4), the C lane (f2, f5).  Each squares its own pair and forms
+// q = x^2 + xi y^2 and k = 2xy (B) or xi 2xy (C), the lanes swap (q, k), and
+// each forms its new pair from the partner's:
+//   B: f1' = out(k_C, f1, +), f4' = out(q_C, f4, -);  C: f2' = out(q_B, f2, -), f5' = out(k_B, f5, +)
+// -- kb_sqr_thr's outputs, term for term (the same bounds: kb_t_out's minus form
+// takes a qsum, its plus form a cross or xi cross).  Selects are branch-free
+// (the two lanes of a pair sit in one wave).
+DG_FN void kb_pair_send(const fp2& x, const fp2& y, bool c, fp2& q, fp2& k) {
+  const fp2 sx = fp2_sqr(x), sy = fp2_sqr(y);
+  const fp2 sxy = fp2_sqr(fp2_carry(fp2_add_lz(x, y)));
+  q = kb_t_qsum(sx, sy);
+  const fp2 kb = kb_t_cross(sxy, sx, sy), kc = kb_t_xi_cross(sxy, sx, sy);
+  k = fp2{fp_cmov(kb.c0, kc.c0, c), fp_cmov(kb.c1, kc.c1, c)};
+}
+DG_FN fp kb_t_out_sel(const fp& x3, const fp& f, bool minus) {
+  const fp t = fp_add_lz(fp_add_lz(x3, x3), x3), f2 = fp_add_lz(f, f);
+  return fp_reduce(fp_norm(fp_cmov(fp_add_lz(t, f2), fp_sub2_lz(t, f2), minus)));
+}
+DG_FN void kb_pair_recv(fp2& x, fp2& y, bool c, const fp2& rq, const fp2& rk) {
+  const fp2 ax{fp_cmov(rk.c0, rq.c0, c), fp_cmov(rk.c1, rq.c1, c)};
+  const fp2 ay{fp_cmov(rq.c0, rk.c0, c), fp_cmov(rq.c1, rk.c1, c)};
+  x = fp2{kb_t_out_sel(ax.c0, x.c0, c), kb_t_out_sel(ax.c1, x.c1, c)};
+  y = fp2{kb_t_out_sel(ay.c0, y.c0, !c), kb_t_out_sel(ay.c1, y.c1, !c)};
+}
+
 // 63 compressed squarings of (f1, f2, f4, f5); snap(j, f1, f2, f4, f5) after
 // s = 16, 48, 57, 60, 62, 63 of them (sum of 2^s = |x|).
 template <class Snap>
@@ -136,6 +162,49 @@ __global__ void __launch_bounds__(256, DG_KB_THR_OCC) k_kb_chain_thr(size_t cnt,
                  kb_st_thr(xbuf, i, pl, 10, f5);
                  if constexpr (NORM) st_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i, eng_kb_norm(f1));
                });
+}
+
+// Two lanes per round (kb_pair_send / _recv): 2 cnt threads, lane 2i the B
+// half of round i, lane 2i + 1 the C half; each lane holds 4 Fp of state
+// instead of 8, so the kernel fits fewer VGPRs than k_kb_chain_thr (more
+// waves per SIMD; tools/engbench/powprobe.hip), for one swap of 4 Fp per
+// squaring (quad_perm [1,0,3,2] DPP moves).  Same planes and snaps as
+// k_kb_chain_thr; NORM: the B lane writes Norm(4 f1).
+#ifndef DG_KB_PAIR_OCC
+#define DG_KB_PAIR_OCC 3
+#endif
+__device__ __forceinline__ fp fp_swap_pair(const fp& a) {
+  fp r;
+#pragma unroll
+  for (int l = 0; l < FP_LIMBS; ++l) r.l[l] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.l[l], 0xB1, 0xF, 0xF, false);
+  return r;
+}
+template <bool NORM>
+__global__ void __launch_bounds__(256, DG_KB_PAIR_OCC) k_kb_chain_pair(size_t cnt, uint32_t* __restrict__ xbuf,
+                                                                       uint32_t* __restrict__ nbuf) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = t >> 1;
+  if (i >= cnt) return;  // both lanes of a pair (same i) leave together
+  const bool c = (t & 1) != 0;
+  const int cx = c ? 4 : 2, cy = c ? 10 : 8;
+  fp2 x = kb_ld_thr(xbuf, i, ENG_KB_PL_M, cx), y = kb_ld_thr(xbuf, i, ENG_KB_PL_M, cy);
+  int s = 0;
+#pragma unroll 1
+  for (int j = 0; j < 6; ++j) {
+    const int sj = j == 0 ? 16 : j == 1 ? 48 : j == 2 ? 57 : j == 3 ? 60 : j == 4 ? 62 : 63;
+#pragma unroll 1
+    for (; s < sj; ++s) {
+      fp2 q, k;
+      kb_pair_send(x, y, c, q, k);
+      kb_pair_recv(x, y, c, fp2{fp_swap_pair(q.c0), fp_swap_pair(q.c1)}, fp2{fp_swap_pair(k.c0), fp_swap_pair(k.c1)});
+    }
+    const int pl = ENG_KB_PL_X0 + j;
+    kb_st_thr(xbuf, i, pl, cx, x);
+    kb_st_thr(xbuf, i, pl, cy, y);
+    if constexpr (NORM) {
+      if (!c) st_soa(nbuf + (size_t)j * FP_LIMBS * cnt, cnt, i, eng_kb_norm(x));
+    }
+  }
 }
 
 }  // namespace dgpu

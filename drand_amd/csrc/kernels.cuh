@@ -147,12 +147,14 @@ __global__ void __launch_bounds__(256, DG_SSWU_OCC) k_h2c_sswu(size_t n, const u
   st_g2j(q_out + which * G2J_WORDS * n, n, i, map_to_curve_sswu_iso3_body(uu));
 }
 
-// The SSWU stage in five launches (round 6): the two exponentiations of
-// each item (~85% of its products) run alone in k_fp_pow_planes, whose few
-// VGPRs let 8 waves share a SIMD, where the fused k_h2c_sswu holds 256 VGPRs
-// (2 waves) for its pre- and post-steps.  The out-of-line Fp calls issue
-// ~1.3x faster at 6-8 waves than at 2 (`tools/engbench/powprobe.hip`,
-// profiles/r06/r06h_powprobe.json).  Item j of 2n (which = j / n, i = j % n):
+// A/B (-DDG_SSWU_STAGED, capi.hip launch_sswu; measured slower in the bulk
+// pass, r06i): the SSWU stage in five launches, the two exponentiations of
+// each item (~85% of its products) alone in k_fp_pow_planes, whose 90 VGPRs
+// let 5 waves share a SIMD, where the fused k_h2c_sswu holds 256 VGPRs (2
+// waves).  In isolation the out-of-line Fp calls issue ~1.3x faster at 5-8
+// waves than at 2 (`tools/engbench/powprobe.hip`, profiles/r06/
+// r06h_powprobe.json); in the pass that did not carry over.  Item j of 2n
+// (which = j / n, i = j % n):
 //   k_sswu_a   u -> N, D, w into the item's q slot (x, y, z words), Norm(w) -> plane 3 which
 //   pow        plane 3 which: alpha -> g = alpha^((p+1)/4)
 //   k_sswu_b   square test (x2 if not), N, w updated in the slot; d -> plane 3 which + 1,

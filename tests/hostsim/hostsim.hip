@@ -1053,3 +1053,44 @@ extern "C" int hs_kb_dec_lz_check(int n, uint64_t seed) {
   }
   return bad;
 }
+
+// kb_thread.cuh's two-lane compressed squaring (kb_pair_send on both halves,
+// the (q, k) swap, kb_pair_recv: what k_kb_chain_pair runs) == kb_sqr_thr,
+// limb for limb, over `reps` chained squarings from n random CI starts and
+// the all-maximal-limb start; returns the number of disagreeing starts.
+extern "C" int hs_kb_pair_check(int n, int reps, uint64_t seed) {
+  uint64_t s = seed | 1;
+  auto rnd = [&]() {
+    fp x;
+    for (int i = 0; i < FP_LIMBS; ++i) {
+      s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+      x.l[i] = (uint32_t)s & FP_MASK;
+    }
+    x.l[FP_LIMBS - 1] &= 0x3FFFFFu;
+    return fp_reduce(x);
+  };
+  fp mx;
+  for (int i = 0; i < FP_LIMBS; ++i) mx.l[i] = FP_MASK;
+  mx.l[FP_LIMBS - 1] = 0x3FFFFFu;
+  mx = fp_reduce(mx);
+  auto same = [](const fp2& a, const fp2& b) { return !memcmp(&a, &b, sizeof(fp2)); };
+  int bad = 0;
+  for (int t = 0; t <= n; ++t) {
+    const bool edge = t == n;
+    fp2 f1 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()}, f2 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()};
+    fp2 f4 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()}, f5 = edge ? fp2{mx, mx} : fp2{rnd(), rnd()};
+    fp2 bx = f1, by = f4, cx = f2, cy = f5;  // the B lane's and the C lane's halves
+    bool ok = true;
+    for (int r = 0; r < reps; ++r) {
+      kb_sqr_thr(f1, f2, f4, f5);
+      fp2 qb, kb, qc, kc;
+      kb_pair_send(bx, by, false, qb, kb);
+      kb_pair_send(cx, cy, true, qc, kc);
+      kb_pair_recv(bx, by, false, qc, kc);
+      kb_pair_recv(cx, cy, true, qb, kb);
+      ok = ok && same(bx, f1) && same(by, f4) && same(cx, f2) && same(cy, f5);
+    }
+    if (!ok) ++bad;
+  }
+  return bad;
+}

@@ -337,6 +337,28 @@ def test_thread_lines_equal_engine_lines():
     assert np.array_equal(thr == 0, expect)
 
 
+def test_karabina_chain_on_two_lanes_equals_default():
+    """The Karabina chain with each round's compressed element split over two
+    lanes (k_kb_chain_pair, A/B build DGPU_KB_PAIR=1: the lanes swap (q, k)
+    once per squaring) against the one-thread chain: 20,011 rounds (odd, a
+    ragged last block), 1% corrupted, on two engine chunk sizes and with the
+    Karabina fallback forced on every 7th item -- identical reasons, equal to
+    the construction."""
+    from drand_amd import _lib
+    from drand_amd.synth import corrupt, make_chain
+    n = 20011
+    c = make_chain(29, n, _lib.SCHEME_CHAINED, seg_len=64)
+    bad = corrupt(c, 29, rate=1e-2)
+    ref = _verify_with_env(c, {"DGPU_KB_PAIR": "0"})
+    pair = _verify_with_env(c, {"DGPU_KB_PAIR": "1"})
+    pair_small = _verify_with_env(c, {"DGPU_KB_PAIR": "1", "DGPU_ENG_CHUNK": "4099"})
+    pair_fb = _verify_with_env(c, {"DGPU_KB_PAIR": "1", "DGPU_KB_TEST_FLAG": "7"})
+    assert pair.tolist() == ref.tolist() == pair_small.tolist() == pair_fb.tolist()
+    expect = np.ones(n, dtype=bool)
+    expect[list(bad.keys())] = False
+    assert np.array_equal(pair == 0, expect)
+
+
 def test_engine_without_idle_lanes_equals_default():
     """The Miller loop and the Karabina FE segments on 16-group 192-thread
     blocks (k_eng_miller_xw, k_eng_fe_seg_xw: groups 5 and 10 span two waves,

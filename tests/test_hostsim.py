@@ -387,6 +387,16 @@ def test_thread_lines_match_oracle_and_engine(hostsim):
         hostsim.hs_eng_set_lines_thread(0)
 
 
+def test_kb_chain_two_lane_squaring_matches(hostsim):
+    # k_kb_chain_pair's squaring (each lane squares its Fp4 half, the lanes
+    # swap (q, k), each forms its new half) == the one-thread kb_sqr_thr, limb
+    # for limb, over 20 chained squarings from 300 random CI starts and the
+    # all-maximal-limb start
+    hostsim.hs_kb_pair_check.restype = ctypes.c_int
+    hostsim.hs_kb_pair_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+    assert hostsim.hs_kb_pair_check(300, 20, 91) == 0
+
+
 def test_kb_decompress_lazy_matches(hostsim):
     # the decompression with lazy linear steps (what k_eng_kb_dec runs) ==
     # the every-step-reduced form, outputs CI, on 2,000 random inputs up to the

@@ -292,22 +292,24 @@ DG_FN void hash_to_field_g2(fp2& u0, fp2& u1, const uint32_t msg[8]) {
 //   sswu_mid   g = alpha^((p+1)/4): gx1 square or not (then x2, w scaled); returns
 //              d (fp2_sqrt_scaled's real part) and dm4 = d Norm(D)^4 for the second
 //   sswu_post  t = dm4^((p-3)/4): y, its sign, the 3-isogeny.
-DG_FN void sswu_pre(const fp2& u, fp2& N, fp2& D, fp2& w) {
-  const fp2 zu2 = fp2_mul(C_SSWU_Z, fp2_sqr(u));
+DG_FN fp2 sswu_zu2(const fp2& u) { return fp2_mul(C_SSWU_Z, fp2_sqr(u)); }
+DG_FN void sswu_pre(const fp2& zu2, fp2& N, fp2& D, fp2& D2, fp2& D3, fp2& w) {
   const fp2 den = fp2_add(fp2_sqr(zu2), zu2);
   const bool den0 = fp2_is_zero(den);
   N = fp2_cmov(fp2_mul(C_SSWU_MINUS_B_OVER_A, fp2_add(den, fp2_one())), C_SSWU_B_OVER_ZA, den0);
   D = fp2_cmov(den, fp2_one(), den0);
-  const fp2 D2 = fp2_sqr(D);
-  const fp2 D3 = fp2_mul(D2, D);
+  D2 = fp2_sqr(D);
+  D3 = fp2_mul(D2, D);
   w = fp2_mul(fp2_add(fp2_mul(N, fp2_add(fp2_sqr(N), fp2_mul(C_SSWU_A, D2))), fp2_mul(C_SSWU_B, D3)), D);
+}
+DG_FN void sswu_pre(const fp2& u, fp2& N, fp2& D, fp2& w) {
+  fp2 D2, D3;
+  sswu_pre(sswu_zu2(u), N, D, D2, D3, w);
 }
 // g: the candidate root of alpha = Norm(w); N, w updated to x2's when gx1 is
 // not a square.  Returns d; dm4 = d Norm(D)^4 (fp2_sqrt_scaled's steps).
-DG_FN fp sswu_mid(const fp2& u, fp2& N, const fp2& D, fp2& w, fp g, fp& dm4) {
-  const fp alpha = fp2_norm(w);
+DG_FN fp sswu_mid(const fp2& u, const fp2& zu2, const fp& alpha, fp2& N, const fp2& D, fp2& w, fp g, fp& dm4) {
   if (!fp_eq(fp_sqr(g), alpha)) {  // gx1 not square: x2 = Z u^2 x1, gx2 = (Z u^2)^3 gx1
-    const fp2 zu2 = fp2_mul(C_SSWU_Z, fp2_sqr(u));
     const fp nu = fp2_norm(u);
     g = fp_mul(fp_mul(C_SQRT_M125, fp_mul(fp_sqr(nu), nu)), g);
     w = fp2_mul(fp2_mul(fp2_sqr(zu2), zu2), w);
@@ -315,13 +317,11 @@ DG_FN fp sswu_mid(const fp2& u, fp2& N, const fp2& D, fp2& w, fp g, fp& dm4) {
   }
   return fp2_sqrt_scaled_pre(w, g, fp2_norm(D), dm4);
 }
-DG_FN g2j sswu_post(const fp2& u, const fp2& N, const fp2& D, const fp2& w, const fp& d, const fp& dm4,
-                    const fp& t) {
+DG_FN g2j sswu_post(const fp2& u, const fp2& N, const fp2& D, const fp2& D2, const fp2& D3, const fp2& w,
+                    const fp& d, const fp& dm4, const fp& t) {
   fp2 y = fp2_mul(fp2_sqrt_scaled_post(w, d, dm4, t), fp2_sqr(fp2_conj(D)));
   if (fp2_sgn0(u) != fp2_sgn0(y)) y = fp2_neg(y);
   // 3-isogeny on x = N/D, numerators homogenized to degree 3 (x denominator 2)
-  const fp2 D2 = fp2_sqr(D);
-  const fp2 D3 = fp2_mul(D2, D);
   const fp2 N2 = fp2_sqr(N);
   const fp2 N3 = fp2_mul(N2, N);
   const fp2 N2D = fp2_mul(N2, D);
@@ -344,12 +344,20 @@ DG_FN g2j sswu_post(const fp2& u, const fp2& N, const fp2& D, const fp2& w, cons
   return r;
 }
 
+DG_FN g2j sswu_post(const fp2& u, const fp2& N, const fp2& D, const fp2& w, const fp& d, const fp& dm4,
+                    const fp& t) {
+  const fp2 D2 = fp2_sqr(D);
+  return sswu_post(u, N, D, D2, fp2_mul(D2, D), w, d, dm4, t);
+}
+
 DG_FN g2j map_to_curve_sswu_iso3_body(const fp2& u) {
-  fp2 N, D, w;
-  sswu_pre(u, N, D, w);
+  const fp2 zu2 = sswu_zu2(u);
+  fp2 N, D, D2, D3, w;
+  sswu_pre(zu2, N, D, D2, D3, w);
+  const fp alpha = fp2_norm(w);
   fp dm4;
-  const fp d = sswu_mid(u, N, D, w, fp_sqrt_cand(fp2_norm(w)), dm4);
-  return sswu_post(u, N, D, w, d, dm4, DG_POW(dm4, EXP_P_MINUS_3_DIV_4));
+  const fp d = sswu_mid(u, zu2, alpha, N, D, w, fp_sqrt_cand(alpha), dm4);
+  return sswu_post(u, N, D, D2, D3, w, d, dm4, DG_POW(dm4, EXP_P_MINUS_3_DIV_4));
 }
 
 DG_NOINL g2j map_to_curve_sswu_iso3(const fp2& u) { return map_to_curve_sswu_iso3_body(u); }

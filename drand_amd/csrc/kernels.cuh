@@ -195,8 +195,8 @@ __global__ void __launch_bounds__(256, 2) k_sswu_b(size_t n, const uint32_t* __r
   const g2j s = ld_g2j(qs, n, i);
   fp2 N = s.x, w = s.z;
   fp dm4;
-  const fp d = sswu_mid(fp2{ld_fp(ub, n, i), ld_fp(ub + FP_WORDS * n, n, i)}, N, s.y, w,
-                        ld_fp(aux.p[3 * which], n, i), dm4);
+  const fp2 uu{ld_fp(ub, n, i), ld_fp(ub + FP_WORDS * n, n, i)};
+  const fp d = sswu_mid(uu, sswu_zu2(uu), fp2_norm(w), N, s.y, w, ld_fp(aux.p[3 * which], n, i), dm4);
   st_g2j(qs, n, i, g2j{N, s.y, w});
   st_fp(aux.p[3 * which + 1], n, i, d);
   st_fp(aux.p[3 * which + 2], n, i, dm4);

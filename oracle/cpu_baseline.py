@@ -71,8 +71,13 @@ def _timed(fn):
 
 def sample_size(n, seconds, cores, per_round_1core, calib_rate=None):
     """Rounds for ~`seconds` of wall time: from a measured parallel rate when
-    there is one (quota-limited boxes run fewer cores than threads)."""
+    there is one (quota-limited boxes run fewer cores than threads), capped
+    at the cgroup quota's rate -- a sub-second calibration burst runs above
+    the quota before the throttle engages (r06: a 12 s budget ran 48 s)."""
     rate = calib_rate if calib_rate else cores / max(per_round_1core, 1e-6)
+    q = host_cores().get("cgroup_quota_cores")
+    if q:
+        rate = min(rate, q / max(per_round_1core, 1e-6))
     return int(max(cores, min(n, seconds * rate)))
 
 

@@ -60,6 +60,44 @@ DG_FN g2j g2_dbl_body(const g2j& p) {
 
 DG_NOINL g2j g2_dbl(const g2j& p) { return g2_dbl_body(p); }
 
+// fp2_mul with its outputs normalized but not reduced -- c0 = t0 + 8p - t1,
+// c1 = t2 + 32p - (t0 + t1) -- for a consumer that reduces anyway (or, as Z
+// of the ladder below, feeds another fp2_mul).  With t0, t1 < 1.05p and
+// t2 < 1.2p (operand sums < 4.02p x 4.02p, or the bounds stated by the
+// caller): c0 < 9.1p, c1 < 33.3p, limbs < 2^28 (top limb < 2^23).
+DG_FN fp2 fp2_mul_nr(const fp2& a, const fp2& b) {
+  const fp t0 = fp_mul(a.c0, b.c0);
+  const fp t1 = fp_mul(a.c1, b.c1);
+  const fp t2 = fp_mul(fp_add_lz(a.c0, a.c1), fp_add_lz(b.c0, b.c1));
+  return fp2{fp_norm(fp_sub_lz(t0, t1)), fp_norm(fp_sub2_lz(t2, fp_add_lz(t0, t1)))};
+}
+
+// g2_dbl_body with four reductions fewer, for the cofactor ladder: Y3's
+// product is left unreduced into fp2_sub32 (65.3p + 32p bound: reduced once),
+// and Z is carried unreduced from doubling to doubling -- Z3 = (2Y) Z with
+// Z.c0 < 9.1p, Z.c1 < 33.3p: operand sums 8.04p x 42.4p = 341 p^2 (fp_mul
+// bound ~2600 p^2), t2 < 1.13p, so Z3 keeps the same bounds.  Z must be
+// reduced (g2_z_reduce) before an addition or any other consumer.
+DG_FN g2j g2_dbl_lz(const g2j& p) {
+  g2j r;
+  r.z = fp2_mul_nr(fp2_add_lz(p.y, p.y), p.z);
+  const fp2 B = fp2_sqr(p.y);
+  const fp2 A = fp2_sqr(p.x);
+  const fp2 XB = fp2_carry(fp2_add_lz(p.x, B));
+  const fp2 C = fp2_sqr(B);
+  const fp2 Dh = fp2_sub32(fp2_sqr(XB), fp2_add_lz(A, C));
+  const fp2 E = fp2_carry(fp2_add_lz(fp2_add_lz(A, A), A));
+  r.x = fp2_sub32(fp2_sqr(E), fp2_carry(fp2_mulk_lz(Dh, 4)));
+  const fp2 D2 = fp2_add_lz(Dh, Dh);
+  const fp2 DX = fp2_carry(fp2{fp_sub_lz(D2.c0, r.x.c0), fp_sub_lz(D2.c1, r.x.c1)});
+  r.y = fp2_sub32(fp2_mul_nr(E, DX), fp2_carry(fp2_mulk_lz(C, 8)));
+  return r;
+}
+DG_FN g2j g2_z_reduce(g2j r) {
+  r.z = fp2{fp_reduce(r.z.c0), fp_reduce(r.z.c1)};
+  return r;
+}
+
 // add-2007-bl with the exceptional cases resolved (P == Q -> dbl,
 // P == -Q -> infinity, either operand infinity -> the other).
 // Lazy linear steps: rr = 2(s2 - s1) and 2h carried (< 4.02p); X3 = rr^2 -
@@ -370,6 +408,13 @@ DG_FN g2j g2_psi2_body(const g2j& p) {
   return g2j{fp2_mul_fp(p.x, fp2(C_PSI2_CX).c0), fp2_mul_fp(p.y, fp2(C_PSI2_CY).c0), p.z};
 }
 
+#ifdef DG_LADDER_DBL_PLAIN  // A/B: every doubling fully reduced (g2_dbl_body)
+#define G2_LADDER_DBL g2_dbl_body
+#define G2_LADDER_ZRED(r) (r)
+#else
+#define G2_LADDER_DBL g2_dbl_lz
+#define G2_LADDER_ZRED(r) g2_z_reduce(r)
+#endif
 // [|x|] of the point in stash slot k, |x| = 0xd201000000010000 (bits 63, 62,
 // 60, 57, 48, 16): runs of 1, 2, 3, 9 and 32 doublings, each closed by an
 // addition of the point reloaded from the slot, then 16 doublings -- only the
@@ -381,12 +426,12 @@ DG_FN g2j g2_mul_absx_stash(Stash& st, int k, bool& exc) {
   for (int a = 0; a < 5; ++a) {
     const int nd = a == 0 ? 1 : a == 1 ? 2 : a == 2 ? 3 : a == 3 ? 9 : 32;
 #pragma unroll 1
-    for (int d = 0; d < nd; ++d) r = g2_dbl_body(r);
-    r = g2_add_nx_q(r, st.at(k), exc);
+    for (int d = 0; d < nd; ++d) r = G2_LADDER_DBL(r);
+    r = g2_add_nx_q(G2_LADDER_ZRED(r), st.at(k), exc);
   }
 #pragma unroll 1
-  for (int d = 0; d < 16; ++d) r = g2_dbl_body(r);
-  return r;
+  for (int d = 0; d < 16; ++d) r = G2_LADDER_DBL(r);
+  return G2_LADDER_ZRED(r);
 }
 
 // h_eff (Q0 + Q1) in the order of g2_clear_cofactor (RFC 9380 G.3) with the

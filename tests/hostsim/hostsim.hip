@@ -1094,3 +1094,25 @@ extern "C" int hs_kb_pair_check(int n, int reps, uint64_t seed) {
   }
   return bad;
 }
+
+// curve.cuh g2_dbl_lz (the cofactor ladder's doubling: Y3's product and Z
+// carried unreduced) == g2_dbl_body over `reps` chained doublings from n
+// points H(msg_i) (Z reduced only at the end, as the ladder does before an
+// addition); returns the number of starts whose chains disagree (compared as
+// affine points).
+extern "C" int hs_g2_dbl_lz_check(int n, int reps, uint64_t seed) {
+  int bad = 0;
+  for (int t = 0; t < n; ++t) {
+    uint32_t m[8];
+    for (int w = 0; w < 8; ++w) m[w] = (uint32_t)(seed * 0x9E3779B97F4A7C15ull >> 32) ^ (uint32_t)(t * 8 + w);
+    fp2 u0, u1;
+    hash_to_field_g2(u0, u1, m);
+    g2j a = map_to_curve_sswu_iso3_body(u0), b = a;  // a point of E' with a large cofactor
+    for (int r = 0; r < reps; ++r) {
+      a = g2_dbl_body(a);
+      b = g2_dbl_lz(b);
+    }
+    if (!g2_eq(a, g2_z_reduce(b))) ++bad;
+  }
+  return bad;
+}

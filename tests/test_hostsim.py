@@ -123,6 +123,15 @@ def test_h2c_finish_ladder_matches_generic(hostsim):
                 assert o.raw[0] & 0x40  # the infinity flag
 
 
+def test_ladder_doubling_lazy_matches(hostsim):
+    # the cofactor ladder's doubling with Y3's product and Z unreduced
+    # (g2_dbl_lz) == the fully reduced doubling over 200 chained doublings
+    # from 20 SSWU points
+    hostsim.hs_g2_dbl_lz_check.restype = ctypes.c_int
+    hostsim.hs_g2_dbl_lz_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
+    assert hostsim.hs_g2_dbl_lz_check(20, 200, 3) == 0
+
+
 def test_decompress_kat(hostsim):
     k = load_golden("kat_bls12381_compat_v112.json")
     o = buf(96)

@@ -434,6 +434,48 @@ DG_FN g2j g2_mul_absx_stash(Stash& st, int k, bool& exc) {
   return G2_LADDER_ZRED(r);
 }
 
+// madd-2007-bl (g2_add_affine_body) for operands that are neither equal,
+// opposite nor the identity, the affine operand fetched through q (q.x(),
+// q.y()) where used; `exc` as g2_add_nx_q.
+template <class Q>
+DG_FN g2j g2_madd_nx_q(const g2j& p, const Q& q, bool& exc) {
+  const fp2 z1z1 = fp2_sqr(p.z);
+  const fp2 h = fp2_sub(fp2_mul(q.x(), z1z1), p.x);
+  const fp2 rh = fp2_sub(fp2_mul(fp2_mul(q.y(), p.z), z1z1), p.y);
+  exc = exc || g2_is_inf(p) || fp2_is_zero(h);
+  const fp2 rr = fp2_carry(fp2_add_lz(rh, rh));
+  const fp2 hh = fp2_sqr(h);
+  const fp2 i = fp2_carry(fp2_mulk_lz(hh, 4));
+  const fp2 j = fp2_mul(h, i);
+  const fp2 v = fp2_mul(p.x, i);
+  g2j r;
+  r.x = fp2_sub32(fp2_sqr(rr), fp2_carry(fp2_add_lz(fp2_add_lz(j, v), v)));
+  const fp2 VX = fp2_carry(fp2{fp_sub_lz(v.c0, r.x.c0), fp_sub_lz(v.c1, r.x.c1)});
+  r.y = fp2_sub(fp2_mul(rr, VX), fp2_mul(fp2_add_lz(p.y, p.y), j));
+  r.z = fp2_sub32(fp2_sqr(fp2_carry(fp2_add_lz(p.z, h))), fp2_add_lz(z1z1, hh));
+  return r;
+}
+
+// G2 membership psi(P) == -[|x|]P (g2_in_subgroup) for an affine P (not the
+// identity) on the cofactor ladder's structure: runs of lazy doublings, each
+// closed by a fast mixed addition of P fetched through q -- only the
+// accumulator lives across the loops.  exc: an exceptional addition (P of
+// small order); the caller then decides with g2_in_subgroup.
+template <class Q>
+DG_FN bool g2_in_subgroup_ladder(const g2a& p, const Q& q, bool& exc) {
+  g2j r = g2_from_affine(p);
+#pragma unroll 1
+  for (int a = 0; a < 5; ++a) {
+    const int nd = a == 0 ? 1 : a == 1 ? 2 : a == 2 ? 3 : a == 3 ? 9 : 32;
+#pragma unroll 1
+    for (int d = 0; d < nd; ++d) r = G2_LADDER_DBL(r);
+    r = g2_madd_nx_q(G2_LADDER_ZRED(r), q, exc);
+  }
+#pragma unroll 1
+  for (int d = 0; d < 16; ++d) r = G2_LADDER_DBL(r);
+  return g2_eq(g2_psi(g2_from_affine(q.get())), g2_neg(G2_LADDER_ZRED(r)));
+}
+
 // h_eff (Q0 + Q1) in the order of g2_clear_cofactor (RFC 9380 G.3) with the
 // cold operands parked in three point slots of `st` (k_h2c_finish: the
 // round's own SoA slots in HBM) so the two [|x|] ladders hold one point each:

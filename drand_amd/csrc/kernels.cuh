@@ -216,6 +216,41 @@ __global__ void __launch_bounds__(256, DG_SSWU_OCC) k_sswu_c(size_t n, const uin
                              ld_fp(aux.p[3 * which + 2], n, i)));
 }
 
+// An affine point at item i of an SoA array ([x.c0, x.c1, y.c0, y.c1][limb][n]),
+// each coordinate loaded where the ladder uses it (the base passes through an
+// empty asm per fetch so the loads stay in the loop instead of being hoisted
+// and spilled).
+struct g2a_soa_fetch {
+  const uint32_t* base;
+  size_t n, i;
+  __device__ __forceinline__ const uint32_t* b() const {
+    const uint32_t* p = base;
+    __asm__ volatile("" : "+s"(p));
+    return p;
+  }
+  __device__ __forceinline__ fp2 x() const {
+    const uint32_t* p = b();
+    return fp2{ld_fp(p, n, i), ld_fp(p + FP_WORDS * n, n, i)};
+  }
+  __device__ __forceinline__ fp2 y() const {
+    const uint32_t* p = b();
+    return fp2{ld_fp(p + 2 * FP_WORDS * n, n, i), ld_fp(p + 3 * FP_WORDS * n, n, i)};
+  }
+  __device__ __forceinline__ g2a get() const { return g2a{x(), y()}; }
+};
+// G2 membership of a decoded signature p, stored first at item i of pts (its
+// output slot): the ladder form, the generic test on an exceptional addition.
+__device__ __forceinline__ bool g2_in_subgroup_stored(const g2a& p, uint32_t* pts, size_t n, size_t i) {
+  st_g2a(pts, n, i, p);
+#ifdef DG_SUBGROUP_GENERIC  // A/B: rounds 1-5, g2_in_subgroup with the point in registers
+  return g2_in_subgroup(g2_from_affine(p));
+#endif
+  bool exc = false;
+  const g2a_soa_fetch f{pts, n, i};
+  const bool in = g2_in_subgroup_ladder(p, f, exc);
+  return exc ? g2_in_subgroup(g2_from_affine(f.get())) : in;
+}
+
 // Point slots of g2_clear_cofactor_stash in the round's own SoA words: 0, 1 =
 // the two SSWU outputs' slots of q (each read once, before it is written),
 // 2 = the output slot (X, Y in h_out, Z in z_out).
@@ -403,15 +438,19 @@ __global__ void __launch_bounds__(256, 2) k_decode_g2_sigs_sub(size_t n, const u
   g2a p{fp2_zero(), fp2_zero()};
   if (sig_len[i] != 96 || msg_bad_record(m, i)) {
     st = ST_DECODE;
+    st_g2a(sig_out, n, i, p);
   } else {
     uint8_t buf[96];
     const uint8_t* src = sigs + i * sig_stride;
     for (int k = 0; k < 96; ++k) buf[k] = src[k];
     int rc = g2_decompress(&p, buf, false);
-    if (rc == DEC_OK && !g2_in_subgroup(g2_from_affine(p))) rc = DEC_ERR_SUBGROUP;
+    if (rc == DEC_OK) {  // p is stored by the membership test (not kept live across its ladder)
+      if (!g2_in_subgroup_stored(p, sig_out, n, i)) rc = DEC_ERR_SUBGROUP;
+    } else {
+      st_g2a(sig_out, n, i, p);
+    }
     st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
   }
-  st_g2a(sig_out, n, i, p);
   status[i] = st;
 }
 

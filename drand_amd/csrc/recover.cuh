@@ -101,15 +101,19 @@ __global__ void __launch_bounds__(256, 2) k_decode_partials(size_t n_items, cons
   uint32_t idx = 0xFFFFFFFFu;
   uint8_t st = ST_DECODE;
   g2a p{fp2_zero(), fp2_zero()};
-  if (len >= 2) {
-    idx = ((uint32_t)src[0] << 8) | src[1];
-    if (len == 98) {
-      uint8_t buf[96];
-      for (int k = 0; k < 96; ++k) buf[k] = src[2 + k];
-      int rc = g2_decompress(&p, buf, false);
-      if (rc == DEC_OK && !g2_in_subgroup(g2_from_affine(p))) rc = DEC_ERR_SUBGROUP;
-      st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
+  if (len >= 2) idx = ((uint32_t)src[0] << 8) | src[1];
+  if (len == 98) {
+    uint8_t buf[96];
+    for (int k = 0; k < 96; ++k) buf[k] = src[2 + k];
+    int rc = g2_decompress(&p, buf, false);
+    if (rc == DEC_OK) {  // p is stored by the membership test (not kept live across its ladder)
+      if (!g2_in_subgroup_stored(p, sig_pts, n_items, i)) rc = DEC_ERR_SUBGROUP;
+    } else {
+      st_g2a(sig_pts, n_items, i, p);
     }
+    st = rc == DEC_OK ? ST_OK : rc == DEC_INFINITY ? ST_INFINITY : rc == DEC_ERR_SUBGROUP ? ST_SUBGROUP : ST_DECODE;
+  } else {
+    st_g2a(sig_pts, n_items, i, p);
   }
   fp nx = fp_zero(), y = fp_zero();
   if (st == ST_OK) {
@@ -120,7 +124,6 @@ __global__ void __launch_bounds__(256, 2) k_decode_partials(size_t n_items, cons
       pubpoly_eval(commits, t, idx, nx, y);
     }
   }
-  st_g2a(sig_pts, n_items, i, p);
   st_fp(pk_items, n_items, i, nx);
   st_fp(pk_items + FP_LIMBS * n_items, n_items, i, y);
   idx_out[i] = idx;

@@ -1116,3 +1116,34 @@ extern "C" int hs_g2_dbl_lz_check(int n, int reps, uint64_t seed) {
   }
   return bad;
 }
+
+// curve.cuh g2_in_subgroup_ladder (the decode kernels' membership test: lazy
+// doublings, fast mixed additions of the fetched point) == g2_in_subgroup on n
+// points of E' outside G2 (SSWU outputs) and their images in G2 (h_eff);
+// returns mismatches (an exceptional addition counts as one: none is expected
+// on these inputs), -1 if the inputs were not what they should be.
+struct hs_g2a_fetch {
+  g2a p;
+  fp2 x() const { return p.x; }
+  fp2 y() const { return p.y; }
+  g2a get() const { return p; }
+};
+extern "C" int hs_g2_subgroup_ladder_check(int n, uint64_t seed) {
+  int bad = 0;
+  for (int t = 0; t < n; ++t) {
+    uint32_t m[8];
+    for (int w = 0; w < 8; ++w) m[w] = (uint32_t)(seed * 0xD1B54A32D192ED03ull >> 32) ^ (uint32_t)(t * 8 + w);
+    fp2 u0, u1;
+    hash_to_field_g2(u0, u1, m);
+    const g2j raw = map_to_curve_sswu_iso3_body(u0);
+    for (int in_g2 = 0; in_g2 < 2; ++in_g2) {
+      const g2a a = g2_to_affine(in_g2 ? g2_clear_cofactor(raw) : raw);
+      const bool ref = g2_in_subgroup(g2_from_affine(a));
+      if (ref != (in_g2 == 1)) return -1;
+      bool exc = false;
+      const bool got = g2_in_subgroup_ladder(a, hs_g2a_fetch{a}, exc);
+      if (exc || got != ref) ++bad;
+    }
+  }
+  return bad;
+}

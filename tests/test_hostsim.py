@@ -132,6 +132,15 @@ def test_ladder_doubling_lazy_matches(hostsim):
     assert hostsim.hs_g2_dbl_lz_check(20, 200, 3) == 0
 
 
+def test_subgroup_ladder_matches_generic(hostsim):
+    # the decode kernels' G2 membership test on the ladder (lazy doublings,
+    # fast mixed additions, P fetched where used) == g2_in_subgroup, on 24
+    # points outside G2 (SSWU outputs) and their cofactor-cleared images
+    hostsim.hs_g2_subgroup_ladder_check.restype = ctypes.c_int
+    hostsim.hs_g2_subgroup_ladder_check.argtypes = [ctypes.c_int, ctypes.c_uint64]
+    assert hostsim.hs_g2_subgroup_ladder_check(24, 11) == 0
+
+
 def test_decompress_kat(hostsim):
     k = load_golden("kat_bls12381_compat_v112.json")
     o = buf(96)

@@ -418,7 +418,44 @@ __device__ __forceinline__ g2a recover_ld_row(const uint32_t* __restrict__ rows,
   return q;
 }
 
+// One window-table entry of the recovery MSM, signed, each coordinate loaded
+// where the addition uses it (the base passes through an empty asm per fetch:
+// not hoisted and spilled).  ROWS: 224-byte rows, else the SoA planes.
+template <bool ROWS>
+struct rec_entry_fetch {
+  const uint32_t* tab;
+  size_t N, ei;
+  bool neg;
+  __device__ __forceinline__ const uint32_t* b() const {
+    const uint32_t* p = tab;
+    __asm__ volatile("" : "+s"(p));
+    return p;
+  }
+  __device__ __forceinline__ fp2 x() const {
+    if (ROWS) {
+      const g2a q = recover_ld_row(b(), ei);
+      return q.x;
+    }
+    return fp2{ld_fp(b(), N, ei), ld_fp(b() + FP_WORDS * N, N, ei)};
+  }
+  __device__ __forceinline__ fp2 y() const {
+    fp2 y;
+    if (ROWS) {
+      y = recover_ld_row(b(), ei).y;
+    } else {
+      y = fp2{ld_fp(b() + 2 * FP_WORDS * N, N, ei), ld_fp(b() + 3 * FP_WORDS * N, N, ei)};
+    }
+    return fp2_cmov(y, fp2_neg(y), neg);
+  }
+  __device__ __forceinline__ g2a get() const { return g2a{x(), y()}; }
+};
+
 // ROWS: the table as rows (k_recover_tab_rows), else the SoA planes.
+// FAST (round 6): the cofactor ladder's structure -- lazy doublings (Z
+// reduced once per window), fast mixed additions of the fetched entry (the
+// identity accumulator handled by a select: acc = e), no call site in the
+// loops; an exceptional addition (acc = +-e) redoes the slice with the
+// generic mixed addition.
 template <bool ROWS>
 __global__ void __launch_bounds__(256, 2) k_recover_msm_aff(size_t n_rounds, int t, const uint8_t* __restrict__ ok,
                                                           const uint64_t* __restrict__ digits,
@@ -432,21 +469,49 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm_aff(size_t n_rounds, int
   const uint64_t* d = digits + r * RECOVER_MAX_T * RECOVER_SLOTS + i;
   const size_t N = n_rounds * (size_t)t * 8;
   const size_t base = r * (size_t)t * 8;
+  bool exc = false;
   g2j acc = g2_infinity();
+#ifndef DG_RECOVER_MSM_GENERIC
 #pragma unroll 1
   for (int w = 16; w >= 0; --w) {
     if (w < 16) {
 #pragma unroll 1
-      for (int s = 0; s < 4; ++s) acc = g2_dbl_body(acc);
+      for (int s = 0; s < 4; ++s) acc = G2_LADDER_DBL(acc);
+      acc = G2_LADDER_ZRED(acc);
     }
 #pragma unroll 1
     for (int j = 0; j < t; ++j) {
       const int dg = win4_digit64(d[RECOVER_SLOTS * j], w);
       const int mag = dg < 0 ? -dg : dg;
-      const size_t ei = base + (size_t)j * 8 + ((mag - 1) & 7);
-      g2a e = ROWS ? recover_ld_row(tab, ei) : ld_g2a(tab, N, ei);
-      e.y = fp2_cmov(e.y, fp2_neg(e.y), dg < 0);
-      acc = g2_cmov(acc, g2_add_affine_body(acc, e), mag != 0);
+      const rec_entry_fetch<ROWS> f{tab, N, base + (size_t)j * 8 + ((mag - 1) & 7), dg < 0};
+      const bool ainf = g2_is_inf(acc);
+      bool ex = false;
+      g2j sum = g2_madd_nx_q(acc, f, ex);
+      if (ainf) sum = g2_from_affine(f.get());  // only before the slice's first nonzero digit
+      exc = exc || (ex && !ainf && mag != 0);
+      acc = g2_cmov(acc, sum, mag != 0);
+    }
+  }
+#else
+  exc = true;
+#endif
+  if (exc) {  // the generic mixed addition (rounds 2-5): exceptional cases resolved
+    acc = g2_infinity();
+#pragma unroll 1
+    for (int w = 16; w >= 0; --w) {
+      if (w < 16) {
+#pragma unroll 1
+        for (int s = 0; s < 4; ++s) acc = g2_dbl_body(acc);
+      }
+#pragma unroll 1
+      for (int j = 0; j < t; ++j) {
+        const int dg = win4_digit64(d[RECOVER_SLOTS * j], w);
+        const int mag = dg < 0 ? -dg : dg;
+        const size_t ei = base + (size_t)j * 8 + ((mag - 1) & 7);
+        g2a e = ROWS ? recover_ld_row(tab, ei) : ld_g2a(tab, N, ei);
+        e.y = fp2_cmov(e.y, fp2_neg(e.y), dg < 0);
+        acc = g2_cmov(acc, g2_add_affine_body(acc, e), mag != 0);
+      }
     }
   }
   st_g2j(part + (size_t)i * G2J_WORDS * n_rounds, n_rounds, r, acc);

@@ -29,6 +29,7 @@
 //   k_sum_level   pairwise tree over the runs of each (MSM, window)
 //   k_msm_root    MSM_m = W_m0 + 2^16 W_m1; P = MSM_0 + endo(MSM_1), S = MSM_2 + endo(MSM_3)
 #pragma once
+#include <type_traits>
 #include "kernels.cuh"
 #include "group_ops.cuh"
 
@@ -251,6 +252,37 @@ __device__ __forceinline__ void msm_seg_emit(uint32_t key, size_t s, size_t e, s
   M::st_jac(whole ? buckets : part, whole ? MSM_KEYS : 2 * T, whole ? key : (s > o ? t : T + t), acc);
 }
 
+// A G2 row (x.c0, x.c1, y.c0, y.c1 limbs, 224 bytes), each coordinate loaded
+// where the addition uses it (empty asm on the address per fetch).
+struct g2_row_fetch {
+  const uint32_t* row;
+  __device__ __forceinline__ const uint32_t* b() const {
+    const uint32_t* p = row;
+    __asm__ volatile("" : "+v"(p));
+    return p;
+  }
+  __device__ __forceinline__ fp2 x() const {
+    const uint32_t* p = b();
+    fp2 v;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) v.c0.l[l] = p[l], v.c1.l[l] = p[FP_LIMBS + l];
+    return v;
+  }
+  __device__ __forceinline__ fp2 y() const {
+    const uint32_t* p = b() + 2 * FP_LIMBS;
+    fp2 v;
+#pragma unroll
+    for (int l = 0; l < FP_LIMBS; ++l) v.c0.l[l] = p[l], v.c1.l[l] = p[FP_LIMBS + l];
+    return v;
+  }
+  __device__ __forceinline__ g2a get() const { return g2a{x(), y()}; }
+};
+
+// G2 (round 6): the runs are summed with fast mixed additions of the fetched
+// row (no call site in the loop; a run's first point is taken as is), and an
+// exceptional addition (the running sum = +-the next point, e.g. a batch
+// holding one signature twice) redoes the thread's range with the generic
+// addition -- the emits are plain stores, so the redo overwrites them.
 template <class Gr>
 __global__ void __launch_bounds__(256, 2) k_msm_bucket_seg(size_t n, size_t T, const uint32_t* __restrict__ offsets,
                                                          const uint32_t* __restrict__ counts,
@@ -266,6 +298,35 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket_seg(size_t n, size_t T, c
   const size_t p0 = t * S;
   if (p0 >= L) return;
   const size_t p1 = p0 + S < L ? p0 + S : L;
+  bool exc = false;
+#ifndef DG_MSM_GENERIC
+  if constexpr (std::is_same<Gr, G2Ops>::value) {
+    uint32_t key = keys[p0];
+    size_t s = p0;
+    g2j acc = g2_infinity();
+    bool first = true;
+#pragma unroll 1
+    for (size_t p = p0; p < p1; ++p) {
+      const uint32_t k = keys[p];
+      if (k != key) {
+        msm_seg_emit<Gr>(key, s, p, t, T, offsets, counts, acc, buckets, part);
+        key = k;
+        s = p;
+        first = true;
+      }
+      const uint32_t* src = aos + ((key >> (MSM_C + 2)) ? n * M::AFF : 0);  // MSMs 2, 3: the signatures
+      const g2_row_fetch f{src + (size_t)list[p] * M::AFF};
+      if (first) {
+        acc = g2_from_affine(f.get());
+        first = false;
+      } else {
+        acc = g2_madd_nx_q(acc, f, exc);
+      }
+    }
+    msm_seg_emit<Gr>(key, s, p1, t, T, offsets, counts, acc, buckets, part);
+    if (!exc) return;
+  }
+#endif
   uint32_t key = keys[p0];
   size_t s = p0;
   typename Gr::jac acc = Gr::inf();

@@ -584,6 +584,38 @@ DG_FN g1j g1_infinity() { return g1j{fp_one(), fp_one(), fp_zero()}; }
 DG_FN bool g1_is_inf(const g1j& a) { return fp_is_zero(a.z); }
 DG_FN g1j g1_neg(const g1j& a) { return g1j{a.x, fp_neg(a.y), a.z}; }
 
+// a limb-wise multiple k a (k a < 2^31 per limb), unnormalized
+DG_FN fp fp_mulk_lz(const fp& a, uint32_t k) {
+  fp r;
+#pragma unroll
+  for (int i = 0; i < FP_LIMBS; ++i) r.l[i] = k * a.l[i];
+  return r;
+}
+
+#ifndef DG_G1_DBL_PLAIN
+// dbl-2009-l (a = 0) with g2_dbl_body's lazy linear steps, in Fp (round 6;
+// 7 products and 3 reductions where the form below, every step reduced, makes
+// 14).  CI in, CI out; bounds in units of p: 2Y lazy (< 4.02p, limbs < 2^29)
+// into the product with Z; X + B normalized (< 3.02p); D/2 = (X + B)^2 - A - C
+// (+32p, < 33.1p) reduced; E = 3A normalized (< 3.03p); X3 = E^2 - 4 (D/2) with
+// 4 (D/2) normalized (< 8.04p); D - X3 = 2 (D/2) + 8p - X3 normalized
+// (< 12.1p) into the product with E (36 p^2); Y3 = E (D - X3) - 8C with 8C
+// normalized (< 8.08p, limbs 8 x 2^28 < 2^31).
+DG_FN g1j g1_dbl_body(const g1j& p) {
+  g1j r;
+  r.z = fp_mul(fp_add_lz(p.y, p.y), p.z);
+  const fp B = fp_sqr(p.y);
+  const fp A = fp_sqr(p.x);
+  const fp XB = fp_norm(fp_add_lz(p.x, B));
+  const fp C = fp_sqr(B);
+  const fp Dh = fp_reduce(fp_norm(fp_sub2_lz(fp_sqr(XB), fp_add_lz(A, C))));
+  const fp E = fp_norm(fp_add_lz(fp_add_lz(A, A), A));
+  r.x = fp_reduce(fp_norm(fp_sub2_lz(fp_sqr(E), fp_norm(fp_mulk_lz(Dh, 4)))));
+  const fp DX = fp_norm(fp_sub_lz(fp_add_lz(Dh, Dh), r.x));
+  r.y = fp_reduce(fp_norm(fp_sub2_lz(fp_mul(E, DX), fp_norm(fp_mulk_lz(C, 8)))));
+  return r;
+}
+#else  // A/B: rounds 1-5, every step reduced
 DG_FN g1j g1_dbl_body(const g1j& p) {
   fp A = fp_sqr(p.x);
   fp B = fp_sqr(p.y);
@@ -597,6 +629,7 @@ DG_FN g1j g1_dbl_body(const g1j& p) {
   r.z = fp_dbl(fp_mul(p.y, p.z));
   return r;
 }
+#endif
 
 DG_NOINL g1j g1_dbl(const g1j& p) { return g1_dbl_body(p); }
 

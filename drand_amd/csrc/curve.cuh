@@ -633,6 +633,36 @@ DG_FN g1j g1_dbl_body(const g1j& p) {
 
 DG_NOINL g1j g1_dbl(const g1j& p) { return g1_dbl_body(p); }
 
+#ifndef DG_G1_ADD_PLAIN
+// add-2007-bl with g2_add_body's lazy linear steps, in Fp (round 6: 4
+// reductions where the every-step-reduced form makes 13; same bounds as the G2
+// form: rr = 2(s2 - s1) and 2h normalized (< 4.02p); X3 = rr^2 - (J + 2V)
+// with the sum normalized (< 6.03p); V - X3 = V + 8p - X3 normalized
+// (< 10.02p) into the product with rr; 2 s1 J = (2 s1) J with 2 s1 lazy;
+// Z1 + Z2 normalized into the square, minus the lazy z1z1 + z2z2).
+DG_FN g1j g1_add_body(const g1j& p, const g1j& q) {
+  const fp z1z1 = fp_sqr(p.z), z2z2 = fp_sqr(q.z);
+  const fp u1 = fp_mul(p.x, z2z2), u2 = fp_mul(q.x, z1z1);
+  const fp s1 = fp_mul(fp_mul(p.y, q.z), z2z2), s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  const fp h = fp_sub(u2, u1);
+  const fp rh = fp_sub(s2, s1);
+  const bool p_inf = g1_is_inf(p), q_inf = g1_is_inf(q);
+  const bool h0 = fp_is_zero(h), r0 = fp_is_zero(rh);
+  const fp rr = fp_norm(fp_add_lz(rh, rh));
+  const fp i = fp_sqr(fp_norm(fp_add_lz(h, h)));
+  const fp j = fp_mul(h, i);
+  const fp v = fp_mul(u1, i);
+  g1j r;
+  r.x = fp_reduce(fp_norm(fp_sub2_lz(fp_sqr(rr), fp_norm(fp_add_lz(fp_add_lz(j, v), v)))));
+  const fp VX = fp_norm(fp_sub_lz(v, r.x));
+  r.y = fp_sub(fp_mul(rr, VX), fp_mul(fp_add_lz(s1, s1), j));
+  r.z = fp_mul(fp_norm(fp_sub2_lz(fp_sqr(fp_norm(fp_add_lz(p.z, q.z))), fp_add_lz(z1z1, z2z2))), h);  // 66.6 p^2
+  if (h0 && !p_inf && !q_inf) r = r0 ? g1_dbl(p) : g1_infinity();
+  if (p_inf) r = q;
+  if (q_inf) r = p;
+  return r;
+}
+#else  // A/B: rounds 1-5, every step reduced
 DG_FN g1j g1_add_body(const g1j& p, const g1j& q) {
   fp z1z1 = fp_sqr(p.z), z2z2 = fp_sqr(q.z);
   fp u1 = fp_mul(p.x, z2z2), u2 = fp_mul(q.x, z1z1);
@@ -653,11 +683,39 @@ DG_FN g1j g1_add_body(const g1j& p, const g1j& q) {
   if (q_inf) r = p;
   return r;
 }
+#endif
 
 DG_NOINL g1j g1_add(const g1j& p, const g1j& q) { return g1_add_body(p, q); }
 
 // Mixed addition p + q, q affine (madd-2007-bl, a = 0: 7M + 4S), exceptional
 // cases resolved (p == q -> dbl, p == -q -> infinity, p infinity -> q).
+#ifndef DG_G1_ADD_PLAIN
+// madd-2007-bl with g2_add_affine_body's lazy linear steps, in Fp (4
+// reductions where the every-step-reduced form makes 12; I = 4 HH normalized,
+// < 4.04p).
+DG_FN g1j g1_add_affine_body(const g1j& p, const g1a& q) {
+  const fp z1z1 = fp_sqr(p.z);
+  const fp u2 = fp_mul(q.x, z1z1);
+  const fp s2 = fp_mul(fp_mul(q.y, p.z), z1z1);
+  const fp h = fp_sub(u2, p.x);
+  const fp rh = fp_sub(s2, p.y);
+  const bool p_inf = g1_is_inf(p);
+  const bool h0 = fp_is_zero(h), r0 = fp_is_zero(rh);
+  const fp rr = fp_norm(fp_add_lz(rh, rh));
+  const fp hh = fp_sqr(h);
+  const fp i = fp_norm(fp_mulk_lz(hh, 4));
+  const fp j = fp_mul(h, i);
+  const fp v = fp_mul(p.x, i);
+  g1j r;
+  r.x = fp_reduce(fp_norm(fp_sub2_lz(fp_sqr(rr), fp_norm(fp_add_lz(fp_add_lz(j, v), v)))));
+  const fp VX = fp_norm(fp_sub_lz(v, r.x));
+  r.y = fp_sub(fp_mul(rr, VX), fp_mul(fp_add_lz(p.y, p.y), j));
+  r.z = fp_reduce(fp_norm(fp_sub2_lz(fp_sqr(fp_norm(fp_add_lz(p.z, h))), fp_add_lz(z1z1, hh))));
+  if (h0 && !p_inf) r = r0 ? g1_dbl(g1j{q.x, q.y, fp_one()}) : g1_infinity();
+  if (p_inf) r = g1j{q.x, q.y, fp_one()};
+  return r;
+}
+#else
 DG_FN g1j g1_add_affine_body(const g1j& p, const g1a& q) {
   const fp z1z1 = fp_sqr(p.z);
   const fp u2 = fp_mul(q.x, z1z1);
@@ -678,6 +736,7 @@ DG_FN g1j g1_add_affine_body(const g1j& p, const g1a& q) {
   if (p_inf) r = g1j{q.x, q.y, fp_one()};
   return r;
 }
+#endif
 
 DG_FN g1j g1_cmov(const g1j& a, const g1j& b, bool take_b) {
   return g1j{fp_cmov(a.x, b.x, take_b), fp_cmov(a.y, b.y, take_b), fp_cmov(a.z, b.z, take_b)};

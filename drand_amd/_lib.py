@@ -18,7 +18,7 @@ AB_LIB_PATH = os.path.join(_HERE, "libdrand_gpu_ab.so")
 AB_KNOBS = frozenset({"DGPU_DEC_OVERLAP", "DGPU_MSM_SEG", "DGPU_LANE_SLICES", "DGPU_KB_NORM", "DGPU_RLC_DESCENT_STEP",
                       "DGPU_RLC_LOCALIZE", "DGPU_G1_LINES", "DGPU_SUBGROUP", "DGPU_RECOVER", "DGPU_RECOVER_ROWS",
                       "DGPU_KB_INV_CHAIN", "DGPU_KB_TEST_FLAG", "DGPU_TEST_ALLOC_CAP", "DGPU_STAGE",
-                      "DGPU_ENG_XW", "DGPU_TEST_STAGE_ONLY", "DGPU_LINES_WAVE", "DGPU_KB_PAIR"})
+                      "DGPU_ENG_XW", "DGPU_TEST_STAGE_ONLY", "DGPU_LINES_WAVE", "DGPU_KB_PAIR", "DGPU_TEST_FORCE_EXC"})
 
 DGPU_OK = 0
 DGPU_EINVAL = -1

@@ -1903,6 +1903,16 @@ int dgpu_open(int device, dgpu_ctx** out) {
   if (tso && !strcmp(tso, "1")) c->test_stage_only = true;
   const char* tac = getenv("DGPU_TEST_ALLOC_CAP");
   if (tac && atol(tac) >= 0) g_test_alloc_cap = (size_t)atol(tac);
+  {  // the fast group-law paths' generic redo on every item (kernels.cuh DG_FORCE_EXC); written at every
+     // dgpu_open of this build, so a context opened without the knob resets it
+    const char* fev2 = getenv("DGPU_TEST_FORCE_EXC");
+    const int force = fev2 && !strcmp(fev2, "1") ? 1 : 0;
+    const hipError_t fe = hipMemcpyToSymbol(HIP_SYMBOL(g_dg_force_exc), &force, sizeof(force));
+    if (fe != hipSuccess) {
+      delete c;
+      return set_err(DGPU_EDEVICE, "DGPU_TEST_FORCE_EXC: %s", hipGetErrorString(fe));
+    }
+  }
 #endif
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking);

@@ -56,6 +56,17 @@ __device__ __forceinline__ g2j ld_g2j(const uint32_t* base, size_t n, size_t i) 
   return p;
 }
 
+// Test hook of the A/B build (DGPU_TEST_FORCE_EXC=1 at dgpu_open): the fast
+// group-law paths (cofactor ladder, membership ladder, MSM additions) take
+// their generic redo as if an exceptional addition had occurred, so the redo
+// code runs on every item.  Always false in the shipped build.
+#ifdef DG_AB_KNOBS
+__device__ int g_dg_force_exc = 0;
+#define DG_FORCE_EXC (g_dg_force_exc != 0)
+#else
+#define DG_FORCE_EXC false
+#endif
+
 // per-round status codes carried between kernels (also the public `reason`)
 enum : uint8_t {
   ST_OK = 0,
@@ -248,7 +259,7 @@ __device__ __forceinline__ bool g2_in_subgroup_stored(const g2a& p, uint32_t* pt
   bool exc = false;
   const g2a_soa_fetch f{pts, n, i};
   const bool in = g2_in_subgroup_ladder(p, f, exc);
-  return exc ? g2_in_subgroup(g2_from_affine(f.get())) : in;
+  return exc || DG_FORCE_EXC ? g2_in_subgroup(g2_from_affine(f.get())) : in;
 }
 
 // Point slots of g2_clear_cofactor_stash in the round's own SoA words: 0, 1 =
@@ -316,7 +327,7 @@ __global__ void __launch_bounds__(256, DG_FINISH_OCC) k_h2c_finish(size_t n, uin
   h2c_finish_stash st{q, h_out, z_out, n, i};
   bool exc = false;
   g2j h = g2_clear_cofactor_stash(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i), st, exc);
-  if (exc) h = g2_clear_cofactor(st.get(0));
+  if (exc || DG_FORCE_EXC) h = g2_clear_cofactor(st.get(0));
   st.put(2, h);
 }
 

@@ -495,7 +495,7 @@ __global__ void __launch_bounds__(256, 2) k_recover_msm_aff(size_t n_rounds, int
 #else
   exc = true;
 #endif
-  if (exc) {  // the generic mixed addition (rounds 2-5): exceptional cases resolved
+  if (exc || DG_FORCE_EXC) {  // the generic mixed addition (rounds 2-5): exceptional cases resolved
     acc = g2_infinity();
 #pragma unroll 1
     for (int w = 16; w >= 0; --w) {

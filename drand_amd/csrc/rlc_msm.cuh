@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(256, 2) k_msm_bucket_seg(size_t n, size_t T, c
       }
     }
     msm_seg_emit<Gr>(key, s, p1, t, T, offsets, counts, acc, buckets, part);
-    if (!exc) return;
+    if (!exc && !DG_FORCE_EXC) return;
   }
 #endif
   uint32_t key = keys[p0];

@@ -247,3 +247,39 @@ def test_gpu_recover_cancelling_partials_rejected():
     got, valid = grp.recover_batch([msg, msg], [parts[:3], parts], statuses=True)
     assert got == [None, sig]
     assert valid == [[False, False, True], [False, False, True, True, True]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("statuses", [True, False])
+def test_gpu_recover_generic_redo_paths_match_fixtures(name, statuses):
+    """The fast group-law paths' generic redo, forced on every item (A/B
+    build test hook DGPU_TEST_FORCE_EXC=1): the partials' membership test
+    (g2_in_subgroup in place of the ladder) and the recovery MSM's windows
+    (the generic mixed addition redoing each slice) -- recovered bytes and
+    failures equal the fixture, per-partial statuses and batched check."""
+    from conftest import open_ctx
+    from drand_amd import _lib
+    from drand_amd.threshold import pack_partials, unpack_recovered
+    import numpy as np
+    g = load_golden(name)
+    commits = [bytes.fromhex(c) for c in g["commits"]]
+    msgs = [bytes.fromhex(c["msg"]) for c in g["cases"]]
+    parts = [[bytes.fromhex(p) for p in c["partials"]] for c in g["cases"]]
+    ctx = open_ctx({"DGPU_TEST_FORCE_EXC": "1"})
+    try:
+        buf = np.frombuffer(b"".join(commits), dtype=np.uint8).copy()
+        _lib.check(ctx.lib.dgpu_set_group(ctx.handle, len(commits), g["n"], _lib.ptr(buf)))
+        mb, pb, plen, m, stride = pack_partials(msgs, parts)
+        nr = len(msgs)
+        out = np.zeros(nr * 96, dtype=np.uint8)
+        ok = np.zeros((nr + 7) // 8, dtype=np.uint8)
+        pv = np.zeros(nr * m, dtype=np.uint8) if statuses else None
+        _lib.check(ctx.lib.dgpu_recover_batch(ctx.handle, nr, _lib.ptr(mb), m, _lib.ptr(pb), stride, _lib.ptr(plen),
+                                              _lib.ptr(out), _lib.ptr(ok), _lib.ptr(pv)))
+        sigs, valid = unpack_recovered(out, ok, pv, parts, m)
+    finally:
+        ctx.close()
+    assert [s.hex() if s else None for s in sigs] == [c["recovered"] for c in g["cases"]]
+    if statuses:
+        assert [v for v in valid] == [c["valid"] for c in g["cases"]]

@@ -62,17 +62,19 @@ struct lt_pt_val {
 // Y + Z need c1 < 7.99p for their a0 - a1 and see products < 300 p^2; the
 // addition step's products and fp2_sub minuends take any normalized operand
 // -- and lt_pair_p reduces the final T (the membership test compares it).
-// Two reductions fewer per doubling.
+// Two reductions fewer per doubling (A/B: -DDG_LINES_DBL_C1R).
 DG_FN fp2 lt_fp2_mul_c1r(const fp2& a, const fp2& b) {
   const fp t0 = fp_mul(a.c0, b.c0);
   const fp t1 = fp_mul(a.c1, b.c1);
   const fp t2 = fp_mul(fp_add_lz(a.c0, a.c1), fp_add_lz(b.c0, b.c1));
   return fp2{fp_norm(fp_sub_lz(t0, t1)), fp_reduce(fp_norm(fp_sub2_lz(t2, fp_add_lz(t0, t1))))};
 }
-#ifdef DG_LINES_DBL_PLAIN  // A/B: rounds 3-5, both outputs reduced
-#define LT_MUL_OUT fp2_mul
-#else
+// Measured without gain (r06s: eng_lines 128.3 vs 127.6 ms per 2M, noise);
+// the A/B build variant -DDG_LINES_DBL_C1R keeps it, both outputs reduced ship.
+#ifdef DG_LINES_DBL_C1R
 #define LT_MUL_OUT lt_fp2_mul_c1r
+#else
+#define LT_MUL_OUT fp2_mul
 #endif
 
 template <class PT, class Emit>

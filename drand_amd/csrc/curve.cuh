@@ -513,7 +513,7 @@ DG_FN g2j g2_clear_cofactor_inl(const g2j& p) {
 
 // Clear cofactor: h_eff * P = [x^2 - x - 1] P + [x - 1] psi(P) + psi^2(2P)
 // (RFC 9380 appendix G.3 sequence).
-DG_NOINL g2j g2_clear_cofactor(const g2j& p) {
+DG_NOINL g2j g2_clear_cofactor_generic(const g2j& p) {
   g2j t1 = g2_mul_x(p);
   g2j t2 = g2_psi(p);
   g2j t3 = g2_psi2(g2_dbl(p));
@@ -523,6 +523,42 @@ DG_NOINL g2j g2_clear_cofactor(const g2j& p) {
   t3 = g2_add(t3, t2);
   t3 = g2_add(t3, g2_neg(t1));
   return g2_add(t3, g2_neg(p));
+}
+
+// [|x|] p in registers on the ladder's structure (lazy doublings, fast
+// additions; exc as g2_add_nx).
+DG_FN g2j g2_mul_absx_fast(const g2j& p, bool& exc) {
+  g2j r = p;
+#pragma unroll 1
+  for (int a = 0; a < 5; ++a) {
+    const int nd = a == 0 ? 1 : a == 1 ? 2 : a == 2 ? 3 : a == 3 ? 9 : 32;
+#pragma unroll 1
+    for (int d = 0; d < nd; ++d) r = G2_LADDER_DBL(r);
+    r = g2_add_nx(G2_LADDER_ZRED(r), p, exc);
+  }
+#pragma unroll 1
+  for (int d = 0; d < 16; ++d) r = G2_LADDER_DBL(r);
+  return G2_LADDER_ZRED(r);
+}
+
+// h_eff P (the sequence above) for the one-off callers -- the RLC node
+// checks (k_rlc_prep), the hash's exceptional redo, hash_to_g2: the ladder
+// form in registers (round 6), the generic form when an addition is
+// exceptional or P is the identity.
+DG_NOINL g2j g2_clear_cofactor(const g2j& p) {
+#ifndef DG_COFACTOR_GENERIC
+  bool exc = g2_is_inf(p);
+  const g2j nt1 = g2_mul_absx_fast(p, exc);  // -[x]P
+  const g2j t2 = g2_psi_body(p);
+  g2j t3 = g2_add_nx(g2_psi2_body(g2_dbl_body(p)), g2_neg(t2), exc);
+  const g2j u = g2_add_nx(g2_neg(nt1), t2, exc);
+  const g2j nt2 = g2_mul_absx_fast(u, exc);  // -[x]U
+  t3 = g2_add_nx(t3, g2_neg(nt2), exc);
+  t3 = g2_add_nx(t3, nt1, exc);
+  t3 = g2_add_nx(t3, g2_neg(p), exc);
+  if (!exc) return t3;
+#endif
+  return g2_clear_cofactor_generic(p);
 }
 
 // ---------------------------------------------------------------- ZCash G2 codec

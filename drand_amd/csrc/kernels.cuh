@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(256, DG_FINISH_OCC) k_h2c_finish(size_t n, uin
   h2c_finish_stash st{q, h_out, z_out, n, i};
   bool exc = false;
   g2j h = g2_clear_cofactor_stash(ld_g2j(q, n, i), ld_g2j(q + G2J_WORDS * n, n, i), st, exc);
-  if (exc || DG_FORCE_EXC) h = g2_clear_cofactor(st.get(0));
+  if (exc || DG_FORCE_EXC) h = DG_FORCE_EXC ? g2_clear_cofactor_generic(st.get(0)) : g2_clear_cofactor(st.get(0));
   st.put(2, h);
 }
 

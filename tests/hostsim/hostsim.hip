@@ -382,6 +382,8 @@ void hs_hash_to_g2(const uint8_t* msg32, uint8_t* out96) {
 // k_h2c_finish's sequence (g2_clear_cofactor_stash, the generic
 // g2_clear_cofactor from slot 0 when it flags an exceptional addition) on
 // Q0, Q1 = SSWU(u0), SSWU(u1) of msg, with Q1 replaced by Q0 (mode 1) or -Q0
+// (compared with g2_clear_cofactor_generic; hs_hash_to_g2 runs the register
+// ladder form of g2_clear_cofactor)
 // (mode 2, P = O) -- H compressed to out96 (the generic path's to gen96);
 // returns the exceptional flag.
 int hs_h2c_finish_check(const uint8_t* msg32, int mode, uint8_t* out96, uint8_t* gen96) {
@@ -397,7 +399,7 @@ int hs_h2c_finish_check(const uint8_t* msg32, int mode, uint8_t* out96, uint8_t*
   bool exc = false;
   g2j h = g2_clear_cofactor_stash(q0, q1, st, exc);
   if (exc) h = g2_clear_cofactor(st.get(0));
-  const g2j g = g2_clear_cofactor(g2_add(q0, q1));
+  const g2j g = g2_clear_cofactor_generic(g2_add(q0, q1));  // the round-5 form, every case resolved
   bool inf = g2_is_inf(h);
   g2_compress(out96, inf ? g2a{fp2_zero(), fp2_zero()} : g2_to_affine(h), inf);
   inf = g2_is_inf(g);
